@@ -1,0 +1,178 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).  Test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+_LIB = None
+
+OP_PNP, OP_PNP_IE, OP_PB, OP_DIFF, OP_DIFF_IE, OP_POISSON = range(6)
+PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI = range(4)
+
+
+class OrcMesh(C.Structure):
+    _fields_ = [("nv", C.c_int), ("xy", C.c_void_p), ("nt", C.c_int), ("tri", C.c_void_p),
+                ("nb", C.c_int), ("bseg", C.c_void_p), ("bgroup", C.c_void_p)]
+
+
+class OrcSurface(C.Structure):
+    _fields_ = [("cb", C.c_int), ("cflux", C.c_double), ("cpot", C.c_double),
+                ("pb", C.c_int), ("pflux", C.c_double), ("pconc", C.c_double),
+                ("mb", C.c_int), ("mflux", C.c_double), ("mconc", C.c_double)]
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("l_b", C.c_double), ("c0", C.c_double), ("tau", C.c_double), ("pi", C.c_double),
+                ("cylindrical", C.c_int), ("nsurf", C.c_int), ("surf", C.c_void_p)]
+
+
+class OrcCsr(C.Structure):
+    _fields_ = [("n", C.c_int), ("nnz", C.c_int), ("rowptr", C.POINTER(C.c_int)),
+                ("col", C.POINTER(C.c_int)), ("val", C.POINTER(C.c_double))]
+
+
+class OrcOperator(C.Structure):
+    _fields_ = [("kind", C.c_int), ("flux", C.c_void_p), ("mask", C.c_void_p), ("dt", C.c_double),
+                ("z", C.c_double), ("phi", C.c_void_p), ("cp", C.c_void_p), ("cm", C.c_void_p),
+                ("x_old", C.c_void_p)]
+
+
+class OrcSolveResult(C.Structure):
+    _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("it_half", C.c_double),
+                ("reduction", C.c_double), ("defect0", C.c_double), ("defect", C.c_double),
+                ("breakdown", C.c_int)]
+
+
+class OrcNewtonOpts(C.Structure):
+    _fields_ = [("reduction", C.c_double), ("abs_limit", C.c_double),
+                ("min_linear_reduction", C.c_double), ("maxit", C.c_int),
+                ("line_search_maxit", C.c_int), ("reassemble_threshold_zero", C.c_int),
+                ("linear_maxit", C.c_int), ("prec", C.c_int), ("fd_jacobian", C.c_int)]
+
+
+class OrcNewtonResult(C.Structure):
+    _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("linear_iterations", C.c_int),
+                ("status", C.c_int), ("first_defect", C.c_double), ("defect", C.c_double)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        so = os.path.join(ORACLE_DIR, "liboracle.so")
+        src = os.path.join(ORACLE_DIR, "pnp_oracle.c")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        _LIB = C.CDLL(so)
+        _LIB.orc_operator_nfields.restype = C.c_int
+    return _LIB
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class Problem:
+    """Holds the ctypes views of one mesh + parameter set for the oracle."""
+
+    def __init__(self, mesh, surfaces, l_b=1.0, c0=0.06, tau=1.0, cylindrical=0, pi=3.1415):
+        self.mesh = mesh
+        self.xy = np.ascontiguousarray(mesh.xy, dtype=np.float64)
+        self.tri = np.ascontiguousarray(mesh.tri, dtype=np.int32)
+        self.bseg = np.ascontiguousarray(mesh.bseg, dtype=np.int32)
+        self.bgroup = np.ascontiguousarray(mesh.bgroup, dtype=np.int32)
+        self.m = OrcMesh(mesh.nv, self.xy.ctypes.data, mesh.nt, self.tri.ctypes.data, mesh.nb,
+                         self.bseg.ctypes.data, self.bgroup.ctypes.data)
+        arr = (OrcSurface * len(surfaces))()
+        for i, s in enumerate(surfaces):
+            arr[i] = OrcSurface(s.cb, s.cflux, s.cpot, s.pb, s.pflux, s.pconc, s.mb, s.mflux,
+                                s.mconc)
+        self._surf = arr
+        self.p = OrcParams(l_b, c0, tau, pi, cylindrical, len(surfaces),
+                           C.cast(arr, C.c_void_p))
+        self.nv = mesh.nv
+
+    # setup -----------------------------------------------------------------------------
+    def mask(self, nfields):
+        out = np.zeros(nfields * self.nv, dtype=np.uint8)
+        lib().orc_dirichlet_mask(C.byref(self.m), C.byref(self.p), nfields, _p(out))
+        return out
+
+    def flux(self):
+        out = np.zeros(3 * self.mesh.nb, dtype=np.float64)
+        lib().orc_flux_container(C.byref(self.m), C.byref(self.p), _p(out))
+        return out
+
+    def initial_state(self, phi_pb):
+        out = np.zeros(3 * self.nv, dtype=np.float64)
+        phi = np.ascontiguousarray(phi_pb, dtype=np.float64)
+        lib().orc_initial_state(C.byref(self.m), C.byref(self.p), _p(phi), _p(out))
+        return out
+
+    # operators ---------------------------------------------------------------------------
+    def operator(self, kind, flux=None, mask=None, dt=0.0, z=0.0, phi=None, cp=None, cm=None,
+                 x_old=None):
+        keep = [a for a in (flux, mask, phi, cp, cm, x_old) if a is not None]
+        ad = lambda a: None if a is None else a.ctypes.data
+        op = OrcOperator(kind, ad(flux), ad(mask), dt, z, ad(phi), ad(cp), ad(cm), ad(x_old))
+        op._keep = keep
+        return op
+
+    def nfields(self, op):
+        return lib().orc_operator_nfields(C.byref(op))
+
+    def residual(self, op, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        r = np.zeros(self.nfields(op) * self.nv, dtype=np.float64)
+        lib().orc_op_residual(C.byref(self.m), C.byref(self.p), C.byref(op), _p(x), _p(r))
+        return r
+
+    def jacobian(self, op, x, fd=False):
+        """Returns a scipy.sparse.csr_matrix (copy) of the operator Jacobian."""
+        import scipy.sparse as sp
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        A = OrcCsr()
+        L = lib()
+        L.orc_csr_pattern(C.byref(self.m), self.nfields(op), C.byref(A))
+        L.orc_op_jacobian(C.byref(self.m), C.byref(self.p), C.byref(op), _p(x), int(fd),
+                          C.byref(A))
+        n, nnz = A.n, A.nnz
+        rp = np.ctypeslib.as_array(A.rowptr, shape=(n + 1,)).copy()
+        col = np.ctypeslib.as_array(A.col, shape=(nnz,)).copy()
+        val = np.ctypeslib.as_array(A.val, shape=(nnz,)).copy()
+        L.orc_csr_free(C.byref(A))
+        return sp.csr_matrix((val, col, rp), shape=(n, n))
+
+    def newton(self, op, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
+               line_search_maxit=500, linear_maxit=20000, prec=PREC_NONE, fd=False):
+        u = np.ascontiguousarray(u, dtype=np.float64).copy()
+        o = OrcNewtonOpts(reduction, abs_limit, min_linear_reduction, maxit, line_search_maxit, 1,
+                          linear_maxit, prec, int(fd))
+        res = OrcNewtonResult()
+        lib().orc_newton(C.byref(self.m), C.byref(self.p), C.byref(op), _p(u), C.byref(o),
+                         C.byref(res))
+        return u, res
+
+
+def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
+    """ISTL-semantics BiCGStab on a scipy CSR matrix (sorted indices)."""
+    A = A.tocsr()
+    A.sort_indices()
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    col = np.ascontiguousarray(A.indices, dtype=np.int32)
+    val = np.ascontiguousarray(A.data, dtype=np.float64)
+    M = OrcCsr(A.shape[0], A.nnz, rp.ctypes.data_as(C.POINTER(C.c_int)),
+               col.ctypes.data_as(C.POINTER(C.c_int)), val.ctypes.data_as(C.POINTER(C.c_double)))
+    x = np.zeros(A.shape[0]) if x0 is None else np.array(x0, dtype=np.float64)
+    bb = np.array(b, dtype=np.float64)
+    res = OrcSolveResult()
+    lib().orc_bicgstab(C.byref(M), prec, C.c_double(reduction), maxit, _p(x), _p(bb),
+                       C.byref(res))
+    return x, res

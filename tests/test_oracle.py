@@ -1,0 +1,203 @@
+"""CPU tests: pin the C oracle (oracle/pnp_oracle.c) against the committed golden fixtures
+(independent numpy restatement, tests/golden/make_golden.py) and against the reference's only
+known-answer data (Gouy-Chapman, test/one_wall_dh/one_wall.gp:4-12)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import meshio
+import oracle_py as O
+from conftest import DATA
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KINDS = {"pnp": O.OP_PNP, "pnp_ie": O.OP_PNP_IE, "pb": O.OP_PB, "diff": O.OP_DIFF,
+         "poisson": O.OP_POISSON}
+
+
+def load(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    m = meshio.Mesh(z["xy"], z["tri"].astype(np.int32), z["bseg"].astype(np.int32),
+                    z["bgroup"].astype(np.int32))
+    surfs = [meshio.Surface(int(s[0]), s[1], s[2], int(s[3]), s[4], s[5], int(s[6]), s[7], s[8])
+             for s in z["surfaces"]]
+    l_b, c0, tau, cyl, pi = z["params"]
+    P = O.Problem(m, surfs, l_b=l_b, c0=c0, tau=tau, cylindrical=int(cyl), pi=pi)
+    return z, m, P
+
+
+def build_op(z, P, kind):
+    flux = P.flux()
+    mask = np.ascontiguousarray(z[kind + "_mask"])
+    kw = {}
+    if kind == "pnp_ie":
+        kw = dict(dt=float(z["params"][2]), x_old=np.ascontiguousarray(z["pnp_ie_x_old"]))
+    if kind == "diff":
+        kw = dict(z=-1.0, phi=np.ascontiguousarray(z["diff_phi"]))
+    if kind == "poisson":
+        kw = dict(cp=np.ascontiguousarray(z["poisson_cp"]),
+                  cm=np.ascontiguousarray(z["poisson_cm"]))
+    return P.operator(KINDS[kind], flux=flux, mask=mask, **kw)
+
+
+def csr(z, key):
+    n = z[key + "_indptr"].shape[0] - 1
+    return sp.csr_matrix((z[key + "_data"], z[key + "_indices"], z[key + "_indptr"]),
+                         shape=(n, n))
+
+
+CASES = [("cylinder_k0", "pnp"), ("cylinder_k0", "pb"), ("pore_small_k0", "pnp"),
+         ("pore_small_k0", "pnp_ie"), ("pore_small_k0", "pb"), ("pore_small_k0", "diff"),
+         ("pore_small_k0", "poisson"), ("pore_pnp_k0", "pnp"), ("pore_pnp_k0", "pb"),
+         ("sphere_k0", "pb"), ("one_wall_k1", "pnp"), ("one_wall_k1", "pb")]
+
+
+@pytest.mark.parametrize("name,kind", CASES)
+def test_residual_matches_golden(name, kind):
+    z, m, P = load(name)
+    op = build_op(z, P, kind)
+    r = P.residual(op, z[kind + "_x"])
+    ref = z[kind + "_r"]
+    # residual tolerance: ||dr||_inf / ||r||_inf <= 1e-12
+    assert np.max(np.abs(r - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("name,kind", [c for c in CASES if c[0] != "pore_pnp_k0"])
+def test_jacobian_matches_golden(name, kind):
+    z, m, P = load(name)
+    op = build_op(z, P, kind)
+    x = z[kind + "_x"]
+    J = P.jacobian(op, x, fd=False)
+    Jref = csr(z, kind + "_J")
+    scale = abs(Jref).max()
+    assert abs(J - Jref).max() <= 1e-12 * scale          # analytic vs analytic
+    Jfd = P.jacobian(op, x, fd=True)
+    Jfd_ref = csr(z, kind + "_Jfd")
+    # two FD evaluations differ by rounding/eps: (eps_mach*|r|/delta)
+    assert abs(Jfd - Jfd_ref).max() <= 1e-6 * scale
+    # analytic vs reference-faithful FD: entrywise relative <= 1e-5 where |A_ij| > 1e-12 ||A||
+    D = (J - Jfd).tocoo()
+    Jd = J.tocsr()
+    big = np.abs(np.asarray(Jd[D.row, D.col]).ravel()) > 1e-12 * scale
+    rel = np.abs(D.data) / np.maximum(np.abs(np.asarray(Jd[D.row, D.col]).ravel()), 1e-300)
+    assert np.all(rel[big] <= 1e-5) or np.max(np.abs(D.data)) <= 1e-5 * scale
+
+
+def test_csr_pattern_is_full_volume_pattern():
+    z, m, P = load("cylinder_k0")
+    op = build_op(z, P, "pnp")
+    J = P.jacobian(op, z["pnp_x"])
+    # 9 * (V + 2E) entries: V + 2E = sum of (degree+1)
+    edges = set()
+    for t in m.tri:
+        for a, b in ((0, 1), (1, 2), (0, 2)):
+            edges.add(tuple(sorted((int(t[a]), int(t[b])))))
+    assert J.nnz == 9 * (m.nv + 2 * len(edges))
+
+
+@pytest.mark.parametrize("name", ["cylinder_k0", "pore_small_k0"])
+def test_newton_pnp_matches_golden(name):
+    z, m, P = load(name)
+    mask = P.mask(3)
+    np.testing.assert_array_equal(mask, z["pnp_mask"])
+    op = P.operator(O.OP_PNP, flux=P.flux(), mask=mask)
+    u, res = P.newton(op, z["newton_pnp_x0"], prec=O.PREC_ILU0)
+    assert res.converged == 1 and res.status == 0
+    ref = z["newton_pnp_u"]
+    assert np.max(np.abs(u - ref)) <= 1e-6 * np.max(np.abs(ref))
+    assert res.defect <= 1e-9 * res.first_defect or res.defect < 1e-12
+
+
+@pytest.mark.parametrize("name", ["pore_small_k0", "sphere_k0", "one_wall_k1"])
+def test_newton_pb_matches_golden(name):
+    z, m, P = load(name)
+    op = P.operator(O.OP_PB, flux=P.flux(), mask=P.mask(1))
+    u, res = P.newton(op, np.zeros(m.nv), prec=O.PREC_ILU0)
+    assert res.converged == 1
+    ref = z["newton_pb_u"]
+    assert np.max(np.abs(u - ref)) <= 1e-6 * max(np.max(np.abs(ref)), 1e-12)
+
+
+def test_bicgstab_preconditioners_agree():
+    z, m, P = load("pore_small_k0")
+    op = build_op(z, P, "pnp")
+    J = P.jacobian(op, z["pnp_x"])
+    b = np.ones(J.shape[0])
+    sols = {}
+    for prec in (O.PREC_ILU0, O.PREC_SSOR, O.PREC_JACOBI):
+        x, res = O.bicgstab(J, b, prec=prec, reduction=1e-12)
+        assert res.converged
+        assert np.linalg.norm(J @ x - b) <= 1e-10 * np.linalg.norm(b)
+        sols[prec] = x
+    # ISTL counts half steps: iterations = ceil(it)
+    x, res = O.bicgstab(J, b, prec=O.PREC_ILU0, reduction=1e-12)
+    assert res.iterations == int(np.ceil(res.it_half))
+
+
+def test_bicgstab_trivial_rhs_returns_immediately():
+    A = sp.identity(10, format="csr")
+    x, res = O.bicgstab(A, np.zeros(10))
+    assert res.converged and res.iterations == 0
+
+
+def test_pnp_nonprec_hits_maxit_like_reference():
+    """Stationary PNP with NOPREC (src/stationary_pnp_from_pb.hh:329-331) on the cylindrical
+    pore mesh does not converge within a small iteration cap; Newton reports the linear-solver
+    failure (PDELab NewtonLinearSolverError), exactly the status the product must report."""
+    z, m, P = load("pore_pnp_k0")
+    op = P.operator(O.OP_PNP, flux=P.flux(), mask=P.mask(3))
+    _, res = P.newton(op, z["pnp_x"], prec=O.PREC_NONE, linear_maxit=50)
+    assert res.status == -3
+
+
+def test_gouy_chapman_known_answer():
+    """Planar PB against the reference's analytic curve family (test/one_wall_dh/one_wall.gp:
+    4-12, Gouy-Chapman): -phi'' + kappa^2 sinh(phi) = 0, phi'(0) = j, phi(L) = 0.  The 1-D
+    solution is computed to high accuracy with scipy.solve_bvp on the same finite slab; the
+    semi-infinite Gouy-Chapman closed form is checked against it as well."""
+    from scipy.integrate import solve_bvp
+    cfg = meshio.read_config(os.path.join(DATA, "one_wall_dh", "one_wall.cfg"))
+    m = meshio.refine(meshio.read_gmsh(cfg.meshfile), 3)
+    s = cfg.system
+    P = O.Problem(m, cfg.surfaces, l_b=s["l_b"], c0=s["c0"], tau=s["tau"],
+                  cylindrical=int(s["cylindrical"]))
+    op = P.operator(O.OP_PB, flux=P.flux(), mask=P.mask(1))
+    u, res = P.newton(op, np.zeros(m.nv), prec=O.PREC_ILU0, reduction=1e-12)
+    assert res.converged
+    k2 = 8 * 3.1415 * s["l_b"] * s["c0"]
+    j = cfg.surfaces[0].cflux
+    L = m.xy[:, 0].max()
+    sol = solve_bvp(lambda x, y: np.vstack([y[1], k2 * np.sinh(y[0])]),
+                    lambda ya, yb: np.array([ya[1] - j, yb[0]]),
+                    np.linspace(0, L, 200), np.zeros((2, 200)), tol=1e-10, max_nodes=100000)
+    assert sol.success
+    exact = sol.sol(m.xy[:, 0])[0]
+    err = np.max(np.abs(u - exact))
+    assert err <= 2e-3 * np.max(np.abs(exact))
+    # semi-infinite Gouy-Chapman closed form (one_wall.gp:9-10) near the wall
+    kappa = np.sqrt(k2)
+    phi0 = -2 * np.arcsinh(j / (2 * kappa))
+    g = np.tanh(phi0 / 4)
+    xs = np.linspace(0, 2, 5)
+    gc = 2 * np.log((1 + g * np.exp(-kappa * xs)) / (1 - g * np.exp(-kappa * xs)))
+    assert np.max(np.abs(gc - sol.sol(xs)[0])) <= 0.02 * abs(phi0)
+
+
+def test_initial_state_dirichlet_values():
+    """BCExtension (src/dirichlet_bc.hh:54-123) puts the configured Dirichlet values on the
+    constrained vertices it finds, and the Boltzmann extension elsewhere."""
+    cfg = meshio.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    m = meshio.read_gmsh(cfg.meshfile)
+    s = cfg.system
+    P = O.Problem(m, cfg.surfaces, l_b=s["l_b"], c0=s["c0"], tau=s["tau"],
+                  cylindrical=int(s["cylindrical"]))
+    rng = np.random.default_rng(1)
+    phi = rng.uniform(-0.5, 0.5, m.nv)
+    x0 = P.initial_state(phi)
+    mask = P.mask(3)
+    outflow = m.bseg[m.bgroup == 4].ravel()
+    assert np.all(x0[outflow] == 24.1)
+    free = mask[:m.nv] == 0
+    np.testing.assert_allclose(x0[m.nv:2 * m.nv][free], 0.06 * np.exp(-phi[free]), rtol=1e-15)
+    np.testing.assert_allclose(x0[2 * m.nv:][free], 0.06 * np.exp(phi[free]), rtol=1e-15)
