@@ -1,0 +1,284 @@
+#!/usr/bin/env python
+"""Benchmark: assembled DOFs/s + BiCGSTAB iterations/s, 3-species PNP on pore.msh refined.
+
+Workload (BASELINE.json configs[2]): test/pore_pnp/pore.msh refined
+k=4 (V = 738,033, N = 2,214,099 DOFs), test/pore_pnp/pore.cfg (cylindrical), PnpOperator.
+State: the Boltzmann initial state of the reference's driver (PB Newton on the GPU, then the
+BCExtension interpolation, src/stationary_pnp_from_pb.hh:105-282); the Jacobian at that state
+and R(x0) are the linear system (SURVEY.md §8(d) "Synthetic inputs").
+
+One step = one full residual + Jacobian assembly of the device-resident state (the headline
+`value`, assembled DOFs/s), timed over K steps bracketed by barrier + device sync.  A second
+timed region runs K x --bicg-iters BiCGSTAB iterations (SSOR = multicolour symmetric GS) on
+the assembled system and reports BiCGSTAB iterations/s.  Roofline numbers come from HIP events
+recorded on the library's own stream around every assembly launch.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling -- the mesh is N mirrored
+copies of the pore glued at their outflow/inflow planes, partitioned by RCB (one copy per GPU),
+with RCCL halo exchange per SpMV and allreduce per BiCGSTAB reduction.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
+import pnp_amd as P  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6290
+
+
+def tile_mesh(mesh, n):
+    """n mirrored copies along x, glued at the x-max plane of each copy (weak scaling)."""
+    if n == 1:
+        return mesh
+    xy, tri, bseg, bg = [mesh.xy], [mesh.tri], [], []
+    x0, x1 = mesh.xy[:, 0].min(), mesh.xy[:, 0].max()
+    L = x1 - x0
+    nv = mesh.nv
+    cur_xy = mesh.xy
+    offset = 0
+    glue_prev = None  # map: vertex index in copy k-1 on its x-max plane -> global id
+    all_b = [(mesh.bseg, mesh.bgroup, 0)]
+    gmap_prev = np.arange(nv)
+    total = nv
+    xy_out = [mesh.xy]
+    tri_out = [mesh.tri]
+    seg_out = []
+    for k in range(1, n):
+        right = x0 + k * L  # plane shared with the previous copy
+        new_xy = cur_xy.copy()
+        new_xy[:, 0] = 2 * right - cur_xy[:, 0]
+        on_plane = np.isclose(cur_xy[:, 0], right, rtol=0, atol=1e-12 * max(1.0, abs(right)))
+        gmap = np.empty(nv, dtype=np.int64)
+        gmap[on_plane] = gmap_prev[on_plane]
+        fresh = ~on_plane
+        gmap[fresh] = total + np.arange(fresh.sum())
+        total += int(fresh.sum())
+        xy_out.append(new_xy[fresh])
+        tri_out.append(gmap[mesh.tri])
+        all_b.append((mesh.bseg, mesh.bgroup, k, gmap))
+        cur_xy, gmap_prev = new_xy, gmap
+    # boundary segments: drop those on glued planes
+    xy_all = np.concatenate(xy_out)
+    bs, bgs = [], []
+    gmaps = [np.arange(nv)] + [a[3] for a in all_b[1:]]
+    for k in range(n):
+        g = gmaps[k]
+        s = g[mesh.bseg]
+        xs = xy_all[s][:, :, 0]
+        glued = np.zeros(len(s), dtype=bool)
+        for p in range(1, n):
+            plane = x0 + p * L
+            glued |= np.all(np.isclose(xs, plane, rtol=0, atol=1e-9), axis=1)
+        bs.append(s[~glued])
+        bgs.append(mesh.bgroup[~glued])
+    return P.Mesh(xy_all, np.concatenate(tri_out), np.concatenate(bs), np.concatenate(bgs))
+
+
+def barrier_sync(dist, world):
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(cfg, refine, seconds):
+    """The oracle (C restatement of the reference algorithm: FD Jacobian with PDELab eps,
+    BCRS-style CSR scatter, ISTL BiCGSTAB) single-threaded on the host, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import meshio
+    import oracle_py as O
+    mesh = meshio.refine(meshio.read_gmsh(cfg.meshfile), refine)
+    s = cfg.system
+    surfs = [meshio.Surface(q.cb, q.cflux, q.cpot, q.pb, q.pflux, q.pconc, q.mb, q.mflux, q.mconc)
+             for q in cfg.surfaces]
+    orc = O.Problem(mesh, surfs, l_b=s["l_b"], c0=s["c0"], tau=s["tau"],
+                    cylindrical=s["cylindrical"])
+    rng = np.random.default_rng(20261015)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    n_asm, t0 = 0, time.perf_counter()
+    J = None
+    while time.perf_counter() - t0 < 0.6 * seconds or n_asm == 0:
+        orc.residual(op, x)
+        J = orc.jacobian(op, x, fd=True)
+        n_asm += 1
+    t_asm = (time.perf_counter() - t0) / n_asm
+    b = orc.residual(op, x)
+    it_budget = max(5, int(0.4 * seconds / max(t_asm / 20, 1e-4)))
+    t1 = time.perf_counter()
+    _, res = O.bicgstab(J, b, prec=O.PREC_NONE, reduction=1e-30, maxit=min(it_budget, 2000))
+    t_it = (time.perf_counter() - t1) / max(res.iterations, 1)
+    return {"dofs": 3 * nv, "assembly_s": t_asm, "dofs_per_s": 3 * nv / t_asm,
+            "bicgstab_nonprec_s_per_it": t_it, "iterations": res.iterations,
+            "nnz_full": int(J.nnz)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--refine", type=int, default=4)
+    ap.add_argument("--bicg-iters", type=int, default=20)
+    ap.add_argument("--prec", default="ssor", choices=["none", "jacobi", "ssor"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-refine", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cfg", default=os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(1)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    uid = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        obj = [P.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+
+    cfg = P.read_config(args.cfg)
+    base = P.Mesh.read_gmsh(cfg.meshfile).refine(args.refine)
+    mesh = tile_mesh(base, world)
+    par = P.Params.from_config(cfg)
+    prec = P.PREC_BY_NAME[args.prec]
+
+    ctx = P.Context(mesh, par, device=local, rank=rank, size=world, unique_id=uid)
+    # Boltzmann initial state: PB Newton (SSOR BiCGSTAB, like ISTLBackend_NOVLP_BCGS_SSORk)
+    t_setup = time.perf_counter()
+    ctx.set_operator(P.OP_PB)
+    phi_pb, pb_res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=P.PREC_SSOR,
+                                linear_maxit=20000)
+    if world > 1:  # each rank returns its owned entries; combine
+        import torch
+        t = torch.from_numpy(phi_pb)
+        dist.all_reduce(t)
+        phi_pb = t.numpy()
+    x0 = ctx.initial_state(phi_pb)
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(x0)
+    t_setup = time.perf_counter() - t_setup
+    info = ctx.info()
+    N_global = 3 * mesh.nv
+    N_local = 3 * info["nv_owned"]
+
+    # ---- warmup ------------------------------------------------------------------------------
+    ctx.assemble_state(args.warmup)
+    ctx.bicgstab_iterations(max(1, args.warmup), prec)
+
+    # ---- timed region 1: assembly --------------------------------------------------------------
+    ctx.assemble_state(1)
+    barrier_sync(dist, world)
+    t0 = time.perf_counter()
+    ctx.assemble_state(args.steps)
+    barrier_sync(dist, world)
+    t_asm = time.perf_counter() - t0
+
+    # ---- timed region 2: BiCGSTAB ---------------------------------------------------------------
+    barrier_sync(dist, world)
+    t0 = time.perf_counter()
+    sres = None
+    for _ in range(args.steps):
+        sres = ctx.bicgstab_iterations(args.bicg_iters, prec)
+    barrier_sync(dist, world)
+    t_bicg = time.perf_counter() - t0
+
+    # ---- event-timed pass (roofline) -------------------------------------------------------------
+    ctx.timers(enable=True, reset=True)
+    ctx.assemble_state(args.steps)
+    ctx.bicgstab_iterations(args.bicg_iters, prec)
+    tm = ctx.timers(enable=False)
+
+    def maxall(v):
+        if world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_asm, t_bicg = maxall(t_asm), maxall(t_bicg)
+    asm_avg_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
+    V, T = info["nv_owned"], None
+    # algorithmic bytes: B_asm = 8 nnz_red + 16 N + 12 T + 16 V, per rank
+    nnz_red = 7 * info["nblocks"]
+    T_local = int(round(mesh.nt * V / mesh.nv))
+    B_asm = 8 * nnz_red + 16 * N_local + 12 * T_local + 16 * V
+    B_it = (48 if prec != P.PREC_NONE else 24) * nnz_red + (304 if prec != P.PREC_NONE else 232) \
+        * N_local
+    achieved_asm = B_asm / asm_avg_s / 1e9
+    it_time_ev = (tm["spmv_ms"] + tm["prec_ms"] + tm["blas_ms"] + tm["halo_ms"] +
+                  tm["allreduce_ms"]) / 1e3 / args.bicg_iters
+
+    dofs_per_s = N_global * args.steps / t_asm
+    iters_per_s = args.steps * args.bicg_iters / t_bicg
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cb = cpu_baseline(cfg, args.cpu_refine, args.cpu_seconds)
+        cpu = {"value": cb["dofs_per_s"], "unit": "assembled DOFs/s", "cores": 1, "kind": "port",
+               "sample": (f"oracle/pnp_oracle.c (C restatement of the reference: PnpOperator "
+                          f"residual + PDELab forward-difference Jacobian + BCRS-style scatter) on "
+                          f"pore_pnp refined k={args.cpu_refine} ({cb['dofs']} DOFs), "
+                          f"{cb['assembly_s']:.3f} s per assembly, single thread on "
+                          f"{platform.processor() or platform.machine()}; ISTL BiCGSTAB NOPREC "
+                          f"on the same system {cb['bicgstab_nonprec_s_per_it'] * 1e3:.2f} ms/it"),
+               "bicgstab_nonprec_iters_per_s_at_sample": 1.0 / cb["bicgstab_nonprec_s_per_it"]}
+
+    if rank == 0:
+        line = {
+            "metric": "assembled DOFs/s + BiCGStab iters/s, 3-species PNP on pore.msh-refined",
+            "value": dofs_per_s,
+            "unit": "assembled DOFs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * t_asm / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic-free: reference meshes/configs (test/pore_pnp), Boltzmann initial "
+                    "state from a GPU PB solve",
+            "config": {"workload": f"config 3: stationary 3-ion PNP, test/pore_pnp/pore.msh "
+                                   f"refined k={args.refine} x {world} mirrored copies",
+                       "dofs": N_global, "dofs_per_gpu": N_local, "mesh_vertices": mesh.nv,
+                       "triangles": mesh.nt, "parallelism": f"mesh partition (RCB) x{world}",
+                       "preconditioner": args.prec},
+            "bicgstab_iters_per_s": iters_per_s,
+            "bicgstab_ms_per_iter": 1e3 * t_bicg / (args.steps * args.bicg_iters),
+            "roofline": {"bound": "hbm", "achieved": achieved_asm, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved_asm / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_assemble<OP_PNP,1>",
+                         "bytes_per_launch": B_asm, "avg_launch_us": asm_avg_s * 1e6},
+            "roofline_bicgstab": {"bound": "hbm", "bytes_per_iter": B_it,
+                                  "event_ms_per_iter": it_time_ev * 1e3,
+                                  "achieved": B_it / it_time_ev / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": B_it / it_time_ev / 1e9 / HBM_PEAK_GBS},
+            "cpu_baseline": cpu,
+            "setup_s": t_setup,
+            "pb_newton": {"iterations": pb_res["iterations"],
+                          "linear_iterations": pb_res["linear_iterations"],
+                          "converged": pb_res["converged"]},
+            "event_timers_ms": tm,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,409 @@
+// Residual + Jacobian assembly on gfx950: owner-computes, atomic-free, one thread per vertex row.
+//
+// The reference assembles element by element (PDELab GridOperator over alpha_volume, e.g.
+// src/pnp_operator.hh:46-195) and differentiates by forward differences (NumericalJacobianVolume,
+// 10 residual evaluations per PNP element), scatter-adding 81 values per element into a BCRS
+// matrix.  Here each thread owns one vertex row i and walks the CCW fan of triangles around i
+// (mesh.cc build_fans): element (i, v_s, v_{s+1}) contributes to row i's diagonal block, to
+// block (i, v_s) and to block (i, v_{s+1}).  Block (i, v_s) only ever receives contributions
+// from the two fan elements on either side of edge (i, v_s), which are consecutive in the walk,
+// so it is complete after step s: it is kept in registers ("pending"), finished, and stored
+// exactly once.  Slot s of the SELL row is the s-th fan neighbour, so at step s every lane of a
+// wave stores slot s: all block stores are coalesced 512-byte lines and there are no atomics.
+//
+// Element integrals are the closed forms of the reference's order-3 quadrature where that rule
+// is exact (PnpOperator / PoissonOperator integrands are polynomials of degree <= 3, also with
+// the cylindrical 2*PI*y weight); PBOperator (sinh) and the PnpTOperator mass (a cubic under the
+// order-2 rule, src/pnp_toperator.hh:26) use the reference's quadrature points explicitly.
+#include "kernels.h"
+
+namespace pnp {
+
+namespace {
+
+struct Geo {
+  double gi0, gi1, gb0, gb1, gc0, gc1;  // physical gradients of the P1 basis at i, b, c
+  double adet;
+};
+
+__device__ __forceinline__ void geometry(double xi, double yi, double xb, double yb, double xc,
+                                         double yc, Geo &G) {
+  double J00 = xb - xi, J01 = xc - xi, J10 = yb - yi, J11 = yc - yi;
+  double det = J00 * J11 - J01 * J10;
+  double id = 1.0 / det;
+  G.gb0 = J11 * id;
+  G.gb1 = -J01 * id;
+  G.gc0 = -J10 * id;
+  G.gc1 = J00 * id;
+  G.gi0 = -G.gb0 - G.gc0;
+  G.gi1 = -G.gb1 - G.gc1;
+  G.adet = fabs(det);
+}
+
+// cylindrical/planar integrals of the P1 basis on the element (i, b, c):
+//   W = int w, m_j = int w psi_j, M_ij = int w psi_i psi_j  (w = 2*PI*y or 1)
+struct Ints {
+  double W, mi, mb, mc, Mii, Mib, Mic;
+};
+__device__ __forceinline__ void integrals(const Geo &G, int cyl, double pi, double yi, double yb,
+                                          double yc, Ints &I) {
+  if (cyl) {
+    double c = 2 * pi * G.adet;
+    double Y = yi + yb + yc;
+    I.W = c * Y * (1.0 / 6.0);
+    I.mi = c * (Y + yi) * (1.0 / 24.0);
+    I.mb = c * (Y + yb) * (1.0 / 24.0);
+    I.mc = c * (Y + yc) * (1.0 / 24.0);
+    I.Mii = c * (yi * (1.0 / 20.0) + (yb + yc) * (1.0 / 60.0));
+    I.Mib = c * ((yi + yb) * (1.0 / 60.0) + yc * (1.0 / 120.0));
+    I.Mic = c * ((yi + yc) * (1.0 / 60.0) + yb * (1.0 / 120.0));
+  } else {
+    I.W = G.adet * 0.5;
+    I.mi = I.mb = I.mc = G.adet * (1.0 / 6.0);
+    I.Mii = G.adet * (1.0 / 12.0);
+    I.Mib = I.Mic = G.adet * (1.0 / 24.0);
+  }
+}
+
+// order-2 (3-point) rule mass, (PnpTOperator, src/pnp_toperator.hh:26 / dune-geometry order 2);
+// barycentric points (1/6, 2/3, 1/6) and permutations, weight 1/6 * |det| * (2 PI y)
+__device__ __forceinline__ void mass_q2(const Geo &G, int cyl, double pi, double yi, double yb,
+                                        double yc, double &Mii, double &Mib, double &Mic) {
+  Mii = Mib = Mic = 0;
+  const double a = 1.0 / 6.0, b = 2.0 / 3.0;
+  const double P[3][3] = {{a, b, a}, {a, a, b}, {b, a, a}};
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    double f = (1.0 / 6.0) * G.adet;
+    if (cyl) f *= (P[q][0] * yi + P[q][1] * yb + P[q][2] * yc) * 2 * pi;
+    Mii += f * P[q][0] * P[q][0];
+    Mib += f * P[q][0] * P[q][1];
+    Mic += f * P[q][0] * P[q][2];
+  }
+}
+
+template <int OP>
+struct OpTraits {
+  static constexpr int NF = (OP == OP_PNP || OP == OP_PNP_IE) ? 3 : 1;
+  static constexpr int PAT = OP == OP_PNP ? kPatPnp : (OP == OP_PNP_IE ? kPatPnpIE : kPatScalar);
+  static constexpr int NV = popc9(PAT);
+};
+
+// Contributions of element (i, b, c) to row i: residual res[NF], blocks (i,i), (i,b), (i,c).
+template <int OP, int JAC>
+__device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double yi, double yb,
+                                        double yc, const double *ui, const double *ub,
+                                        const double *uc, double pi_, double pb_, double pc_,
+                                        double qi, double qb, double qc, double *res, double *Bd,
+                                        double *Bb, double *Bc) {
+  using T = OpTraits<OP>;
+  constexpr int PAT = T::PAT;
+  const double PI = a.pi;
+  double Gii = G.gi0 * G.gi0 + G.gi1 * G.gi1;
+  double Gib = G.gb0 * G.gi0 + G.gb1 * G.gi1;
+  double Gic = G.gc0 * G.gi0 + G.gc1 * G.gi1;
+  if constexpr (OP == OP_PNP || OP == OP_PNP_IE) {
+    Ints I;
+    integrals(G, a.cylindrical, PI, yi, yb, yc, I);
+    double gph0 = ui[0] * G.gi0 + ub[0] * G.gb0 + uc[0] * G.gc0;
+    double gph1 = ui[0] * G.gi1 + ub[0] * G.gb1 + uc[0] * G.gc1;
+    double gcp0 = ui[1] * G.gi0 + ub[1] * G.gb0 + uc[1] * G.gc0;
+    double gcp1 = ui[1] * G.gi1 + ub[1] * G.gb1 + uc[1] * G.gc1;
+    double gcm0 = ui[2] * G.gi0 + ub[2] * G.gb0 + uc[2] * G.gc0;
+    double gcm1 = ui[2] * G.gi1 + ub[2] * G.gb1 + uc[2] * G.gc1;
+    double gp = gph0 * G.gi0 + gph1 * G.gi1;
+    double Sp = ui[1] * I.mi + ub[1] * I.mb + uc[1] * I.mc;
+    double Sm = ui[2] * I.mi + ub[2] * I.mb + uc[2] * I.mc;
+    double kap = 4 * PI * a.l_b;
+    double sc = (OP == OP_PNP_IE) ? a.dt : 1.0;
+    res[0] += sc * (gp * I.W + kap * ((ui[1] - ui[2]) * I.Mii + (ub[1] - ub[2]) * I.Mib +
+                                      (uc[1] - uc[2]) * I.Mic));
+    res[1] += sc * ((gcp0 * G.gi0 + gcp1 * G.gi1) * I.W - gp * Sp);
+    res[2] += sc * ((gcm0 * G.gi0 + gcm1 * G.gi1) * I.W + gp * Sm);
+    double M2ii = 0, M2ib = 0, M2ic = 0;
+    if constexpr (OP == OP_PNP_IE) {
+      mass_q2(G, a.cylindrical, PI, yi, yb, yc, M2ii, M2ib, M2ic);
+      res[1] += a.tau * ((ui[1] + ui[2]) * M2ii + (ub[1] + ub[2]) * M2ib + (uc[1] + uc[2]) * M2ic);
+    }
+    if constexpr (JAC) {
+      auto blk = [&](double *B, double Gij, double Mij, double mj, double M2ij) {
+        B[pat_index(PAT, 0, 0)] += sc * Gij * I.W;
+        B[pat_index(PAT, 0, 1)] += sc * kap * Mij;
+        B[pat_index(PAT, 0, 2)] -= sc * kap * Mij;
+        B[pat_index(PAT, 1, 0)] -= sc * Gij * Sp;
+        B[pat_index(PAT, 1, 1)] += sc * (Gij * I.W - gp * mj);
+        B[pat_index(PAT, 2, 0)] += sc * Gij * Sm;
+        B[pat_index(PAT, 2, 2)] += sc * (Gij * I.W + gp * mj);
+        if constexpr (OP == OP_PNP_IE) {
+          B[pat_index(PAT, 1, 1)] += a.tau * M2ij;
+          B[pat_index(PAT, 1, 2)] += a.tau * M2ij;
+        }
+      };
+      blk(Bd, Gii, I.Mii, I.mi, M2ii);
+      blk(Bb, Gib, I.Mib, I.mb, M2ib);
+      blk(Bc, Gic, I.Mic, I.mc, M2ic);
+    }
+  } else if constexpr (OP == OP_PB) {
+    // 4-point order-3 rule, barycentric (psi_i, psi_b, psi_c)
+    const double P[4][3] = {{1.0 / 3, 1.0 / 3, 1.0 / 3}, {0.2, 0.6, 0.2}, {0.2, 0.2, 0.6},
+                            {0.6, 0.2, 0.2}};
+    const double w[4] = {0.5 * -27.0 / 48.0, 0.5 * 25.0 / 48.0, 0.5 * 25.0 / 48.0,
+                         0.5 * 25.0 / 48.0};
+    double gu0 = ui[0] * G.gi0 + ub[0] * G.gb0 + uc[0] * G.gc0;
+    double gu1 = ui[0] * G.gi1 + ub[0] * G.gb1 + uc[0] * G.gc1;
+    double gg = gu0 * G.gi0 + gu1 * G.gi1;
+    double beta = 8 * PI * a.l_b * a.c0;
+    double W = 0, Ri = 0, Jii = 0, Jib = 0, Jic = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      double f = w[q] * G.adet;
+      if (a.cylindrical) f *= (P[q][0] * yi + P[q][1] * yb + P[q][2] * yc) * 2 * PI;
+      double u = P[q][0] * ui[0] + P[q][1] * ub[0] + P[q][2] * uc[0];
+      W += f;
+      Ri += f * sinh(u) * P[q][0];
+      if constexpr (JAC) {
+        double ch = f * cosh(u) * P[q][0];
+        Jii += ch * P[q][0];
+        Jib += ch * P[q][1];
+        Jic += ch * P[q][2];
+      }
+    }
+    res[0] += gg * W + beta * Ri;
+    if constexpr (JAC) {
+      Bd[0] += Gii * W + beta * Jii;
+      Bb[0] += Gib * W + beta * Jib;
+      Bc[0] += Gic * W + beta * Jic;
+    }
+  } else if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE) {
+    // DiffusionOperator: no cylindrical weight (quirk Q8); grad Phi of the frozen potential
+    double W = G.adet * 0.5, m = G.adet * (1.0 / 6.0);
+    double gu0 = ui[0] * G.gi0 + ub[0] * G.gb0 + uc[0] * G.gc0;
+    double gu1 = ui[0] * G.gi1 + ub[0] * G.gb1 + uc[0] * G.gc1;
+    double gP0 = pi_ * G.gi0 + pb_ * G.gb0 + pc_ * G.gc0;
+    double gP1 = pi_ * G.gi1 + pb_ * G.gb1 + pc_ * G.gc1;
+    double gpP = gP0 * G.gi0 + gP1 * G.gi1;
+    double sc = (OP == OP_DIFF_IE) ? a.dt : 1.0;
+    res[0] += sc * ((gu0 * G.gi0 + gu1 * G.gi1) * W + a.z * gpP * m * (ui[0] + ub[0] + uc[0]));
+    double Mii = G.adet * (1.0 / 12.0), Mij = G.adet * (1.0 / 24.0);
+    if constexpr (OP == OP_DIFF_IE) res[0] += ui[0] * Mii + (ub[0] + uc[0]) * Mij;
+    if constexpr (JAC) {
+      Bd[0] += sc * (Gii * W + a.z * gpP * m);
+      Bb[0] += sc * (Gib * W + a.z * gpP * m);
+      Bc[0] += sc * (Gic * W + a.z * gpP * m);
+      if constexpr (OP == OP_DIFF_IE) {
+        Bd[0] += Mii;
+        Bb[0] += Mij;
+        Bc[0] += Mij;
+      }
+    }
+  } else {  // OP_POISSON: frozen c+ (aux0 -> pi_, ..) and c- (aux1 -> qi, ..)
+    Ints I;
+    integrals(G, a.cylindrical, PI, yi, yb, yc, I);
+    double gu0 = ui[0] * G.gi0 + ub[0] * G.gb0 + uc[0] * G.gc0;
+    double gu1 = ui[0] * G.gi1 + ub[0] * G.gb1 + uc[0] * G.gc1;
+    double kap = a.l_b * 4 * PI;
+    res[0] += (gu0 * G.gi0 + gu1 * G.gi1) * I.W +
+              kap * ((qi - pi_) * I.Mii + (qb - pb_) * I.Mib + (qc - pc_) * I.Mic);
+    if constexpr (JAC) {
+      Bd[0] += Gii * I.W;
+      Bb[0] += Gib * I.W;
+      Bc[0] += Gic * I.W;
+    }
+  }
+}
+
+
+template <int OP>
+__device__ __forceinline__ void store_block(double *__restrict__ vb, int s, const double *B,
+                                            unsigned dm, bool diag) {
+  using T = OpTraits<OP>;
+  constexpr int PAT = T::PAT, NV = T::NV, NF = T::NF;
+#pragma unroll
+  for (int f = 0; f < NF; f++)
+#pragma unroll
+    for (int g = 0; g < NF; g++) {
+      const int v = pat_index(PAT, f, g);
+      if (v < 0) continue;
+      double val = B[v];
+      if ((dm >> f) & 1) val = (diag && f == g) ? 1.0 : 0.0;  // constrained row -> identity
+      vb[(size_t(s) * NV + v) * kRows] = val;
+    }
+}
+
+// One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
+template <int OP, int JAC>
+__global__ __launch_bounds__(256) void k_assemble(DevLayout L, AsmArgs a) {
+  using T = OpTraits<OP>;
+  constexpr int NF = T::NF, NV = T::NV;
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk];
+  const uint64_t meta = L.rowmeta[row];
+  const int len = int(meta & 63);
+  const bool closed = (meta >> 6) & 1;
+  const int *__restrict__ cix = L.colidx + off + lane;
+  double *__restrict__ vb = a.vals + size_t(off) * NV + lane;
+
+  const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
+  double ui[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) ui[f] = a.x[size_t(row) * NF + f];
+  double ai = 0, aq = 0;
+  if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) ai = a.aux0[row];
+  if constexpr (OP == OP_POISSON) aq = a.aux1[row];
+  unsigned dm = 0;
+#pragma unroll
+  for (int f = 0; f < NF; f++) dm |= unsigned(a.dmask[size_t(row) * NF + f] != 0) << f;
+
+  double R[NF], D[NV], P[NV], F[NV];
+#pragma unroll
+  for (int f = 0; f < NF; f++) R[f] = 0;
+#pragma unroll
+  for (int v = 0; v < NV; v++) D[v] = P[v] = F[v] = 0;
+
+  for (int s = 1; s < len; ++s) {
+    const int t = (s + 1 < len) ? s + 1 : (closed ? 1 : -1);
+    const bool elem = t > 0 && !((meta >> (8 + s)) & 1);
+    if (elem) {
+      const int b = cix[s * kRows], c = cix[t * kRows];
+      const double2 pb2 = reinterpret_cast<const double2 *>(L.xy)[b];
+      const double2 pc2 = reinterpret_cast<const double2 *>(L.xy)[c];
+      double ub[NF], uc[NF];
+#pragma unroll
+      for (int f = 0; f < NF; f++) {
+        ub[f] = a.x[size_t(b) * NF + f];
+        uc[f] = a.x[size_t(c) * NF + f];
+      }
+      double ab = 0, ac = 0, qb = 0, qc = 0;
+      if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) {
+        ab = a.aux0[b];
+        ac = a.aux0[c];
+      }
+      if constexpr (OP == OP_POISSON) {
+        qb = a.aux1[b];
+        qc = a.aux1[c];
+      }
+      Geo G;
+      geometry(pi2.x, pi2.y, pb2.x, pb2.y, pc2.x, pc2.y, G);
+      double Cs[NV], Ct[NV];
+#pragma unroll
+      for (int v = 0; v < NV; v++) Cs[v] = Ct[v] = 0;
+      element<OP, JAC>(a, G, pi2.y, pb2.y, pc2.y, ui, ub, uc, ai, ab, ac, aq, qb, qc, R, D, Cs,
+                       Ct);
+      if constexpr (JAC) {
+#pragma unroll
+        for (int v = 0; v < NV; v++) P[v] += Cs[v];
+        if (s == 1 && closed) {
+#pragma unroll
+          for (int v = 0; v < NV; v++) F[v] = P[v];
+        } else {
+          store_block<OP>(vb, s, P, dm, false);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; v++) P[v] = Ct[v];
+      }
+    } else if constexpr (JAC) {
+      store_block<OP>(vb, s, P, dm, false);
+#pragma unroll
+      for (int v = 0; v < NV; v++) P[v] = 0;
+    }
+  }
+  if constexpr (JAC) {
+    if (closed) {
+#pragma unroll
+      for (int v = 0; v < NV; v++) F[v] += P[v];
+      store_block<OP>(vb, 1, F, dm, false);
+    }
+    store_block<OP>(vb, 0, D, dm, true);
+  }
+#pragma unroll
+  for (int f = 0; f < NF; f++) {
+    double rv = R[f] + a.cvec[size_t(row) * NF + f];
+    a.r[size_t(row) * NF + f] = ((dm >> f) & 1) ? 0.0 : rv;
+  }
+}
+
+// cvec[row] -= M(x_old)[row]: PnpTOperator (tau * (c+ + c-) into the c+ row, Q2) or the
+// DiffusionTOperator mass, for the implicit Euler residual M(u) - M(u_old) + dt R(u).
+template <int OP>
+__global__ __launch_bounds__(256) void k_mass_apply(DevLayout L, double tau, double pi, int cyl,
+                                                    const double *__restrict__ xo,
+                                                    double *__restrict__ cvec) {
+  constexpr int NF = OpTraits<OP>::NF;
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk];
+  const uint64_t meta = L.rowmeta[row];
+  const int len = int(meta & 63);
+  const bool closed = (meta >> 6) & 1;
+  const int *cix = L.colidx + off + lane;
+  const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
+  double acc = 0;
+  for (int s = 1; s < len; ++s) {
+    const int t = (s + 1 < len) ? s + 1 : (closed ? 1 : -1);
+    if (t < 0 || ((meta >> (8 + s)) & 1)) continue;
+    const int b = cix[s * kRows], c = cix[t * kRows];
+    const double2 pb2 = reinterpret_cast<const double2 *>(L.xy)[b];
+    const double2 pc2 = reinterpret_cast<const double2 *>(L.xy)[c];
+    Geo G;
+    geometry(pi2.x, pi2.y, pb2.x, pb2.y, pc2.x, pc2.y, G);
+    if constexpr (OP == OP_PNP_IE) {
+      double Mii, Mib, Mic;
+      mass_q2(G, cyl, pi, pi2.y, pb2.y, pc2.y, Mii, Mib, Mic);
+      acc += tau * ((xo[size_t(row) * 3 + 1] + xo[size_t(row) * 3 + 2]) * Mii +
+                    (xo[size_t(b) * 3 + 1] + xo[size_t(b) * 3 + 2]) * Mib +
+                    (xo[size_t(c) * 3 + 1] + xo[size_t(c) * 3 + 2]) * Mic);
+    } else {
+      acc += xo[row] * G.adet * (1.0 / 12.0) + (xo[b] + xo[c]) * G.adet * (1.0 / 24.0);
+    }
+  }
+  if constexpr (OP == OP_PNP_IE)
+    cvec[size_t(row) * NF + 1] -= acc;
+  else
+    cvec[row] -= acc;
+}
+
+}  // namespace
+
+hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  dim3 grid((L.n_owned + 255) / 256), block(256);
+#define PNP_ASM_CASE(OPK)                                                      \
+  case OPK:                                                                    \
+    if (a.jac)                                                                 \
+      hipLaunchKernelGGL((k_assemble<OPK, 1>), grid, block, 0, s, L, a);       \
+    else                                                                       \
+      hipLaunchKernelGGL((k_assemble<OPK, 0>), grid, block, 0, s, L, a);       \
+    break;
+  switch (a.kind) {
+    PNP_ASM_CASE(OP_PNP)
+    PNP_ASM_CASE(OP_PNP_IE)
+    PNP_ASM_CASE(OP_PB)
+    PNP_ASM_CASE(OP_DIFF)
+    PNP_ASM_CASE(OP_DIFF_IE)
+    PNP_ASM_CASE(OP_POISSON)
+  default:
+    return hipErrorInvalidValue;
+  }
+#undef PNP_ASM_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi, int cylindrical,
+                             const double *x_old, double *cvec, hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  dim3 grid((L.n_owned + 255) / 256), block(256);
+  if (kind == OP_PNP_IE)
+    hipLaunchKernelGGL(k_mass_apply<OP_PNP_IE>, grid, block, 0, s, L, tau, pi, cylindrical, x_old,
+                       cvec);
+  else if (kind == OP_DIFF_IE)
+    hipLaunchKernelGGL(k_mass_apply<OP_DIFF_IE>, grid, block, 0, s, L, tau, pi, cylindrical,
+                       x_old, cvec);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace pnp

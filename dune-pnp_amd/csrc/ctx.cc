@@ -1,0 +1,1096 @@
+// C-ABI implementation (include/pnp_capi.h): context, device buffers, halo exchange over RCCL,
+// device-resident BiCGSTAB (ISTL semantics) and PDELab-semantics Newton, host-orchestrated.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pnp_capi.h"
+#include "kernels.h"
+#include "mesh.h"
+
+namespace {
+
+thread_local std::string g_err;  // errors without a context (create / mesh calls)
+
+template <typename T>
+struct DBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    release();
+    n = count;
+    if (count == 0) return hipSuccess;
+    return hipMalloc(&p, sizeof(T) * count);
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DBuf() { release(); }
+};
+
+enum TimerCat { T_ASM = 0, T_SPMV, T_PREC, T_BLAS, T_HALO, T_ALLRED, T_NCAT };
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct pnp_mesh_buf {
+  pnp::Mesh m;
+};
+
+struct pnp_ctx {
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+
+  pnp::Mesh mesh;
+  pnp::Params params;
+  pnp::Fans fans;
+  pnp::LocalLayout L;
+  pnp::DevLayout dl;
+
+  DBuf<int> d_chunk_len, d_chunk_off, d_colidx, d_l2g, d_send_idx;
+  DBuf<uint64_t> d_rowmeta;
+  DBuf<double> d_xy;
+
+  // operator
+  int kind = -1, nf = 0, pat = 0, nvb = 0;
+  pnp::AsmArgs aa{};
+  DBuf<double> vals;
+  DBuf<uint8_t> dmask;
+  DBuf<double> cvec, aux0, aux1;
+  bool assembled = false;
+
+  // vectors (sized n_local * 3)
+  DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials;
+  DBuf<pnp::Scalars> S;
+  pnp::Scalars *hS = nullptr;  // pinned host mirror
+
+  // timers
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[T_NCAT];
+  std::vector<hipEvent_t> ev_pool;
+  double t_ms[T_NCAT] = {0};
+  long long t_n[T_NCAT] = {0};
+
+  ~pnp_ctx() {
+    for (auto &v : ev_pending)
+      for (auto &pr : v) {
+        hipEventDestroy(pr.first);
+        hipEventDestroy(pr.second);
+      }
+    for (auto e : ev_pool) hipEventDestroy(e);
+    if (hS) hipHostFree(hS);
+    if (comm) ncclCommDestroy(comm);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  int fail(int code, const std::string &msg) {
+    err = msg;
+    return code;
+  }
+  int hipfail(hipError_t e, const char *what) {
+    err = std::string(what) + ": " + hipGetErrorString(e);
+    return PNP_E_HIP;
+  }
+
+  // ---- timers -------------------------------------------------------------------------------
+  hipEvent_t ev_get() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+  }
+  hipEvent_t tb(int cat) {
+    if (!timing) return nullptr;
+    hipEvent_t e = ev_get();
+    hipEventRecord(e, stream);
+    (void)cat;
+    return e;
+  }
+  void te(int cat, hipEvent_t start) {
+    if (!timing || !start) return;
+    hipEvent_t e = ev_get();
+    hipEventRecord(e, stream);
+    ev_pending[cat].push_back({start, e});
+    t_n[cat]++;
+  }
+  void timers_flush() {
+    hipStreamSynchronize(stream);
+    for (int c = 0; c < T_NCAT; c++) {
+      for (auto &pr : ev_pending[c]) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, pr.first, pr.second);
+        t_ms[c] += ms;
+        ev_pool.push_back(pr.first);
+        ev_pool.push_back(pr.second);
+      }
+      ev_pending[c].clear();
+    }
+  }
+
+  // ---- helpers ------------------------------------------------------------------------------
+  long long nown() const { return (long long)L.n_owned * nf; }
+
+  int halo(double *vec, int nfv) {
+    if (nranks == 1 || L.nbr_ranks.empty()) return PNP_OK;
+    hipEvent_t t0 = tb(T_HALO);
+    int ns = int(L.send_idx.size());
+    hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, stream);
+    if (e != hipSuccess) return hipfail(e, "halo pack");
+    if (ncclGroupStart() != ncclSuccess) return fail(PNP_E_RCCL, "ncclGroupStart");
+    for (size_t q = 0; q < L.nbr_ranks.size(); q++) {
+      int peer = L.nbr_ranks[q];
+      size_t sc = size_t(L.send_ptr[q + 1] - L.send_ptr[q]) * nfv;
+      size_t rc = size_t(L.recv_ptr[q + 1] - L.recv_ptr[q]) * nfv;
+      if (ncclSend(sendbuf.p + size_t(L.send_ptr[q]) * nfv, sc, ncclDouble, peer, comm, stream) !=
+          ncclSuccess)
+        return fail(PNP_E_RCCL, "ncclSend");
+      if (ncclRecv(vec + (size_t(L.n_owned) + L.recv_ptr[q]) * nfv, rc, ncclDouble, peer, comm,
+                   stream) != ncclSuccess)
+        return fail(PNP_E_RCCL, "ncclRecv");
+    }
+    if (ncclGroupEnd() != ncclSuccess) return fail(PNP_E_RCCL, "ncclGroupEnd");
+    te(T_HALO, t0);
+    return PNP_OK;
+  }
+
+  int allreduce_red(int k) {
+    if (nranks == 1) return PNP_OK;
+    hipEvent_t t0 = tb(T_ALLRED);
+    double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p) +
+                                             offsetof(pnp::Scalars, red));
+    if (ncclAllReduce(red, red, k, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
+      return fail(PNP_E_RCCL, "ncclAllReduce");
+    te(T_ALLRED, t0);
+    return PNP_OK;
+  }
+
+  // norm over owned rows of a vector, synchronous
+  int norm(const double *vec, double &out) {
+    hipEvent_t t0 = tb(T_BLAS);
+    hipError_t e = pnp::launch_dot(nown(), vec, vec, 0, partials.p, stream);
+    if (e == hipSuccess) {
+      // reduce through the scalar block without touching the BiCGSTAB state: use a scratch
+      // Scalars at S.p + 1
+      e = pnp::launch_reduce(partials.p, pnp::blas_nparts(nown()), 1, S.p + 1, stream);
+    }
+    if (e != hipSuccess) return hipfail(e, "norm");
+    te(T_BLAS, t0);
+    if (nranks > 1) {
+      double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p + 1) +
+                                               offsetof(pnp::Scalars, red));
+      if (ncclAllReduce(red, red, 1, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
+        return fail(PNP_E_RCCL, "ncclAllReduce");
+    }
+    e = hipMemcpyAsync(hS + 1, S.p + 1, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "norm readback");
+    out = std::sqrt(hS[1].red[0]);
+    return PNP_OK;
+  }
+
+  int upload_ext(const double *host, int nfv, double *dev, bool with_ghosts) {
+    size_t ne = size_t(mesh.nv) * nfv;
+    hipError_t e = hipMemcpyAsync(ext.p, host, sizeof(double) * ne, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_gather_ext(with_ghosts ? L.n_owned + L.n_ghost : L.n_owned, nfv, mesh.nv,
+                                 d_l2g.p, ext.p, dev, stream);
+    if (e != hipSuccess) return hipfail(e, "upload");
+    return PNP_OK;
+  }
+
+  int download_ext(const double *dev, int nfv, double *host) {
+    size_t ne = size_t(mesh.nv) * nfv;
+    hipError_t e = pnp::launch_scatter_ext(L.n_owned, nfv, mesh.nv, d_l2g.p, dev, ext.p, stream);
+    std::vector<double> tmp(ne);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(tmp.data(), ext.p, sizeof(double) * ne, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "download");
+    for (int i = 0; i < L.n_owned; i++) {
+      int g = L.l2g[i];
+      for (int f = 0; f < nfv; f++) host[size_t(f) * mesh.nv + g] = tmp[size_t(f) * mesh.nv + g];
+    }
+    return PNP_OK;
+  }
+
+  int assemble(const double *xdev, int jac) {
+    if (kind < 0) return fail(PNP_E_STATE, "no operator set (pnp_set_operator)");
+    aa.x = xdev;
+    aa.jac = jac;
+    aa.r = r.p;
+    hipEvent_t t0 = tb(T_ASM);
+    hipError_t e = pnp::launch_assemble(dl, aa, stream);
+    if (e != hipSuccess) return hipfail(e, "assemble");
+    te(T_ASM, t0);
+    if (jac) assembled = true;
+    return PNP_OK;
+  }
+
+  // v = M^{-1} d over owned rows (v sized n_local)
+  int precond(int prec, const double *d, double *vout) {
+    hipEvent_t t0 = tb(T_PREC);
+    hipError_t e = hipSuccess;
+    if (prec == PNP_PREC_JACOBI) {
+      e = pnp::launch_jacobi(dl, nf, pat, vals.p, d, vout, stream);
+    } else if (prec == PNP_PREC_SSOR || prec == PNP_PREC_ILU0) {
+      e = pnp::launch_sgs(dl, L.color_ptr.data(), nf, pat, vals.p, d, vout, stream);
+    } else {
+      e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
+    }
+    if (e != hipSuccess) return hipfail(e, "preconditioner");
+    te(T_PREC, t0);
+    return PNP_OK;
+  }
+
+  // BiCGSTAB on J zout = bdev (owned rows), zout zero start.  fixed > 0: exactly that many
+  // iterations, no convergence stop (reduction 0), used by the benchmarks.
+  int bicgstab(const double *bdev, double *zout, const pnp_solve_opts &o, pnp_solve_result &res,
+               int fixed) {
+    if (!assembled) return fail(PNP_E_STATE, "no Jacobian assembled");
+    double t_start = now_s();
+    long long n = nown();
+    int np = pnp::blas_nparts(n);
+    int rows_np = (L.n_owned + 255) / 256;
+    (void)rows_np;
+    hipError_t e;
+    e = hipMemsetAsync(zout, 0, sizeof(double) * n, stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(rs.p + 0, bdev, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(rt.p, bdev, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(v.p, 0, sizeof(double) * n, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p.p, 0, sizeof(double) * n, stream);
+    if (e != hipSuccess) return hipfail(e, "bicgstab init");
+    // set reduction, reset flags
+    pnp::Scalars &init = hS[2];  // pinned staging slot
+    std::memset(&init, 0, sizeof init);
+    init.reduction = fixed > 0 ? 0.0 : o.reduction;
+    e = hipMemcpyAsync(S.p, &init, sizeof init, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return hipfail(e, "bicgstab scalars");
+    hipEvent_t t0 = tb(T_BLAS);
+    e = pnp::launch_dot(n, rs.p, rs.p, 0, partials.p, stream);
+    if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 1, S.p, stream);
+    if (e != hipSuccess) return hipfail(e, "bicgstab norm0");
+    te(T_BLAS, t0);
+    int rc = allreduce_red(1);
+    if (rc) return rc;
+    e = pnp::launch_derive(S.p, 0, stream);
+    if (e != hipSuccess) return hipfail(e, "derive");
+    int maxit = fixed > 0 ? fixed : o.maxit;
+    int check = o.check_every > 0 ? o.check_every : 8;
+    if (fixed > 0) check = fixed;
+    int prec = o.prec;
+    int nsp = 0;
+    for (int k = 0; k < maxit; k++) {
+      // p = r + beta (p - omega v)
+      t0 = tb(T_BLAS);
+      e = pnp::launch_update_p(n, S.p, rs.p, v.p, p.p, k == 0 ? 1 : 0, stream);
+      if (e != hipSuccess) return hipfail(e, "update_p");
+      te(T_BLAS, t0);
+      // y = M^{-1} p ; v = A y ; h = <rt, v>
+      const double *yin = p.p;
+      if (prec != PNP_PREC_NONE) {
+        if ((rc = precond(prec, p.p, y.p))) return rc;
+        yin = y.p;
+      }
+      if ((rc = halo(const_cast<double *>(yin), nf))) return rc;
+      t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, yin, v.p, 1, rt.p, partials.p, &nsp, stream);
+      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, nsp, 1, S.p, stream);
+      if (e != hipSuccess) return hipfail(e, "spmv h");
+      te(T_SPMV, t0);
+      if ((rc = allreduce_red(1))) return rc;
+      if ((e = pnp::launch_derive(S.p, 1, stream)) != hipSuccess) return hipfail(e, "derive");
+      // x += alpha y ; r -= alpha v ; ||r||
+      t0 = tb(T_BLAS);
+      e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials.p, stream);
+      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 1, S.p, stream);
+      if (e != hipSuccess) return hipfail(e, "update x r (1)");
+      te(T_BLAS, t0);
+      if ((rc = allreduce_red(1))) return rc;
+      if ((e = pnp::launch_derive(S.p, 2, stream)) != hipSuccess) return hipfail(e, "derive");
+      // y = M^{-1} r ; t = A y ; <t,r>, <t,t>
+      const double *yin2 = rs.p;
+      if (prec != PNP_PREC_NONE) {
+        if ((rc = precond(prec, rs.p, y.p))) return rc;
+        yin2 = y.p;
+      }
+      if ((rc = halo(const_cast<double *>(yin2), nf))) return rc;
+      t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, yin2, t.p, 2, rs.p, partials.p, &nsp, stream);
+      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, nsp, 2, S.p, stream);
+      if (e != hipSuccess) return hipfail(e, "spmv t");
+      te(T_SPMV, t0);
+      if ((rc = allreduce_red(2))) return rc;
+      if ((e = pnp::launch_derive(S.p, 3, stream)) != hipSuccess) return hipfail(e, "derive");
+      // x += omega y ; r -= omega t ; ||r||, <rt, r>
+      t0 = tb(T_BLAS);
+      e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
+      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 2, S.p, stream);
+      if (e != hipSuccess) return hipfail(e, "update x r (2)");
+      te(T_BLAS, t0);
+      if ((rc = allreduce_red(2))) return rc;
+      if ((e = pnp::launch_derive(S.p, 4, stream)) != hipSuccess) return hipfail(e, "derive");
+      if ((k + 1) % check == 0 || k + 1 == maxit) {
+        e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hipfail(e, "bicgstab poll");
+        if (hS->done) break;
+      }
+    }
+    e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "bicgstab result");
+    double it = std::min(double(maxit), hS->it_half);
+    res.converged = hS->done == 1 ? 1 : 0;
+    res.breakdown = hS->breakdown;
+    res.it_half = it;
+    res.iterations = int(std::ceil(it));
+    res.defect0 = hS->norm0;
+    res.defect = hS->norm;
+    res.reduction = hS->norm0 > 0 ? hS->norm / hS->norm0 : 0.0;
+    res.elapsed = now_s() - t_start;
+    return PNP_OK;
+  }
+};
+
+using pnp_ctx_t = pnp_ctx;
+
+// ---------------------------------------------------------------------------------------------
+// mesh / comm
+// ---------------------------------------------------------------------------------------------
+extern "C" int pnp_mesh_read_gmsh(const char *path, pnp_mesh_buf **out) {
+  if (!path || !out) return PNP_E_ARG;
+  auto mb = std::make_unique<pnp_mesh_buf>();
+  std::string err;
+  if (!pnp::read_gmsh(path, mb->m, err)) {
+    g_err = err;
+    return err.rfind("cannot open", 0) == 0 ? PNP_E_IO : PNP_E_MESH;
+  }
+  *out = mb.release();
+  return PNP_OK;
+}
+
+static bool mesh_from_view(const pnp_mesh *in, pnp::Mesh &m, std::string &err) {
+  if (!in || in->nv <= 0 || in->nt <= 0 || !in->coords || !in->tri || in->nbseg < 0 ||
+      (in->nbseg > 0 && (!in->bseg || !in->bseg_group))) {
+    err = "invalid pnp_mesh";
+    return false;
+  }
+  m.nv = in->nv;
+  m.nt = in->nt;
+  m.nb = in->nbseg;
+  m.xy.assign(in->coords, in->coords + 2 * size_t(in->nv));
+  m.tri.assign(in->tri, in->tri + 3 * size_t(in->nt));
+  m.bseg.assign(in->bseg, in->bseg + 2 * size_t(in->nbseg));
+  m.bgroup.assign(in->bseg_group, in->bseg_group + size_t(in->nbseg));
+  return pnp::validate(m, err);
+}
+
+extern "C" int pnp_mesh_refine(const pnp_mesh *in, int32_t k, pnp_mesh_buf **out) {
+  if (!out || k < 0) return PNP_E_ARG;
+  pnp::Mesh m;
+  std::string err;
+  if (!mesh_from_view(in, m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  auto mb = std::make_unique<pnp_mesh_buf>();
+  mb->m = pnp::refine(m, k);
+  *out = mb.release();
+  return PNP_OK;
+}
+
+extern "C" int pnp_mesh_view(const pnp_mesh_buf *mb, pnp_mesh *view) {
+  if (!mb || !view) return PNP_E_ARG;
+  view->nv = mb->m.nv;
+  view->coords = mb->m.xy.data();
+  view->nt = mb->m.nt;
+  view->tri = mb->m.tri.data();
+  view->nbseg = mb->m.nb;
+  view->bseg = mb->m.bseg.data();
+  view->bseg_group = mb->m.bgroup.data();
+  return PNP_OK;
+}
+
+extern "C" void pnp_mesh_free(pnp_mesh_buf *m) { delete m; }
+
+extern "C" const char *pnp_last_error(const pnp_ctx *ctx) {
+  return ctx ? ctx->err.c_str() : g_err.c_str();
+}
+
+extern "C" int pnp_rccl_unique_id(void *out128) {
+  if (!out128) return PNP_E_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) {
+    g_err = "ncclGetUniqueId failed";
+    return PNP_E_RCCL;
+  }
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out128, &id, 128);
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------------
+static void params_from(const pnp_params *pp, pnp::Params &P) {
+  P.l_b = pp->l_b;
+  P.c0 = pp->c0;
+  P.tau = pp->tau;
+  P.pi = pp->pi;
+  P.cylindrical = pp->cylindrical;
+  P.surf.resize(pp->n_surfaces);
+  for (int i = 0; i < pp->n_surfaces; i++) {
+    const pnp_surface &s = pp->surfaces[i];
+    pnp::Surface &d = P.surf[i];
+    d.cb = s.coulomb_btype;
+    d.cflux = s.coulomb_flux;
+    d.cpot = s.coulomb_potential;
+    d.pb = s.plus_btype;
+    d.pflux = s.plus_flux;
+    d.pconc = s.plus_concentration;
+    d.mb = s.minus_btype;
+    d.mflux = s.minus_flux;
+    d.mconc = s.minus_concentration;
+  }
+}
+
+#define CK(expr, what)                                 \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return c->hipfail(e_, what); \
+  } while (0)
+
+extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
+                          const pnp_comm *comm, pnp_ctx **out) {
+  if (!mesh || !params || !out) {
+    g_err = "pnp_create: null argument";
+    return PNP_E_ARG;
+  }
+  if (params->n_surfaces < 0 || (params->n_surfaces > 0 && !params->surfaces)) {
+    g_err = "pnp_create: invalid surfaces";
+    return PNP_E_ARG;
+  }
+  auto c = std::make_unique<pnp_ctx>();
+  std::string err;
+  if (!mesh_from_view(mesh, c->mesh, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  for (int s = 0; s < c->mesh.nb; s++)
+    if (c->mesh.bgroup[s] < 0 || c->mesh.bgroup[s] >= params->n_surfaces) {
+      g_err = "boundary segment " + std::to_string(s) + " has physical group " +
+              std::to_string(c->mesh.bgroup[s]) + " but only " +
+              std::to_string(params->n_surfaces) + " surfaces are configured";
+      return PNP_E_ARG;
+    }
+  params_from(params, c->params);
+  if (comm && comm->size > 1) {
+    c->rank = comm->rank;
+    c->nranks = comm->size;
+    if (comm->rank < 0 || comm->rank >= comm->size || !comm->rccl_unique_id) {
+      g_err = "invalid pnp_comm";
+      return PNP_E_ARG;
+    }
+  }
+  if (!pnp::build_fans(c->mesh, c->fans, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  std::vector<int> part;
+  pnp::rcb_partition(c->mesh, c->nranks, part);
+  if (!pnp::build_local_layout(c->mesh, c->fans, part, c->rank, c->nranks, c->L, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    g_err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return PNP_E_HIP;
+  }
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    g_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+    return PNP_E_HIP;
+  }
+  if (c->nranks > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, comm->rccl_unique_id, sizeof id);
+    if (ncclCommInitRank(&c->comm, c->nranks, id, c->rank) != ncclSuccess) {
+      g_err = "ncclCommInitRank failed";
+      return PNP_E_RCCL;
+    }
+  }
+  pnp::LocalLayout &L = c->L;
+  int nloc = L.n_owned + L.n_ghost;
+  std::vector<double> xy(2 * size_t(nloc));
+  for (int i = 0; i < nloc; i++) {
+    xy[2 * size_t(i)] = c->mesh.xy[2 * size_t(L.l2g[i])];
+    xy[2 * size_t(i) + 1] = c->mesh.xy[2 * size_t(L.l2g[i]) + 1];
+  }
+  pnp_ctx *cp = c.get();
+  auto up = [&](auto &buf, const auto &vec, const char *what) -> int {
+    hipError_t e2 = buf.alloc(vec.size());
+    if (e2 == hipSuccess && !vec.empty())
+      e2 = hipMemcpy(buf.p, vec.data(), sizeof(vec[0]) * vec.size(), hipMemcpyHostToDevice);
+    if (e2 != hipSuccess) return cp->hipfail(e2, what);
+    return PNP_OK;
+  };
+  int rc;
+  if ((rc = up(c->d_chunk_len, L.chunk_len, "chunk_len")) ||
+      (rc = up(c->d_chunk_off, L.chunk_off, "chunk_off")) ||
+      (rc = up(c->d_colidx, L.colidx, "colidx")) || (rc = up(c->d_rowmeta, L.rowmeta, "rowmeta")) ||
+      (rc = up(c->d_xy, xy, "xy")) || (rc = up(c->d_l2g, L.l2g, "l2g")) ||
+      (rc = up(c->d_send_idx, L.send_idx, "send_idx"))) {
+    g_err = c->err;
+    return rc;
+  }
+  c->dl.n_owned = L.n_owned;
+  c->dl.n_local = nloc;
+  c->dl.nchunks = L.nchunks;
+  c->dl.ncolors = int(L.color_ptr.size()) - 1;
+  c->dl.chunk_len = c->d_chunk_len.p;
+  c->dl.chunk_off = c->d_chunk_off.p;
+  c->dl.colidx = c->d_colidx.p;
+  c->dl.rowmeta = c->d_rowmeta.p;
+  c->dl.xy = c->d_xy.p;
+  // buffers
+  size_t nv3 = 3 * size_t(nloc);
+  auto al = [&](auto &buf, size_t n, const char *what) -> int {
+    hipError_t e2 = buf.alloc(n);
+    if (e2 == hipSuccess && n) e2 = hipMemset(buf.p, 0, sizeof(*buf.p) * n);
+    if (e2 != hipSuccess) return cp->hipfail(e2, what);
+    return PNP_OK;
+  };
+  if ((rc = al(c->vals, size_t(L.nslots) * 8, "vals")) || (rc = al(c->x, nv3, "x")) ||
+      (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
+      (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
+      (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
+      (rc = al(c->ext, 3 * size_t(c->mesh.nv), "ext")) ||
+      (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
+      (rc = al(c->partials, 2 * 4096, "partials")) || (rc = al(c->S, 2, "scalars")) ||
+      (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
+      (rc = al(c->cvec, 3 * size_t(L.n_owned), "cvec")) || (rc = al(c->aux0, nloc, "aux0")) ||
+      (rc = al(c->aux1, nloc, "aux1"))) {
+    g_err = c->err;
+    return rc;
+  }
+  if ((e = hipHostMalloc(&c->hS, 3 * sizeof(pnp::Scalars))) != hipSuccess) {
+    g_err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+    return PNP_E_HIP;
+  }
+  *out = c.release();
+  return PNP_OK;
+}
+
+extern "C" void pnp_destroy(pnp_ctx *ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  delete ctx;
+}
+
+extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
+  if (!c || !info) return PNP_E_ARG;
+  std::memset(info, 0, sizeof *info);
+  info->nv_global = c->mesh.nv;
+  info->nv_owned = c->L.n_owned;
+  info->nv_ghost = c->L.n_ghost;
+  info->nfields = c->nf;
+  info->ncolors = int(c->L.color_ptr.size()) - 1;
+  info->nchunks = c->L.nchunks;
+  info->max_slots = c->fans.max_slots;
+  info->nranks = c->nranks;
+  info->nblocks = c->L.nblocks;
+  info->nnz_reduced = c->L.nblocks * (c->nvb ? c->nvb : 1);
+  info->nslots = c->L.nslots;
+  size_t b = 0;
+  b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
+                        c->b.n + c->prevu.n + c->ext.n) * 8;
+  b += c->d_colidx.n * 4 + c->d_rowmeta.n * 8 + c->d_xy.n * 8;
+  info->device_bytes = int64_t(b);
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// operators
+// ---------------------------------------------------------------------------------------------
+extern "C" int pnp_nfields(pnp_ctx *c) { return c ? c->nf : PNP_E_ARG; }
+
+extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
+  if (!c || !a) return PNP_E_ARG;
+  if (a->kind < PNP_OP_PNP || a->kind > PNP_OP_POISSON)
+    return c->fail(PNP_E_ARG, "unknown operator kind");
+  hipSetDevice(c->device);
+  int kind = a->kind;
+  const bool ie = kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_DIFF_IMPLICIT_EULER;
+  if (ie && !(a->dt > 0)) return c->fail(PNP_E_ARG, "implicit Euler needs dt > 0");
+  if (ie && !a->x_old) return c->fail(PNP_E_ARG, "implicit Euler needs x_old");
+  if ((kind == PNP_OP_DIFF || kind == PNP_OP_DIFF_IMPLICIT_EULER) &&
+      (!a->phi || (a->field != 1 && a->field != 2)))
+    return c->fail(PNP_E_ARG, "diffusion operator needs phi and field 1 or 2");
+  if (kind == PNP_OP_POISSON && (!a->cp || !a->cm))
+    return c->fail(PNP_E_ARG, "Poisson operator needs cp and cm");
+  c->kind = kind;
+  c->nf = (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER) ? 3 : 1;
+  c->pat = kind == PNP_OP_PNP ? pnp::kPatPnp
+                              : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE : pnp::kPatScalar);
+  c->nvb = pnp::popc9(c->pat);
+  c->assembled = false;
+  const pnp::Mesh &m = c->mesh;
+  const pnp::LocalLayout &L = c->L;
+  int nf = c->nf;
+  // Dirichlet mask and constant load (Neumann flux of alpha_boundary), owned rows
+  int field0 = (kind == PNP_OP_DIFF || kind == PNP_OP_DIFF_IMPLICIT_EULER) ? a->field : 0;
+  std::vector<uint8_t> mask;
+  pnp::dirichlet_mask(m, c->params, nf, field0, mask);
+  std::vector<double> load(size_t(m.nv) * nf, 0.0);
+  if (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_PB ||
+      kind == PNP_OP_POISSON) {
+    pnp::neumann_load(m, c->params, nf, 0, load);
+    if (kind == PNP_OP_PNP_IMPLICIT_EULER)
+      for (auto &v : load) v *= a->dt;
+  }
+  std::vector<uint8_t> lmask(size_t(L.n_owned) * nf);
+  std::vector<double> lload(size_t(L.n_owned) * nf);
+  for (int i = 0; i < L.n_owned; i++)
+    for (int f = 0; f < nf; f++) {
+      lmask[size_t(i) * nf + f] = mask[size_t(L.l2g[i]) * nf + f];
+      lload[size_t(i) * nf + f] = load[size_t(L.l2g[i]) * nf + f];
+    }
+  CK(hipMemcpy(c->dmask.p, lmask.data(), lmask.size(), hipMemcpyHostToDevice), "dmask");
+  CK(hipMemcpy(c->cvec.p, lload.data(), sizeof(double) * lload.size(), hipMemcpyHostToDevice),
+     "cvec");
+  int nloc = L.n_owned + L.n_ghost;
+  auto up_field = [&](const double *h, double *d) -> int {
+    std::vector<double> tmp(nloc);
+    for (int i = 0; i < nloc; i++) tmp[i] = h[L.l2g[i]];
+    hipError_t e = hipMemcpy(d, tmp.data(), sizeof(double) * nloc, hipMemcpyHostToDevice);
+    return e == hipSuccess ? PNP_OK : c->hipfail(e, "aux upload");
+  };
+  int rc;
+  if (kind == PNP_OP_DIFF || kind == PNP_OP_DIFF_IMPLICIT_EULER)
+    if ((rc = up_field(a->phi, c->aux0.p))) return rc;
+  if (kind == PNP_OP_POISSON)
+    if ((rc = up_field(a->cp, c->aux0.p)) || (rc = up_field(a->cm, c->aux1.p))) return rc;
+  if (ie) {  // cvec -= M(x_old), rows of this rank (x_old with ghosts)
+    if ((rc = c->upload_ext(a->x_old, nf, c->prevu.p, true))) return rc;
+    int k = kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::OP_PNP_IE : pnp::OP_DIFF_IE;
+    CK(pnp::launch_mass_apply(c->dl, k, c->params.tau, c->params.pi, c->params.cylindrical,
+                              c->prevu.p, c->cvec.p, c->stream),
+       "mass apply");
+    CK(hipStreamSynchronize(c->stream), "mass apply");
+  }
+  pnp::AsmArgs &aa = c->aa;
+  aa = pnp::AsmArgs{};
+  aa.kind = kind;  // PNP_OP_* == pnp::OP_* by construction
+  aa.l_b = c->params.l_b;
+  aa.c0 = c->params.c0;
+  aa.tau = c->params.tau;
+  aa.pi = c->params.pi;
+  aa.dt = a->dt;
+  aa.z = a->z;
+  aa.cylindrical = c->params.cylindrical;
+  aa.aux0 = c->aux0.p;
+  aa.aux1 = c->aux1.p;
+  aa.cvec = c->cvec.p;
+  aa.dmask = c->dmask.p;
+  aa.vals = c->vals.p;
+  return PNP_OK;
+}
+
+extern "C" int pnp_residual(pnp_ctx *c, const double *x, double *r) {
+  if (!c || !x || !r) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  hipSetDevice(c->device);
+  int rc;
+  if ((rc = c->upload_ext(x, c->nf, c->x.p, true))) return rc;
+  if ((rc = c->assemble(c->x.p, 0))) return rc;
+  return c->download_ext(c->r.p, c->nf, r);
+}
+
+extern "C" int pnp_jacobian(pnp_ctx *c, const double *x) {
+  if (!c || !x) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  hipSetDevice(c->device);
+  int rc;
+  if ((rc = c->upload_ext(x, c->nf, c->x.p, true))) return rc;
+  if ((rc = c->assemble(c->x.p, 1))) return rc;
+  CK(hipStreamSynchronize(c->stream), "jacobian");
+  return PNP_OK;
+}
+
+extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, int32_t *col,
+                                   double *val) {
+  if (!c || !nnz) return PNP_E_ARG;
+  if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
+  const pnp::LocalLayout &L = c->L;
+  int nf = c->nf, NV = c->nvb, nv = c->mesh.nv;
+  long long total = 0;
+  for (int i = 0; i < L.n_owned; i++) total += (long long)pnp::meta_len(L.rowmeta[i]);
+  total *= NV;
+  *nnz = total;
+  if (!rowptr || !col || !val) return PNP_OK;
+  std::vector<double> hv(size_t(L.nslots) * NV);
+  CK(hipMemcpy(hv.data(), c->vals.p, sizeof(double) * hv.size(), hipMemcpyDeviceToHost), "export");
+  // rows of the external layout: f*nv + g ; count per row
+  int n = nf * nv;
+  std::vector<int> cnt(n + 1, 0);
+  for (int i = 0; i < L.n_owned; i++) {
+    int len = pnp::meta_len(L.rowmeta[i]);
+    for (int f = 0; f < nf; f++) {
+      int k = 0;
+      for (int g = 0; g < nf; g++) k += pnp::pat_index(c->pat, f, g) >= 0;
+      cnt[f * nv + L.l2g[i] + 1] += k * len;
+    }
+  }
+  for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+  std::vector<int> fill(n, 0);
+  std::vector<std::pair<int, double>> tmp;
+  for (int i = 0; i < L.n_owned; i++) {
+    int chunk = i / pnp::kRows, lane = i % pnp::kRows;
+    int len = pnp::meta_len(L.rowmeta[i]);
+    for (int f = 0; f < nf; f++) {
+      int R = f * nv + L.l2g[i];
+      tmp.clear();
+      for (int s = 0; s < len; s++) {
+        int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows + lane];
+        for (int g = 0; g < nf; g++) {
+          int v = pnp::pat_index(c->pat, f, g);
+          if (v < 0) continue;
+          double value =
+              hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NV + size_t(v) * pnp::kRows +
+                 lane];
+          tmp.push_back({g * nv + L.l2g[j], value});
+        }
+      }
+      std::sort(tmp.begin(), tmp.end());
+      for (auto &pr : tmp) {
+        col[cnt[R] + fill[R]] = pr.first;
+        val[cnt[R] + fill[R]] = pr.second;
+        fill[R]++;
+      }
+    }
+  }
+  for (int i = 0; i <= n; i++) rowptr[i] = cnt[i];
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// solves
+// ---------------------------------------------------------------------------------------------
+extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const pnp_solve_opts *o,
+                                pnp_solve_result *res) {
+  if (!c || !rhs || !z || !o || !res) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  std::memset(res, 0, sizeof *res);
+  int rc;
+  if ((rc = c->upload_ext(rhs, c->nf, c->b.p, false))) return rc;
+  if ((rc = c->bicgstab(c->b.p, c->z.p, *o, *res, 0))) return rc;
+  if ((rc = c->download_ext(c->z.p, c->nf, z))) return rc;
+  return res->breakdown ? PNP_E_BREAKDOWN : PNP_OK;
+}
+
+extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_newton_result *res) {
+  if (!c || !u || !o || !res) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  hipSetDevice(c->device);
+  std::memset(res, 0, sizeof *res);
+  double t_start = now_s();
+  int rc;
+  long long n = c->nown();
+  if ((rc = c->upload_ext(u, c->nf, c->x.p, true))) return rc;
+  double ta = now_s();
+  if ((rc = c->assemble(c->x.p, 0))) return rc;
+  double defect;
+  if ((rc = c->norm(c->r.p, defect))) return rc;
+  res->assemble_seconds += now_s() - ta;
+  res->first_defect = defect;
+  double prev_defect = defect;
+  res->status = PNP_OK;
+  for (;;) {
+    res->converged = (defect < o->abs_limit || defect < res->first_defect * o->reduction) ? 1 : 0;
+    if (res->converged) break;
+    if (res->iterations >= o->maxit) {
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    ta = now_s();
+    if ((rc = c->assemble(c->x.p, 1))) return rc;  // reassemble every step (threshold 0)
+    CK(hipStreamSynchronize(c->stream), "assemble");
+    res->assemble_seconds += now_s() - ta;
+    double stop_defect = std::max(res->first_defect * o->reduction, o->abs_limit);
+    double lin_red;
+    if (stop_defect / (10 * defect) > defect * defect / (prev_defect * prev_defect))
+      lin_red = stop_defect / (10 * defect);
+    else
+      lin_red = std::min(o->min_linear_reduction, defect * defect / (prev_defect * prev_defect));
+    prev_defect = defect;
+    // z solves J z = r(u); r lives in c->r (owned rows); keep it in b for the solver
+    CK(hipMemcpyAsync(c->b.p, c->r.p, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream),
+       "rhs");
+    pnp_solve_opts lo = o->linear;
+    lo.reduction = lin_red;
+    pnp_solve_result sr{};
+    double ts = now_s();
+    if ((rc = c->bicgstab(c->b.p, c->z.p, lo, sr, 0))) return rc;
+    res->solve_seconds += now_s() - ts;
+    res->linear_iterations += sr.iterations;
+    if (sr.breakdown) {
+      res->status = PNP_E_BREAKDOWN;
+      break;
+    }
+    if (!sr.converged) {  // PDELab NewtonLinearSolverError
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    // hackbuschReuskenAcceptBest line search
+    double lambda = 1.0, best_lambda = 0.0, best_defect = defect;
+    CK(hipMemcpyAsync(c->prevu.p, c->x.p, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream),
+       "prevu");
+    int i = 0;
+    bool ls_fail = false;
+    for (;;) {
+      CK(pnp::launch_axpby(n, 1.0, c->prevu.p, -lambda, c->z.p, c->x.p, c->stream), "axpby");
+      if ((rc = c->halo(c->x.p, c->nf))) return rc;
+      ta = now_s();
+      if ((rc = c->assemble(c->x.p, 0))) return rc;
+      if ((rc = c->norm(c->r.p, defect))) return rc;
+      res->assemble_seconds += now_s() - ta;
+      if (std::isfinite(defect) && defect <= (1.0 - lambda / 4) * prev_defect) break;
+      if (std::isfinite(defect) && defect < best_defect) {
+        best_defect = defect;
+        best_lambda = lambda;
+      }
+      if (++i >= o->line_search_maxit) {
+        if (best_lambda == 0.0) {
+          ls_fail = true;
+          break;
+        }
+        if (best_lambda != lambda) {
+          CK(pnp::launch_axpby(n, 1.0, c->prevu.p, -best_lambda, c->z.p, c->x.p, c->stream),
+             "axpby");
+          if ((rc = c->halo(c->x.p, c->nf))) return rc;
+          if ((rc = c->assemble(c->x.p, 0))) return rc;
+          if ((rc = c->norm(c->r.p, defect))) return rc;
+        }
+        break;
+      }
+      lambda *= 0.5;
+    }
+    if (ls_fail) {
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    res->iterations++;
+  }
+  res->defect = defect;
+  if ((rc = c->download_ext(c->x.p, c->nf, u))) return rc;
+  res->elapsed = now_s() - t_start;
+  return PNP_OK;
+}
+
+extern "C" int pnp_initial_state(pnp_ctx *c, const double *phi_pb, double *x0) {
+  if (!c || !x0) return PNP_E_ARG;
+  pnp::initial_state(c->mesh, c->params, phi_pb, x0);
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// device-resident hot path (benchmarks)
+// ---------------------------------------------------------------------------------------------
+extern "C" int pnp_state_set(pnp_ctx *c, const double *x) {
+  if (!c || !x) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  hipSetDevice(c->device);
+  int rc = c->upload_ext(x, c->nf, c->x.p, true);
+  if (rc) return rc;
+  CK(hipStreamSynchronize(c->stream), "state_set");
+  return PNP_OK;
+}
+
+extern "C" int pnp_state_get(pnp_ctx *c, double *x) {
+  if (!c || !x) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  return c->download_ext(c->x.p, c->nf, x);
+}
+
+extern "C" int pnp_assemble_state(pnp_ctx *c, int32_t n) {
+  if (!c || n < 0) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  for (int k = 0; k < n; k++) {
+    int rc = c->assemble(c->x.p, 1);
+    if (rc) return rc;
+  }
+  CK(hipStreamSynchronize(c->stream), "assemble_state");
+  return PNP_OK;
+}
+
+extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_solve_result *res) {
+  if (!c || !res || n <= 0) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  std::memset(res, 0, sizeof *res);
+  pnp_solve_opts o{};
+  o.prec = prec;
+  o.maxit = n;
+  CK(hipMemcpyAsync(c->b.p, c->r.p, sizeof(double) * c->nown(), hipMemcpyDeviceToDevice,
+                    c->stream),
+     "rhs");
+  return c->bicgstab(c->b.p, c->z.p, o, *res, n);
+}
+
+extern "C" int pnp_timers_enable(pnp_ctx *c, int32_t on) {
+  if (!c) return PNP_E_ARG;
+  c->timing = on != 0;
+  return PNP_OK;
+}
+
+extern "C" int pnp_timers_get(pnp_ctx *c, pnp_timers *t) {
+  if (!c || !t) return PNP_E_ARG;
+  c->timers_flush();
+  t->assemble_ms = c->t_ms[T_ASM];
+  t->spmv_ms = c->t_ms[T_SPMV];
+  t->prec_ms = c->t_ms[T_PREC];
+  t->blas_ms = c->t_ms[T_BLAS];
+  t->halo_ms = c->t_ms[T_HALO];
+  t->allreduce_ms = c->t_ms[T_ALLRED];
+  t->assemble_launches = c->t_n[T_ASM];
+  t->spmv_launches = c->t_n[T_SPMV];
+  t->prec_launches = c->t_n[T_PREC];
+  t->blas_launches = c->t_n[T_BLAS];
+  return PNP_OK;
+}
+
+extern "C" int pnp_timers_reset(pnp_ctx *c) {
+  if (!c) return PNP_E_ARG;
+  c->timers_flush();
+  for (int k = 0; k < T_NCAT; k++) {
+    c->t_ms[k] = 0;
+    c->t_n[k] = 0;
+  }
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host-only setup / inspection
+// ---------------------------------------------------------------------------------------------
+struct pnp_layout_buf {
+  pnp::Fans fans;
+  pnp::LocalLayout L;
+  std::vector<int> chunk_off32;
+};
+
+extern "C" int pnp_setup_boundary(const pnp_mesh *mesh, const pnp_params *params, int32_t nfields,
+                                  int32_t field0, uint8_t *mask, double *load) {
+  if (!params || nfields < 1 || field0 < 0 || field0 + nfields > 3) return PNP_E_ARG;
+  pnp::Mesh m;
+  std::string err;
+  if (!mesh_from_view(mesh, m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  pnp::Params P;
+  params_from(params, P);
+  for (int s = 0; s < m.nb; s++)
+    if (m.bgroup[s] < 0 || m.bgroup[s] >= int(P.surf.size())) return PNP_E_ARG;
+  std::vector<uint8_t> mk;
+  std::vector<double> ld;
+  pnp::dirichlet_mask(m, P, nfields, field0, mk);
+  pnp::neumann_load(m, P, nfields, field0, ld);
+  for (int v = 0; v < m.nv; v++)
+    for (int f = 0; f < nfields; f++) {
+      if (mask) mask[size_t(f) * m.nv + v] = mk[size_t(v) * nfields + f];
+      if (load) load[size_t(f) * m.nv + v] = ld[size_t(v) * nfields + f];
+    }
+  return PNP_OK;
+}
+
+extern "C" int pnp_setup_initial_state(const pnp_mesh *mesh, const pnp_params *params,
+                                       const double *phi_pb, double *x0) {
+  if (!params || !x0) return PNP_E_ARG;
+  pnp::Mesh m;
+  std::string err;
+  if (!mesh_from_view(mesh, m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  pnp::Params P;
+  params_from(params, P);
+  for (int s = 0; s < m.nb; s++)
+    if (m.bgroup[s] < 0 || m.bgroup[s] >= int(P.surf.size())) return PNP_E_ARG;
+  pnp::initial_state(m, P, phi_pb, x0);
+  return PNP_OK;
+}
+
+extern "C" int pnp_layout_build(const pnp_mesh *mesh, int32_t rank, int32_t nranks,
+                                pnp_layout_buf **out) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks) return PNP_E_ARG;
+  pnp::Mesh m;
+  std::string err;
+  if (!mesh_from_view(mesh, m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  auto b = std::make_unique<pnp_layout_buf>();
+  if (!pnp::build_fans(m, b->fans, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  std::vector<int> part;
+  pnp::rcb_partition(m, nranks, part);
+  if (!pnp::build_local_layout(m, b->fans, part, rank, nranks, b->L, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  *out = b.release();
+  return PNP_OK;
+}
+
+extern "C" int pnp_layout_view(const pnp_layout_buf *b, pnp_layout *v) {
+  if (!b || !v) return PNP_E_ARG;
+  const pnp::LocalLayout &L = b->L;
+  v->n_owned = L.n_owned;
+  v->n_ghost = L.n_ghost;
+  v->ncolors = int(L.color_ptr.size()) - 1;
+  v->nchunks = L.nchunks;
+  v->nnbr = int(L.nbr_ranks.size());
+  v->max_slots = b->fans.max_slots;
+  v->nslots = L.nslots;
+  v->nblocks = L.nblocks;
+  v->l2g = L.l2g.data();
+  v->color_ptr = L.color_ptr.data();
+  v->chunk_len = L.chunk_len.data();
+  v->chunk_off = L.chunk_off.data();
+  v->colidx = L.colidx.data();
+  v->rowmeta = L.rowmeta.data();
+  v->nbr_ranks = L.nbr_ranks.data();
+  v->recv_ptr = L.recv_ptr.data();
+  v->send_ptr = L.send_ptr.data();
+  v->send_idx = L.send_idx.data();
+  return PNP_OK;
+}
+
+extern "C" void pnp_layout_free(pnp_layout_buf *b) { delete b; }

@@ -1,0 +1,134 @@
+// Device data structures and kernel launchers of the MI355X PNP hot path.
+//
+// HBM layout (per GPU / per rank):
+//   rows       = owned vertices, coloured, Morton-ordered inside a colour (mesh.cc)
+//   vectors    = vertex-interleaved: x[i*NF + f], owned rows first, then ghosts
+//   matrix     = SELL-64 of NF x NF vertex-pair blocks. Chunk c holds rows 64c..64c+63 with
+//                chunk_len[c] slots; slot 0 is the diagonal block, slot s >= 1 the s-th
+//                neighbour of the row's CCW fan.  Column indices: colidx[off_c + 64 s + lane].
+//                Only the structurally non-zero entries of a block are stored (BlockPattern):
+//                NV doubles per block, value v of slot s at vals[(off_c + 64 s) * NV + 64 v + lane],
+//                so every (slot, value) plane of a chunk is one 512-byte coalesced line.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pnp {
+
+constexpr int kRows = 64;  // rows per SELL chunk = one wavefront
+
+// ---- operator kinds / block patterns ----------------------------------------------------------
+enum OpKind : int {
+  OP_PNP = 0,
+  OP_PNP_IE = 1,
+  OP_PB = 2,
+  OP_DIFF = 3,
+  OP_DIFF_IE = 4,
+  OP_POISSON = 5
+};
+
+// Block pattern: bit (f*3+g) set if entry (f,g) of a vertex-pair block can be non-zero.
+// PNP: c+ and c- never couple (7 of 9).  PNP with the PnpTOperator mass: the c- mass sits in the
+// c+ rows (quirk Q2, src/pnp_toperator.hh:99), so (c+, c-) is added (8 of 9).  Scalar: 1x1.
+constexpr int kPatPnp = 0x1FF & ~((1 << 5) | (1 << 7));
+constexpr int kPatPnpIE = 0x1FF & ~(1 << 7);
+constexpr int kPatScalar = 1;
+
+__host__ __device__ constexpr int popc9(int m) {
+  int c = 0;
+  for (int i = 0; i < 9; i++) c += (m >> i) & 1;
+  return c;
+}
+// position of (f,g) among the stored values (row-major order), -1 if not stored
+__host__ __device__ constexpr int pat_index(int mask, int f, int g) {
+  if (!((mask >> (f * 3 + g)) & 1)) return -1;
+  int c = 0;
+  for (int i = 0; i < f * 3 + g; i++) c += (mask >> i) & 1;
+  return c;
+}
+
+// ---- device views ----------------------------------------------------------------------------
+struct DevLayout {
+  int n_owned = 0, n_local = 0, nchunks = 0, ncolors = 0;
+  const int *chunk_len = nullptr;
+  const int *chunk_off = nullptr;   // nchunks + 1
+  const int *colidx = nullptr;
+  const uint64_t *rowmeta = nullptr;
+  const double *xy = nullptr;       // [n_local][2]
+};
+
+struct AsmArgs {
+  int kind;
+  int jac;               // 1: residual + Jacobian, 0: residual only
+  double l_b, c0, tau, pi, dt, z;
+  int cylindrical;
+  const double *x;       // [n_local * NF]
+  const double *aux0;    // DIFF: phi [n_local]; POISSON: cp [n_local]
+  const double *aux1;    // POISSON: cm [n_local]
+  const double *cvec;    // constant part of the residual [n_owned * NF] (Neumann load, old mass)
+  const uint8_t *dmask;  // Dirichlet mask [n_owned * NF]
+  double *r;             // [n_owned * NF]
+  double *vals;          // SELL values
+};
+
+// BiCGSTAB scalar block, resident on the device (no host round trip per half step)
+struct Scalars {
+  double rho, rho_new, alpha, omega, h, norm0, norm, reduction;
+  double it_half;        // ISTL half-step counter of the last completed half step
+  double red[4];         // reduction results (after allreduce)
+  int done;              // 0 running, 1 converged, 2 breakdown
+  int breakdown;         // 1 rho, 2 omega, 3 h
+  int iter;              // full iterations started
+  int pad;
+};
+
+// ---- launchers (return hipError_t of the launch) ----------------------------------------------
+hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s);
+// old-time mass M(x_old) (PnpTOperator / DiffusionTOperator) subtracted into cvec
+hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi, int cylindrical,
+                             const double *x_old, double *cvec, hipStream_t s);
+
+// y = A x over owned rows; optional fused dots: out partials[block*k + j]
+//   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2)
+hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
+                       double *y, int mode, const double *w, double *partials, int *nparts,
+                       hipStream_t s);
+
+// preconditioners: v = M^{-1} d (v over owned rows)
+hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
+                         double *v, hipStream_t s);
+hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
+                      const double *vals, const double *d, double *v, hipStream_t s);
+
+// BLAS-1 over n = n_owned*nf entries
+int blas_nparts(long long n);
+// p = (it<1) ? r : beta*(p - omega*v) + r, with beta from Scalars
+hipError_t launch_update_p(long long n, const Scalars *S, const double *r, const double *v,
+                           double *p, int first, hipStream_t s);
+// x += a*y; r -= a*v; partials <r,r> [, <rt, r>];  a = S->alpha (which=0) or S->omega (which=1)
+hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x, const double *y,
+                            double *r, const double *v, const double *rt, double *partials,
+                            hipStream_t s);
+// partials of <a,b> (and <a,a> if two)
+hipError_t launch_dot(long long n, const double *a, const double *b, int two, double *partials,
+                      hipStream_t s);
+// sum partials[nparts][k] -> S->red[0..k) (deterministic order)
+hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s);
+// derive scalars after a reduction; stage: 0 init (red: <r,r>), 1 after h, 2 after first half
+// norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>)
+hipError_t launch_derive(Scalars *S, int stage, hipStream_t s);
+
+// y = x - lambda*z (Newton line search), copy/scale helpers
+hipError_t launch_axpby(long long n, double a, const double *x, double b, const double *y,
+                        double *out, hipStream_t s);
+// halo pack: buf[k*nf+f] = x[idx[k]*nf+f]
+hipError_t launch_pack(int n, int nf, const int *idx, const double *x, double *buf, hipStream_t s);
+// external <-> internal permutation: ext[f*nv_global + l2g[i]] <-> in[i*nf + f], i < n
+hipError_t launch_gather_ext(int n, int nf, int nv_global, const int *l2g, const double *ext,
+                             double *in, hipStream_t s);
+hipError_t launch_scatter_ext(int n, int nf, int nv_global, const int *l2g, const double *in,
+                              double *ext, hipStream_t s);
+
+}  // namespace pnp

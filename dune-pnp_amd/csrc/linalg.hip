@@ -1,0 +1,471 @@
+// Sparse linear algebra of the BiCGSTAB path on gfx950 (replaces ISTL BCRSMatrix::mv,
+// BiCGSTABSolver's BLAS-1 and dots, SeqSSOR).
+//
+// * SpMV: SELL-64, one thread per vertex row, lanes = 64 consecutive rows, so every column-index
+//   and value load of a slot is one coalesced 256/512-byte line; x is gathered as NF contiguous
+//   doubles per neighbour vertex (L2 / Infinity-Cache resident for Morton-ordered rows).  Dots
+//   that BiCGSTAB needs right after a SpMV are fused into its epilogue.
+// * Reductions are deterministic: per-block partials in a fixed grid, summed by one block in a
+//   fixed order; the BiCGSTAB scalars (rho, alpha, omega, norms, half-step counter, convergence
+//   and breakdown flags) never leave the device, so the host only polls for termination.
+// * SSOR(k=1, w=1) = one multicolour symmetric Gauss-Seidel sweep: rows of one colour have no
+//   coupling among themselves, so each colour is one fully parallel launch (forward: colours
+//   ascending, backward: descending); couplings to ghost rows are dropped (block-Jacobi across
+//   GPUs, like the reference's non-overlapping SSOR on the local matrix).
+#include "kernels.h"
+
+namespace pnp {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr double kEps = 1e-80;  // ISTL BiCGSTABSolver EPSILON
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum of K values, result written by thread 0 to out[0..K)
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double *out) {
+  __shared__ double sh[kBlock / 64][K > 0 ? K : 1];
+  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    double s = wave_sum(v[k]);
+    if (l == 0) sh[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      double s = 0;
+      for (int i = 0; i < kBlock / 64; i++) s += sh[i][k];
+      out[k] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// SpMV (+ fused dots)
+// ------------------------------------------------------------------------------------------
+template <int NF, int PAT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__restrict__ vals,
+                                                 const double *__restrict__ x,
+                                                 double *__restrict__ y,
+                                                 const double *__restrict__ w,
+                                                 double *__restrict__ partials) {
+  constexpr int NV = popc9(PAT);
+  const int row = blockIdx.x * kBlock + threadIdx.x;
+  double d[2] = {0, 0};
+  if (row < L.n_owned) {
+    const int chunk = row / kRows, lane = row % kRows;
+    const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
+    const int *__restrict__ cix = L.colidx + off + lane;
+    const double *__restrict__ vb = vals + size_t(off) * NV + lane;
+    double acc[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) acc[f] = 0;
+    for (int s = 0; s < len; s++) {
+      const int j = cix[s * kRows];
+      double xj[NF];
+#pragma unroll
+      for (int g = 0; g < NF; g++) xj[g] = x[size_t(j) * NF + g];
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int v = pat_index(PAT, f, g);
+          if (v >= 0) acc[f] += vb[(size_t(s) * NV + v) * kRows] * xj[g];
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++) y[size_t(row) * NF + f] = acc[f];
+    if constexpr (MODE >= 1) {
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[0] += acc[f] * w[size_t(row) * NF + f];
+    }
+    if constexpr (MODE == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[1] += acc[f] * acc[f];
+    }
+  }
+  if constexpr (MODE == 1) {
+    double v1[1] = {d[0]};
+    block_sum<1>(v1, partials + blockIdx.x);
+  } else if constexpr (MODE == 2) {
+    double v2[2] = {d[0], d[1]};
+    block_sum<2>(v2, partials + 2 * blockIdx.x);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// preconditioners
+// ------------------------------------------------------------------------------------------
+template <int NF, int PAT>
+__global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__restrict__ vals,
+                                                   const double *__restrict__ d,
+                                                   double *__restrict__ v) {
+  constexpr int NV = popc9(PAT);
+  const int row = blockIdx.x * kBlock + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const double *vb = vals + size_t(L.chunk_off[chunk]) * NV + lane;
+#pragma unroll
+  for (int f = 0; f < NF; f++)
+    v[size_t(row) * NF + f] = d[size_t(row) * NF + f] / vb[size_t(pat_index(PAT, f, f)) * kRows];
+}
+
+// one colour of a Gauss-Seidel sweep: v_i += D_i^{-1} (d_i - sum_j A_ij v_j), rows of the
+// colour in parallel, the NF fields of a row in sequence (ascending forward, descending back).
+template <int NF, int PAT, int FWD>
+__global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int r0, int r1,
+                                                      const double *__restrict__ vals,
+                                                      const double *__restrict__ d,
+                                                      double *__restrict__ v) {
+  constexpr int NV = popc9(PAT);
+  const int row = r0 + blockIdx.x * kBlock + threadIdx.x;
+  if (row >= r1) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
+  const int *__restrict__ cix = L.colidx + off + lane;
+  const double *__restrict__ vb = vals + size_t(off) * NV + lane;
+  double rhs[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) rhs[f] = d[size_t(row) * NF + f];
+  for (int s = 1; s < len; s++) {
+    const int j = cix[s * kRows];
+    if (j >= L.n_owned || j == row) continue;  // ghost (block-Jacobi) or padding
+    if (FWD && j > row) continue;              // later colours are still zero
+    double vj[NF];
+#pragma unroll
+    for (int g = 0; g < NF; g++) vj[g] = v[size_t(j) * NF + g];
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int g = 0; g < NF; g++) {
+        const int k = pat_index(PAT, f, g);
+        if (k >= 0) rhs[f] -= vb[(size_t(s) * NV + k) * kRows] * vj[g];
+      }
+  }
+  double vi[NF], Dg[NV];
+#pragma unroll
+  for (int f = 0; f < NF; f++) vi[f] = v[size_t(row) * NF + f];
+#pragma unroll
+  for (int k = 0; k < NV; k++) Dg[k] = vb[size_t(k) * kRows];
+#pragma unroll
+  for (int ff = 0; ff < NF; ff++) {
+    const int f = FWD ? ff : NF - 1 - ff;
+    double r = rhs[f];
+#pragma unroll
+    for (int g = 0; g < NF; g++) {
+      const int k = pat_index(PAT, f, g);
+      if (k >= 0) r -= Dg[k] * vi[g];
+    }
+    vi[f] += r / Dg[pat_index(PAT, f, f)];
+  }
+#pragma unroll
+  for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = vi[f];
+}
+
+// ------------------------------------------------------------------------------------------
+// BLAS-1 and reductions
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_update_p(long long n, const Scalars *__restrict__ S,
+                                                     const double *__restrict__ r,
+                                                     const double *__restrict__ v,
+                                                     double *__restrict__ p, int first) {
+  if (S->done) return;
+  const double beta = first ? 0.0 : (S->rho_new / S->rho) * (S->alpha / S->omega);
+  const double om = S->omega;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock)
+    p[i] = first ? r[i] : beta * (p[i] - om * v[i]) + r[i];
+}
+
+template <int TWO>
+__global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars *__restrict__ S,
+                                                      int which, double *__restrict__ x,
+                                                      const double *__restrict__ y,
+                                                      double *__restrict__ r,
+                                                      const double *__restrict__ v,
+                                                      const double *__restrict__ rt,
+                                                      double *__restrict__ partials) {
+  if (S->done) return;
+  const double a = which ? S->omega : S->alpha;
+  double acc[2] = {0, 0};
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock) {
+    x[i] += a * y[i];
+    const double ri = r[i] - a * v[i];
+    r[i] = ri;
+    acc[0] += ri * ri;
+    if (TWO) acc[1] += rt[i] * ri;
+  }
+  if (TWO) {
+    block_sum<2>(acc, partials + 2 * blockIdx.x);
+  } else {
+    double a1[1] = {acc[0]};
+    block_sum<1>(a1, partials + blockIdx.x);
+  }
+}
+
+template <int TWO>
+__global__ __launch_bounds__(kBlock) void k_dot(long long n, const double *__restrict__ a,
+                                                const double *__restrict__ b,
+                                                double *__restrict__ partials) {
+  double acc[2] = {0, 0};
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock) {
+    acc[0] += a[i] * b[i];
+    if (TWO) acc[1] += a[i] * a[i];
+  }
+  if (TWO) {
+    block_sum<2>(acc, partials + 2 * blockIdx.x);
+  } else {
+    double a1[1] = {acc[0]};
+    block_sum<1>(a1, partials + blockIdx.x);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce(const double *__restrict__ partials, int np,
+                                                   int k, Scalars *__restrict__ S) {
+  if (S->done) return;
+  double acc[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < np; i += kBlock)
+    for (int j = 0; j < k; j++) acc[j] += partials[size_t(i) * k + j];
+  double out[4];
+  block_sum<4>(acc, out);
+  if (threadIdx.x == 0)
+    for (int j = 0; j < k; j++) S->red[j] = out[j];
+}
+
+__global__ void k_derive(Scalars *S, int stage) {
+  if (threadIdx.x != 0) return;
+  if (stage == 0) {  // start: red = <r,r> with rt = r
+    S->norm0 = S->norm = sqrt(S->red[0]);
+    S->rho_new = S->red[0];
+    S->rho = S->alpha = S->omega = 1.0;
+    S->it_half = 0;
+    S->iter = 0;
+    S->breakdown = 0;
+    S->done = (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) ? 1 : 0;
+    return;
+  }
+  if (S->done) return;
+  if (stage == 1) {  // h = <rt, v>
+    S->h = S->red[0];
+    if (fabs(S->h) < kEps) {
+      S->done = 2;
+      S->breakdown = 3;
+      return;
+    }
+    S->alpha = S->rho_new / S->h;
+  } else if (stage == 2) {  // first half step norm
+    S->norm = sqrt(S->red[0]);
+    S->it_half += 0.5;
+    if (S->norm < S->reduction * S->norm0) S->done = 1;
+  } else if (stage == 3) {  // omega = <t,r>/<t,t>
+    S->omega = S->red[0] / S->red[1];
+  } else if (stage == 4) {  // second half step: red = <r,r>, <rt,r>
+    S->norm = sqrt(S->red[0]);
+    S->it_half += 0.5;
+    S->iter += 1;
+    S->rho = S->rho_new;
+    S->rho_new = S->red[1];
+    if (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) {
+      S->done = 1;
+    } else if (fabs(S->rho) <= kEps) {
+      S->done = 2;
+      S->breakdown = 1;
+    } else if (fabs(S->omega) <= kEps) {
+      S->done = 2;
+      S->breakdown = 2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_axpby(long long n, double a,
+                                                  const double *__restrict__ x, double b,
+                                                  const double *__restrict__ y,
+                                                  double *__restrict__ out) {
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock)
+    out[i] = a * x[i] + (y ? b * y[i] : 0.0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(int n, int nf, const int *__restrict__ idx,
+                                                 const double *__restrict__ x,
+                                                 double *__restrict__ buf) {
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n * nf) return;
+  buf[k] = x[size_t(idx[k / nf]) * nf + k % nf];
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_ext(int n, int nf, int nvg,
+                                                       const int *__restrict__ l2g,
+                                                       const double *__restrict__ ext,
+                                                       double *__restrict__ in) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int g = l2g[i];
+  for (int f = 0; f < nf; f++) in[size_t(i) * nf + f] = ext[size_t(f) * nvg + g];
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter_ext(int n, int nf, int nvg,
+                                                        const int *__restrict__ l2g,
+                                                        const double *__restrict__ in,
+                                                        double *__restrict__ ext) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int g = l2g[i];
+  for (int f = 0; f < nf; f++) ext[size_t(f) * nvg + g] = in[size_t(i) * nf + f];
+}
+
+inline dim3 rows_grid(int n) { return dim3((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+int blas_nparts(long long n) {
+  long long b = (n + 4LL * kBlock - 1) / (4LL * kBlock);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  return int(b);
+}
+
+#define PNP_PAT_DISPATCH(NF_, PAT_, CALL)                                 \
+  do {                                                                    \
+    if ((NF_) == 3 && (PAT_) == kPatPnp) {                                \
+      constexpr int NFc = 3, PATc = kPatPnp;                              \
+      CALL;                                                               \
+    } else if ((NF_) == 3 && (PAT_) == kPatPnpIE) {                       \
+      constexpr int NFc = 3, PATc = kPatPnpIE;                            \
+      CALL;                                                               \
+    } else if ((NF_) == 1) {                                              \
+      constexpr int NFc = 1, PATc = kPatScalar;                           \
+      CALL;                                                               \
+    } else {                                                              \
+      return hipErrorInvalidValue;                                        \
+    }                                                                     \
+  } while (0)
+
+hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
+                       double *y, int mode, const double *w, double *partials, int *nparts,
+                       hipStream_t s) {
+  dim3 g = rows_grid(L.n_owned);
+  if (nparts) *nparts = int(g.x);
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    if (mode == 0)
+      hipLaunchKernelGGL((k_spmv<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+    else if (mode == 1)
+      hipLaunchKernelGGL((k_spmv<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+    else
+      hipLaunchKernelGGL((k_spmv<NFc, PATc, 2>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
+                         double *v, hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    hipLaunchKernelGGL((k_jacobi<NFc, PATc>), rows_grid(L.n_owned), dim3(kBlock), 0, s, L, vals,
+                       d, v);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const double *vals,
+                      const double *d, double *v, hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(v, 0, sizeof(double) * size_t(L.n_owned) * nf, s);
+  if (e != hipSuccess) return e;
+  PNP_PAT_DISPATCH(nf, pat, {
+    for (int c = 0; c < L.ncolors; c++) {
+      int n = cp[c + 1] - cp[c];
+      if (n > 0)
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 1>), rows_grid(n), dim3(kBlock), 0, s, L,
+                           cp[c], cp[c + 1], vals, d, v);
+    }
+    for (int c = L.ncolors - 1; c >= 0; c--) {
+      int n = cp[c + 1] - cp[c];
+      if (n > 0)
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 0>), rows_grid(n), dim3(kBlock), 0, s, L,
+                           cp[c], cp[c + 1], vals, d, v);
+    }
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_update_p(long long n, const Scalars *S, const double *r, const double *v,
+                           double *p, int first, hipStream_t s) {
+  hipLaunchKernelGGL(k_update_p, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, r, v, p, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x, const double *y,
+                            double *r, const double *v, const double *rt, double *partials,
+                            hipStream_t s) {
+  if (rt)
+    hipLaunchKernelGGL(k_update_xr<1>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, which, x, y,
+                       r, v, rt, partials);
+  else
+    hipLaunchKernelGGL(k_update_xr<0>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, which, x, y,
+                       r, v, rt, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot(long long n, const double *a, const double *b, int two, double *partials,
+                      hipStream_t s) {
+  if (two)
+    hipLaunchKernelGGL(k_dot<1>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, a, b, partials);
+  else
+    hipLaunchKernelGGL(k_dot<0>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, a, b, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, nparts, k, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_derive(Scalars *S, int stage, hipStream_t s) {
+  hipLaunchKernelGGL(k_derive, dim3(1), dim3(64), 0, s, S, stage);
+  return hipGetLastError();
+}
+
+hipError_t launch_axpby(long long n, double a, const double *x, double b, const double *y,
+                        double *out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_axpby, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, a, x, b, y, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(int n, int nf, const int *idx, const double *x, double *buf,
+                       hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack, rows_grid(n * nf), dim3(kBlock), 0, s, n, nf, idx, x, buf);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_ext(int n, int nf, int nvg, const int *l2g, const double *ext,
+                             double *in, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_ext, rows_grid(n), dim3(kBlock), 0, s, n, nf, nvg, l2g, ext, in);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_ext(int n, int nf, int nvg, const int *l2g, const double *in,
+                              double *ext, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_ext, rows_grid(n), dim3(kBlock), 0, s, n, nf, nvg, l2g, in, ext);
+  return hipGetLastError();
+}
+
+}  // namespace pnp

@@ -1,0 +1,643 @@
+// Host-side mesh pipeline; see mesh.h.
+#include "mesh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+#include <unordered_map>
+
+namespace pnp {
+
+static inline uint64_t edge_key(int a, int b) {
+  if (a > b) std::swap(a, b);
+  return (uint64_t(uint32_t(a)) << 32) | uint32_t(b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// gmsh v2 ASCII reader
+// ---------------------------------------------------------------------------------------------
+bool read_gmsh(const std::string &path, Mesh &m, std::string &err) {
+  std::ifstream in(path);
+  if (!in) {
+    err = "cannot open mesh file '" + path + "'";
+    return false;
+  }
+  std::unordered_map<long long, int> node_index;  // gmsh node id -> position in node_xy
+  std::vector<double> node_xy;
+  std::vector<int> lines;   // [a, b, group] gmsh ids
+  std::vector<long long> tris;
+  std::string tok;
+  bool have_nodes = false, have_elems = false;
+  while (in >> tok) {
+    if (tok == "$MeshFormat") {
+      double ver;
+      int ft, ds;
+      in >> ver >> ft >> ds;
+      if (ver < 2.0 || ver >= 3.0 || ft != 0) {
+        err = "unsupported gmsh format (need ASCII v2.x)";
+        return false;
+      }
+    } else if (tok == "$Nodes") {
+      long long n;
+      in >> n;
+      node_xy.resize(2 * n);
+      for (long long i = 0; i < n; i++) {
+        long long id;
+        double x, y, z;
+        in >> id >> x >> y >> z;
+        node_index[id] = int(i);
+        node_xy[2 * i] = x;
+        node_xy[2 * i + 1] = y;
+      }
+      have_nodes = true;
+    } else if (tok == "$Elements") {
+      long long n;
+      in >> n;
+      std::string line;
+      std::getline(in, line);
+      for (long long i = 0; i < n; i++) {
+        std::getline(in, line);
+        std::istringstream ls(line);
+        long long id;
+        int type, ntags;
+        ls >> id >> type >> ntags;
+        std::vector<long long> tags(ntags);
+        for (int t = 0; t < ntags; t++) ls >> tags[t];
+        if (type == 1) {
+          long long a, b;
+          ls >> a >> b;
+          lines.push_back(int(a));
+          lines.push_back(int(b));
+          lines.push_back(ntags > 0 ? int(tags[0]) : 0);
+        } else if (type == 2) {
+          long long a, b, c;
+          ls >> a >> b >> c;
+          tris.push_back(a);
+          tris.push_back(b);
+          tris.push_back(c);
+        } else if (type == 15) {
+          // points: ignored (dune-grid's reader skips them as well)
+        } else {
+          err = "unsupported gmsh element type " + std::to_string(type) + " (P1 triangles only)";
+          return false;
+        }
+        if (!ls) {
+          err = "malformed element line";
+          return false;
+        }
+      }
+      have_elems = true;
+    }
+  }
+  if (!have_nodes || !have_elems) {
+    err = "mesh file lacks $Nodes or $Elements";
+    return false;
+  }
+  // vertices numbered in order of first use by a triangle
+  std::vector<int> renum(node_xy.size() / 2, -1);
+  m = Mesh();
+  m.nt = int(tris.size() / 3);
+  m.tri.resize(tris.size());
+  for (size_t i = 0; i < tris.size(); i++) {
+    auto it = node_index.find(tris[i]);
+    if (it == node_index.end()) {
+      err = "triangle references unknown node";
+      return false;
+    }
+    int k = it->second;
+    if (renum[k] < 0) {
+      renum[k] = m.nv++;
+      m.xy.push_back(node_xy[2 * k]);
+      m.xy.push_back(node_xy[2 * k + 1]);
+    }
+    m.tri[i] = renum[k];
+  }
+  m.nb = int(lines.size() / 3);
+  m.bseg.resize(2 * m.nb);
+  m.bgroup.resize(m.nb);
+  for (int s = 0; s < m.nb; s++) {
+    for (int a = 0; a < 2; a++) {
+      auto it = node_index.find(lines[3 * s + a]);
+      if (it == node_index.end() || renum[it->second] < 0) {
+        err = "boundary segment references a node not used by any triangle";
+        return false;
+      }
+      m.bseg[2 * s + a] = renum[it->second];
+    }
+    m.bgroup[s] = lines[3 * s + 2];
+  }
+  return validate(m, err);
+}
+
+// ---------------------------------------------------------------------------------------------
+// red refinement
+// ---------------------------------------------------------------------------------------------
+static Mesh refine_once(const Mesh &m) {
+  Mesh r;
+  std::unordered_map<uint64_t, int> mid;
+  mid.reserve(size_t(m.nt) * 2);
+  r.xy = m.xy;
+  r.nv = m.nv;
+  auto midpoint = [&](int a, int b) {
+    uint64_t k = edge_key(a, b);
+    auto it = mid.find(k);
+    if (it != mid.end()) return it->second;
+    int v = r.nv++;
+    r.xy.push_back(0.5 * (m.xy[2 * a] + m.xy[2 * b]));
+    r.xy.push_back(0.5 * (m.xy[2 * a + 1] + m.xy[2 * b + 1]));
+    mid.emplace(k, v);
+    return v;
+  };
+  r.nt = 4 * m.nt;
+  r.tri.resize(3 * size_t(r.nt));
+  for (int e = 0; e < m.nt; e++) {
+    int a = m.tri[3 * e], b = m.tri[3 * e + 1], c = m.tri[3 * e + 2];
+    int mab = midpoint(a, b), mbc = midpoint(b, c), mca = midpoint(c, a);
+    int ch[4][3] = {{a, mab, mca}, {mab, b, mbc}, {mca, mbc, c}, {mab, mbc, mca}};
+    for (int k = 0; k < 4; k++)
+      for (int j = 0; j < 3; j++) r.tri[3 * (size_t(4) * e + k) + j] = ch[k][j];
+  }
+  r.nb = 2 * m.nb;
+  r.bseg.resize(2 * size_t(r.nb));
+  r.bgroup.resize(r.nb);
+  for (int s = 0; s < m.nb; s++) {
+    int a = m.bseg[2 * s], b = m.bseg[2 * s + 1];
+    int mm = mid.at(edge_key(a, b));
+    r.bseg[4 * s + 0] = a;
+    r.bseg[4 * s + 1] = mm;
+    r.bseg[4 * s + 2] = mm;
+    r.bseg[4 * s + 3] = b;
+    r.bgroup[2 * s] = r.bgroup[2 * s + 1] = m.bgroup[s];
+  }
+  return r;
+}
+
+Mesh refine(const Mesh &m, int k) {
+  Mesh r = m;
+  for (int i = 0; i < k; i++) r = refine_once(r);
+  return r;
+}
+
+bool validate(const Mesh &m, std::string &err) {
+  if (m.nv <= 0 || m.nt <= 0) {
+    err = "empty mesh";
+    return false;
+  }
+  for (int i = 0; i < 3 * m.nt; i++)
+    if (m.tri[i] < 0 || m.tri[i] >= m.nv) {
+      err = "triangle vertex index out of range";
+      return false;
+    }
+  for (int i = 0; i < 2 * m.nb; i++)
+    if (m.bseg[i] < 0 || m.bseg[i] >= m.nv) {
+      err = "boundary segment vertex index out of range";
+      return false;
+    }
+  std::unordered_map<uint64_t, int> ecount;
+  ecount.reserve(size_t(m.nt) * 2);
+  for (int e = 0; e < m.nt; e++) {
+    const int *t = &m.tri[3 * e];
+    if (t[0] == t[1] || t[1] == t[2] || t[0] == t[2]) {
+      err = "degenerate triangle " + std::to_string(e);
+      return false;
+    }
+    double ax = m.xy[2 * t[1]] - m.xy[2 * t[0]], ay = m.xy[2 * t[1] + 1] - m.xy[2 * t[0] + 1];
+    double bx = m.xy[2 * t[2]] - m.xy[2 * t[0]], by = m.xy[2 * t[2] + 1] - m.xy[2 * t[0] + 1];
+    if (ax * by - ay * bx == 0.0) {
+      err = "zero-area triangle " + std::to_string(e);
+      return false;
+    }
+    for (int k = 0; k < 3; k++) ecount[edge_key(t[k], t[(k + 1) % 3])]++;
+  }
+  std::unordered_map<uint64_t, int> seg;
+  for (int s = 0; s < m.nb; s++) {
+    uint64_t k = edge_key(m.bseg[2 * s], m.bseg[2 * s + 1]);
+    auto it = ecount.find(k);
+    if (it == ecount.end() || it->second != 1) {
+      err = "boundary segment " + std::to_string(s) + " is not a boundary edge of the mesh";
+      return false;
+    }
+    if (!seg.emplace(k, s).second) {
+      err = "duplicate boundary segment " + std::to_string(s);
+      return false;
+    }
+  }
+  for (auto &kv : ecount) {
+    if (kv.second > 2) {
+      err = "non-manifold edge";
+      return false;
+    }
+    if (kv.second == 1 && !seg.count(kv.first)) {
+      err = "boundary edge without a boundary segment (UG needs every boundary edge covered)";
+      return false;
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// vertex fans (CCW)
+// ---------------------------------------------------------------------------------------------
+bool build_fans(const Mesh &m, Fans &f, std::string &err) {
+  int nv = m.nv;
+  // per vertex: list of (j, k) = CCW successor pairs (edge i-j is followed by edge i-k)
+  std::vector<int> cnt(nv + 1, 0);
+  for (int e = 0; e < 3 * m.nt; e++) cnt[m.tri[e] + 1]++;
+  for (int v = 0; v < nv; v++) cnt[v + 1] += cnt[v];
+  std::vector<int> pj(cnt[nv]), pk(cnt[nv]);
+  std::vector<int> fill(nv, 0);
+  for (int e = 0; e < m.nt; e++) {
+    int t[3] = {m.tri[3 * e], m.tri[3 * e + 1], m.tri[3 * e + 2]};
+    double ax = m.xy[2 * t[1]] - m.xy[2 * t[0]], ay = m.xy[2 * t[1] + 1] - m.xy[2 * t[0] + 1];
+    double bx = m.xy[2 * t[2]] - m.xy[2 * t[0]], by = m.xy[2 * t[2] + 1] - m.xy[2 * t[0] + 1];
+    if (ax * by - ay * bx < 0) std::swap(t[1], t[2]);
+    for (int a = 0; a < 3; a++) {
+      int i = t[a], j = t[(a + 1) % 3], k = t[(a + 2) % 3];
+      int pos = cnt[i] + fill[i]++;
+      pj[pos] = j;
+      pk[pos] = k;
+    }
+  }
+  f.ptr.assign(nv + 1, 0);
+  f.nbr.clear();
+  f.nbr.reserve(size_t(cnt[nv]) + nv);
+  f.meta.assign(nv, 0);
+  f.max_slots = 0;
+  std::vector<int> seq;
+  std::vector<uint8_t> used;
+  for (int i = 0; i < nv; i++) {
+    int b0 = cnt[i], n = cnt[i + 1] - cnt[i];
+    if (n == 0) {
+      err = "vertex " + std::to_string(i) + " belongs to no triangle";
+      return false;
+    }
+    used.assign(n, 0);
+    seq.clear();
+    uint64_t breaks = 0;
+    bool closed = false;
+    int nfans = 0;
+    int remaining = n;
+    while (remaining > 0) {
+      // start at a pair whose j is nobody's k (open fan start); else any unused pair
+      int start = -1;
+      for (int a = 0; a < n && start < 0; a++) {
+        if (used[a]) continue;
+        bool has_pred = false;
+        for (int b = 0; b < n; b++)
+          if (!used[b] && pk[b0 + b] == pj[b0 + a]) has_pred = true;
+        if (!has_pred) start = a;
+      }
+      bool this_closed = false;
+      if (start < 0) {
+        for (int a = 0; a < n; a++)
+          if (!used[a]) {
+            start = a;
+            break;
+          }
+        this_closed = true;
+      }
+      if (nfans > 0) breaks |= uint64_t(1) << (8 + int(seq.size()));  // no element between
+      int first = pj[b0 + start];
+      seq.push_back(first);
+      int cur = start;
+      while (true) {
+        used[cur] = 1;
+        remaining--;
+        int k = pk[b0 + cur];
+        if (this_closed && k == first) break;
+        seq.push_back(k);
+        int nxt = -1;
+        for (int a = 0; a < n; a++)
+          if (!used[a] && pj[b0 + a] == k) {
+            nxt = a;
+            break;
+          }
+        if (nxt < 0) break;
+        cur = nxt;
+      }
+      if (this_closed) {
+        if (nfans > 0 || remaining > 0) {
+          err = "vertex " + std::to_string(i) + ": closed fan mixed with other fans";
+          return false;
+        }
+        closed = true;
+      }
+      nfans++;
+    }
+    int L = 1 + int(seq.size());
+    if (L > 31 || 8 + L > 63) {
+      err = "vertex " + std::to_string(i) + " has degree " + std::to_string(L - 1) +
+            " (max supported 30)";
+      return false;
+    }
+    // a neighbour appearing twice would mean a malformed fan
+    for (size_t a = 0; a < seq.size(); a++)
+      for (size_t b = a + 1; b < seq.size(); b++)
+        if (seq[a] == seq[b]) {
+          err = "vertex " + std::to_string(i) + ": repeated neighbour in fan";
+          return false;
+        }
+    // breaks were recorded at slot index = seq position of the next fan's first neighbour;
+    // convert: bit (8 + p) means "no element between slot p and slot p+1" with slot = pos + 1
+    uint64_t bmask = 0;
+    for (int p = 1; p <= 30; p++)
+      if ((breaks >> (8 + p)) & 1) bmask |= uint64_t(1) << (8 + p);  // seq pos p == slot p+1
+    // seq position p (0-based) is slot p+1; a break recorded at seq position p sits between
+    // slot p and slot p+1.
+    f.meta[i] = uint64_t(L) | (closed ? (uint64_t(1) << 6) : 0) | bmask;
+    f.max_slots = std::max(f.max_slots, L);
+    for (int v : seq) f.nbr.push_back(v);
+    f.ptr[i + 1] = int(f.nbr.size());
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// boundary data
+// ---------------------------------------------------------------------------------------------
+void dirichlet_mask(const Mesh &m, const Params &p, int nf, int field0, std::vector<uint8_t> &mask) {
+  mask.assign(size_t(m.nv) * nf, 0);
+  for (int s = 0; s < m.nb; s++) {
+    const Surface &S = p.surf[m.bgroup[s]];
+    for (int f = 0; f < nf; f++)
+      if (S.btype(field0 + f) == 0) {
+        mask[size_t(m.bseg[2 * s]) * nf + f] = 1;
+        mask[size_t(m.bseg[2 * s + 1]) * nf + f] = 1;
+      }
+  }
+}
+
+void neumann_load(const Mesh &m, const Params &p, int nf, int field0, std::vector<double> &load) {
+  load.assign(size_t(m.nv) * nf, 0.0);
+  const double t[2] = {0.5 - 0.5 / std::sqrt(3.0), 0.5 + 0.5 / std::sqrt(3.0)};
+  for (int s = 0; s < m.nb; s++) {
+    const Surface &S = p.surf[m.bgroup[s]];
+    int a = m.bseg[2 * s], b = m.bseg[2 * s + 1];
+    double dx = m.xy[2 * b] - m.xy[2 * a], dy = m.xy[2 * b + 1] - m.xy[2 * a + 1];
+    double len = std::sqrt(dx * dx + dy * dy);
+    for (int q = 0; q < 2; q++) {
+      double factor = 0.5 * len;
+      if (p.cylindrical) factor *= (m.xy[2 * a + 1] + t[q] * dy) * 2 * p.pi;
+      for (int f = 0; f < nf; f++) {
+        if (S.btype(field0 + f) == 0) continue;
+        double j = S.flux(field0 + f);
+        load[size_t(a) * nf + f] += j * (1.0 - t[q]) * factor;
+        load[size_t(b) * nf + f] += j * t[q] * factor;
+      }
+    }
+  }
+}
+
+void initial_state(const Mesh &m, const Params &p, const double *phi_pb, double *x0) {
+  // element neighbours and boundary faces (DUNE reference-triangle face order (0,1),(0,2),(1,2))
+  static const int F[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+  std::unordered_map<uint64_t, int> seg, first;
+  seg.reserve(size_t(m.nb) * 2);
+  first.reserve(size_t(m.nt) * 2);
+  for (int s = 0; s < m.nb; s++) seg[edge_key(m.bseg[2 * s], m.bseg[2 * s + 1])] = s;
+  std::vector<int> nbr(3 * size_t(m.nt), -1), bsi(3 * size_t(m.nt), -1);
+  for (int e = 0; e < m.nt; e++)
+    for (int k = 0; k < 3; k++) {
+      uint64_t key = edge_key(m.tri[3 * e + F[k][0]], m.tri[3 * e + F[k][1]]);
+      auto it = first.find(key);
+      if (it == first.end()) {
+        first.emplace(key, 3 * e + k);
+      } else {
+        nbr[3 * size_t(e) + k] = it->second / 3;
+        nbr[it->second] = e;
+      }
+    }
+  for (int e = 0; e < m.nt; e++)
+    for (int k = 0; k < 3; k++)
+      if (nbr[3 * size_t(e) + k] < 0) {
+        auto it = seg.find(edge_key(m.tri[3 * e + F[k][0]], m.tri[3 * e + F[k][1]]));
+        bsi[3 * size_t(e) + k] = it == seg.end() ? -1 : it->second;
+      }
+  auto on_line = [&](int s, double px, double py) {  // Q6: infinite line, tol 1e-9
+    const double *c0 = &m.xy[2 * size_t(m.bseg[2 * s])], *c1 = &m.xy[2 * size_t(m.bseg[2 * s + 1])];
+    double vx = c1[0] - c0[0], vy = c1[1] - c0[1];
+    double n = std::sqrt(vx * vx + vy * vy);
+    vx /= n;
+    vy /= n;
+    double dx = px - c0[0], dy = py - c0[1];
+    double proj = dx * vx + dy * vy;
+    double ex = vx * proj - dx, ey = vy * proj - dy;
+    return std::sqrt(ex * ex + ey * ey) < 1e-9;
+  };
+  int nv = m.nv;
+  for (int e = 0; e < m.nt; e++) {
+    for (int a = 0; a < 3; a++) {
+      int v = m.tri[3 * e + a];
+      double px = m.xy[2 * size_t(v)], py = m.xy[2 * size_t(v) + 1];
+      int pgi = -1;
+      auto consider = [&](int s) {
+        if (s < 0 || !on_line(s, px, py)) return;
+        // Q5: bctype() falls through to minusDiffusionBtype for every component
+        if (pgi == -1 || p.surf[pgi].mb != 0) pgi = m.bgroup[s];
+      };
+      for (int k = 0; k < 3; k++) {
+        int s = bsi[3 * size_t(e) + k];
+        if (s >= 0) {
+          consider(s);
+        } else if (nbr[3 * size_t(e) + k] >= 0) {
+          int o = nbr[3 * size_t(e) + k];
+          for (int k2 = 0; k2 < 3; k2++) consider(bsi[3 * size_t(o) + k2]);
+        }
+      }
+      double phi = phi_pb ? phi_pb[v] : 0.0;
+      const Surface *S = pgi > -1 ? &p.surf[pgi] : nullptr;
+      x0[v] = (S && S->cb == 0) ? S->cpot : phi;
+      x0[nv + v] = (S && S->pb == 0) ? S->pconc : p.c0 * std::exp(-phi);
+      x0[2 * nv + v] = (S && S->mb == 0) ? S->mconc : p.c0 * std::exp(+phi);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// partition, ordering, layout
+// ---------------------------------------------------------------------------------------------
+static void rcb_rec(const Mesh &m, std::vector<int> &ids, size_t lo, size_t hi, int part0,
+                    int nparts, std::vector<int> &part) {
+  if (nparts == 1) {
+    for (size_t i = lo; i < hi; i++) part[ids[i]] = part0;
+    return;
+  }
+  double mn[2] = {1e300, 1e300}, mx[2] = {-1e300, -1e300};
+  for (size_t i = lo; i < hi; i++)
+    for (int d = 0; d < 2; d++) {
+      mn[d] = std::min(mn[d], m.xy[2 * size_t(ids[i]) + d]);
+      mx[d] = std::max(mx[d], m.xy[2 * size_t(ids[i]) + d]);
+    }
+  int dim = (mx[0] - mn[0] >= mx[1] - mn[1]) ? 0 : 1;
+  int pl = nparts / 2;
+  size_t mid = lo + (hi - lo) * size_t(pl) / size_t(nparts);
+  std::nth_element(ids.begin() + lo, ids.begin() + mid, ids.begin() + hi, [&](int a, int b) {
+    double xa = m.xy[2 * size_t(a) + dim], xb = m.xy[2 * size_t(b) + dim];
+    return xa < xb || (xa == xb && a < b);
+  });
+  rcb_rec(m, ids, lo, mid, part0, pl, part);
+  rcb_rec(m, ids, mid, hi, part0 + pl, nparts - pl, part);
+}
+
+void rcb_partition(const Mesh &m, int nparts, std::vector<int> &part) {
+  part.assign(m.nv, 0);
+  if (nparts <= 1) return;
+  std::vector<int> ids(m.nv);
+  std::iota(ids.begin(), ids.end(), 0);
+  rcb_rec(m, ids, 0, ids.size(), 0, nparts, part);
+}
+
+static inline uint64_t morton2(uint32_t x, uint32_t y) {
+  auto spread = [](uint64_t v) {
+    v &= 0xffffffffull;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+  };
+  return spread(x) | (spread(y) << 1);
+}
+
+bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &part, int rank,
+                        int nranks, LocalLayout &L, std::string &err) {
+  L = LocalLayout();
+  L.rank = rank;
+  L.nranks = nranks;
+  int nv = m.nv;
+  std::vector<int> owned;
+  for (int v = 0; v < nv; v++)
+    if (part[v] == rank) owned.push_back(v);
+  if (owned.empty()) {
+    err = "rank " + std::to_string(rank) + " owns no vertices";
+    return false;
+  }
+  // Morton keys on the bounding box of the whole mesh
+  double mn[2] = {1e300, 1e300}, mx[2] = {-1e300, -1e300};
+  for (int v = 0; v < nv; v++)
+    for (int d = 0; d < 2; d++) {
+      mn[d] = std::min(mn[d], m.xy[2 * size_t(v) + d]);
+      mx[d] = std::max(mx[d], m.xy[2 * size_t(v) + d]);
+    }
+  double sc = 4294967295.0 / std::max(mx[0] - mn[0], mx[1] - mn[1]);
+  auto key = [&](int v) {
+    return morton2(uint32_t((m.xy[2 * size_t(v)] - mn[0]) * sc),
+                   uint32_t((m.xy[2 * size_t(v) + 1] - mn[1]) * sc));
+  };
+  std::sort(owned.begin(), owned.end(), [&](int a, int b) {
+    uint64_t ka = key(a), kb = key(b);
+    return ka < kb || (ka == kb && a < b);
+  });
+  // greedy colouring of the owned subgraph in Morton order
+  std::vector<int> color(nv, -1);
+  int ncolors = 0;
+  for (int v : owned) {
+    uint64_t usedc = 0;
+    for (int k = f.ptr[v]; k < f.ptr[v + 1]; k++) {
+      int u = f.nbr[k];
+      if (part[u] == rank && color[u] >= 0) usedc |= uint64_t(1) << color[u];
+    }
+    int c = 0;
+    while ((usedc >> c) & 1) c++;
+    color[v] = c;
+    ncolors = std::max(ncolors, c + 1);
+  }
+  std::stable_sort(owned.begin(), owned.end(), [&](int a, int b) { return color[a] < color[b]; });
+  L.color_ptr.assign(ncolors + 1, 0);
+  for (int v : owned) L.color_ptr[color[v] + 1]++;
+  for (int c = 0; c < ncolors; c++) L.color_ptr[c + 1] += L.color_ptr[c];
+  // inside each colour: windows of 4096 rows sorted by slot count (longest first, stable) so
+  // that SELL chunks carry little padding
+  const int W = 4096;
+  for (int c = 0; c < ncolors; c++)
+    for (int w0 = L.color_ptr[c]; w0 < L.color_ptr[c + 1]; w0 += W) {
+      int w1 = std::min(w0 + W, L.color_ptr[c + 1]);
+      std::stable_sort(owned.begin() + w0, owned.begin() + w1, [&](int a, int b) {
+        return meta_len(f.meta[a]) > meta_len(f.meta[b]);
+      });
+    }
+  L.n_owned = int(owned.size());
+  L.g2l.assign(nv, -1);
+  L.l2g = owned;
+  for (int i = 0; i < L.n_owned; i++) L.g2l[owned[i]] = i;
+  // ghosts: neighbours of owned rows owned elsewhere, ordered by (owner, global id)
+  std::vector<int> ghosts;
+  for (int v : owned)
+    for (int k = f.ptr[v]; k < f.ptr[v + 1]; k++) {
+      int u = f.nbr[k];
+      if (part[u] != rank && L.g2l[u] == -1) {
+        L.g2l[u] = -2;
+        ghosts.push_back(u);
+      }
+    }
+  std::sort(ghosts.begin(), ghosts.end(), [&](int a, int b) {
+    return part[a] < part[b] || (part[a] == part[b] && a < b);
+  });
+  L.n_ghost = int(ghosts.size());
+  for (int i = 0; i < L.n_ghost; i++) {
+    L.g2l[ghosts[i]] = L.n_owned + i;
+    L.l2g.push_back(ghosts[i]);
+  }
+  // halo lists
+  std::vector<int> nbrs;
+  for (int g : ghosts)
+    if (nbrs.empty() || nbrs.back() != part[g]) nbrs.push_back(part[g]);
+  L.nbr_ranks = nbrs;
+  L.recv_ptr.assign(nbrs.size() + 1, 0);
+  for (size_t q = 0, g = 0; q < nbrs.size(); q++) {
+    while (g < ghosts.size() && part[ghosts[g]] == nbrs[q]) g++;
+    L.recv_ptr[q + 1] = int(g);
+  }
+  L.send_ptr.assign(nbrs.size() + 1, 0);
+  for (size_t q = 0; q < nbrs.size(); q++) {
+    std::vector<int> s;
+    for (int v : owned) {
+      bool touches = false;
+      for (int k = f.ptr[v]; k < f.ptr[v + 1] && !touches; k++)
+        touches = part[f.nbr[k]] == nbrs[q];
+      if (touches) s.push_back(v);
+    }
+    std::sort(s.begin(), s.end());
+    for (int v : s) L.send_idx.push_back(L.g2l[v]);
+    L.send_ptr[q + 1] = int(L.send_idx.size());
+  }
+  // SELL-64 layout
+  L.nchunks = (L.n_owned + kChunk - 1) / kChunk;
+  L.chunk_len.assign(L.nchunks, 0);
+  L.chunk_off.assign(L.nchunks + 1, 0);
+  L.rowmeta.assign(L.n_owned, 0);
+  for (int i = 0; i < L.n_owned; i++) {
+    L.rowmeta[i] = f.meta[owned[i]];
+    int c = i / kChunk;
+    L.chunk_len[c] = std::max(L.chunk_len[c], meta_len(L.rowmeta[i]));
+    L.nblocks += meta_len(L.rowmeta[i]);
+  }
+  for (int c = 0; c < L.nchunks; c++) L.chunk_off[c + 1] = L.chunk_off[c] + L.chunk_len[c] * kChunk;
+  L.nslots = L.chunk_off[L.nchunks];
+  L.colidx.assign(L.nslots, 0);
+  for (int c = 0; c < L.nchunks; c++)
+    for (int lane = 0; lane < kChunk; lane++) {
+      int i = c * kChunk + lane;
+      for (int s = 0; s < L.chunk_len[c]; s++) {
+        long long pos = L.chunk_off[c] + (long long)s * kChunk + lane;
+        if (i >= L.n_owned) {
+          L.colidx[pos] = 0;  // rows past the end: never read for results
+          continue;
+        }
+        int v = owned[i];
+        int len = meta_len(L.rowmeta[i]);
+        if (s == 0 || s >= len)
+          L.colidx[pos] = i;
+        else
+          L.colidx[pos] = L.g2l[f.nbr[f.ptr[v] + s - 1]];
+      }
+    }
+  return true;
+}
+
+}  // namespace pnp

@@ -1,0 +1,482 @@
+"""Host-side mirror of the reference's PDELab/ISTL surface over libpnp_amd.so (ctypes).
+
+This is the Python face of the C ABI in include/pnp_capi.h.  It mirrors the reference's
+objects and call sequence (src/stationary_pnp_from_pb.hh:93-369):
+
+    Sysparams / readConfigFile        -> read_config()           (src/sysparams.cc:16-98)
+    GmshReader + UGGrid               -> Mesh.read_gmsh(), Mesh.refine()
+    GridOperator(GFS, CC, LOP)        -> Context.set_operator(OP_PNP | OP_PB | ...)
+    go.residual(u, r) / go.jacobian   -> Context.residual(x) / Context.jacobian(x)
+    ISTLBackend_NOVLP_BCGS_*.apply    -> Context.linear_solve(rhs, prec=...)
+    Newton::apply                     -> Context.newton(u, ...)
+    interpolate(BCExtension)          -> Context.initial_state(phi_pb)
+
+Everything numeric runs in the HIP kernels of libpnp_amd.so; there is no Python or CPU fallback:
+if the shared library is missing or the GPU is absent, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(HERE))          # dune-pnp_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "libpnp_amd.so")
+HEADER = os.path.join(REPO_ROOT, "include", "pnp_capi.h")
+
+OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = \
+    0, -1, -2, -3, -4, -5, -6, -7, -8
+OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
+PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI = range(4)
+PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
+                "jacobi": PREC_JACOBI}
+MAX_SURFACES = 64
+
+
+class PnpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"pnp error {code}: {msg}")
+        self.code = code
+
+
+# ------------------------------------------------------------------------------------------------
+# ctypes structures (must match include/pnp_capi.h)
+# ------------------------------------------------------------------------------------------------
+class _Mesh(C.Structure):
+    _fields_ = [("nv", C.c_int32), ("coords", C.c_void_p), ("nt", C.c_int32),
+                ("tri", C.c_void_p), ("nbseg", C.c_int32), ("bseg", C.c_void_p),
+                ("bseg_group", C.c_void_p)]
+
+
+class _Surface(C.Structure):
+    _fields_ = [("coulomb_btype", C.c_int32), ("coulomb_flux", C.c_double),
+                ("coulomb_potential", C.c_double), ("plus_btype", C.c_int32),
+                ("plus_flux", C.c_double), ("plus_concentration", C.c_double),
+                ("minus_btype", C.c_int32), ("minus_flux", C.c_double),
+                ("minus_concentration", C.c_double)]
+
+
+class _Params(C.Structure):
+    _fields_ = [("l_b", C.c_double), ("c0", C.c_double), ("tau", C.c_double), ("pi", C.c_double),
+                ("cylindrical", C.c_int32), ("n_surfaces", C.c_int32), ("surfaces", C.c_void_p)]
+
+
+class _Config(C.Structure):
+    _fields_ = [("meshfile", C.c_char * 1024), ("n_surfaces", C.c_int32),
+                ("verbosity", C.c_int32), ("cylindrical", C.c_int32),
+                ("linear_solver_iterations", C.c_int32), ("l_b", C.c_double),
+                ("newton_reassemble_threshold", C.c_double), ("newton_reduction", C.c_double),
+                ("newton_min_linear_reduction", C.c_double), ("newton_max_iterations", C.c_int32),
+                ("newton_line_search_max_iteration", C.c_int32), ("c0", C.c_double),
+                ("tau", C.c_double), ("output_freq", C.c_int32), ("n_steps", C.c_int32),
+                ("potential_update_freq", C.c_int32), ("surfaces", _Surface * MAX_SURFACES),
+                ("defaulted", C.c_uint32)]
+
+
+class _Comm(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("size", C.c_int32), ("rccl_unique_id", C.c_void_p)]
+
+
+class _Info(C.Structure):
+    _fields_ = [("nv_global", C.c_int32), ("nv_owned", C.c_int32), ("nv_ghost", C.c_int32),
+                ("nfields", C.c_int32), ("ncolors", C.c_int32), ("nchunks", C.c_int32),
+                ("max_slots", C.c_int32), ("nranks", C.c_int32), ("nblocks", C.c_int64),
+                ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64)]
+
+
+class _OpArgs(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("dt", C.c_double), ("z", C.c_double),
+                ("field", C.c_int32), ("phi", C.c_void_p), ("cp", C.c_void_p),
+                ("cm", C.c_void_p), ("x_old", C.c_void_p)]
+
+
+class _SolveOpts(C.Structure):
+    _fields_ = [("prec", C.c_int32), ("reduction", C.c_double), ("maxit", C.c_int32),
+                ("check_every", C.c_int32)]
+
+
+class _SolveResult(C.Structure):
+    _fields_ = [("converged", C.c_int32), ("iterations", C.c_int32), ("breakdown", C.c_int32),
+                ("it_half", C.c_double), ("defect0", C.c_double), ("defect", C.c_double),
+                ("reduction", C.c_double), ("elapsed", C.c_double)]
+
+
+class _NewtonOpts(C.Structure):
+    _fields_ = [("reduction", C.c_double), ("abs_limit", C.c_double),
+                ("min_linear_reduction", C.c_double), ("maxit", C.c_int32),
+                ("line_search_maxit", C.c_int32), ("linear", _SolveOpts)]
+
+
+class _NewtonResult(C.Structure):
+    _fields_ = [("converged", C.c_int32), ("iterations", C.c_int32),
+                ("linear_iterations", C.c_int32), ("status", C.c_int32),
+                ("first_defect", C.c_double), ("defect", C.c_double), ("elapsed", C.c_double),
+                ("assemble_seconds", C.c_double), ("solve_seconds", C.c_double)]
+
+
+class _Timers(C.Structure):
+    _fields_ = [("assemble_ms", C.c_double), ("spmv_ms", C.c_double), ("prec_ms", C.c_double),
+                ("blas_ms", C.c_double), ("halo_ms", C.c_double), ("allreduce_ms", C.c_double),
+                ("assemble_launches", C.c_int64), ("spmv_launches", C.c_int64),
+                ("prec_launches", C.c_int64), ("blas_launches", C.c_int64)]
+
+
+class _Layout(C.Structure):
+    _fields_ = [("n_owned", C.c_int32), ("n_ghost", C.c_int32), ("ncolors", C.c_int32),
+                ("nchunks", C.c_int32), ("nnbr", C.c_int32), ("max_slots", C.c_int32),
+                ("nslots", C.c_int64), ("nblocks", C.c_int64),
+                ("l2g", C.POINTER(C.c_int32)), ("color_ptr", C.POINTER(C.c_int32)),
+                ("chunk_len", C.POINTER(C.c_int32)), ("chunk_off", C.POINTER(C.c_int32)),
+                ("colidx", C.POINTER(C.c_int32)), ("rowmeta", C.POINTER(C.c_uint64)),
+                ("nbr_ranks", C.POINTER(C.c_int32)), ("recv_ptr", C.POINTER(C.c_int32)),
+                ("send_ptr", C.POINTER(C.c_int32)), ("send_idx", C.POINTER(C.c_int32))]
+
+
+_LIB = None
+
+
+def lib():
+    """Load libpnp_amd.so; raises if it has not been built (no silent fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise PnpError(E_IO, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C "
+                                 f"dune-pnp_amd)")
+        L = C.CDLL(LIB_PATH)
+        L.pnp_last_error.restype = C.c_char_p
+        L.pnp_last_error.argtypes = [C.c_void_p]
+        L.pnp_create.argtypes = [C.POINTER(_Mesh), C.POINTER(_Params), C.c_int32,
+                                 C.POINTER(_Comm), C.POINTER(C.c_void_p)]
+        for name in ("pnp_destroy", "pnp_mesh_free", "pnp_layout_free"):
+            getattr(L, name).restype = None
+            getattr(L, name).argtypes = [C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def _check(rc, ctx=None):
+    if rc != OK:
+        msg = lib().pnp_last_error(ctx)
+        raise PnpError(rc, (msg or b"").decode())
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------------------------------------
+# mesh + config
+# ------------------------------------------------------------------------------------------------
+class Mesh:
+    """Triangle mesh + boundary segments (what GmshReader hands the reference)."""
+
+    def __init__(self, xy, tri, bseg, bgroup):
+        self.xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+        self.tri = np.ascontiguousarray(tri, dtype=np.int32).reshape(-1, 3)
+        self.bseg = np.ascontiguousarray(bseg, dtype=np.int32).reshape(-1, 2)
+        self.bgroup = np.ascontiguousarray(bgroup, dtype=np.int32).reshape(-1)
+
+    nv = property(lambda s: s.xy.shape[0])
+    nt = property(lambda s: s.tri.shape[0])
+    nb = property(lambda s: s.bseg.shape[0])
+
+    def c(self):
+        return _Mesh(self.nv, self.xy.ctypes.data, self.nt, self.tri.ctypes.data, self.nb,
+                     self.bseg.ctypes.data, self.bgroup.ctypes.data)
+
+    @staticmethod
+    def _from_buf(buf):
+        v = _Mesh()
+        _check(lib().pnp_mesh_view(buf, C.byref(v)))
+        xy = np.ctypeslib.as_array(C.cast(v.coords, C.POINTER(C.c_double)), (v.nv * 2,)).copy()
+        tri = np.ctypeslib.as_array(C.cast(v.tri, C.POINTER(C.c_int32)), (v.nt * 3,)).copy()
+        if v.nbseg:
+            bs = np.ctypeslib.as_array(C.cast(v.bseg, C.POINTER(C.c_int32)), (v.nbseg * 2,)).copy()
+            bg = np.ctypeslib.as_array(C.cast(v.bseg_group, C.POINTER(C.c_int32)),
+                                       (v.nbseg,)).copy()
+        else:
+            bs, bg = np.zeros(0, np.int32), np.zeros(0, np.int32)
+        lib().pnp_mesh_free(buf)
+        return Mesh(xy, tri, bs, bg)
+
+    @staticmethod
+    def read_gmsh(path):
+        buf = C.c_void_p()
+        _check(lib().pnp_mesh_read_gmsh(path.encode(), C.byref(buf)))
+        return Mesh._from_buf(buf)
+
+    def refine(self, k):
+        if k == 0:
+            return self
+        buf = C.c_void_p()
+        m = self.c()
+        _check(lib().pnp_mesh_refine(C.byref(m), int(k), C.byref(buf)))
+        return Mesh._from_buf(buf)
+
+
+@dataclass
+class Surface:
+    cb: int = 1
+    cflux: float = 0.0
+    cpot: float = 0.0
+    pb: int = 1
+    pflux: float = 0.0
+    pconc: float = 0.0
+    mb: int = 1
+    mflux: float = 0.0
+    mconc: float = 0.0
+
+
+@dataclass
+class Config:
+    meshfile: str
+    system: dict
+    surfaces: list
+    defaulted_mask: int
+
+
+_SYSTEM_KEYS = ["verbosity", "cylindrical", "l_b", "linearSolverIterations",
+                "newtonReassembleThreshold", "newtonReduction", "newtonMinLinearReduction",
+                "newtonMaxIterations", "newtonLineSearchMaxIteration", "c0", "tau", "outputFreq",
+                "nSteps", "potentialUpdateFreq"]
+
+
+def read_config(path) -> Config:
+    c = _Config()
+    _check(lib().pnp_config_read(str(path).encode(), C.byref(c)))
+    system = {"verbosity": c.verbosity, "cylindrical": c.cylindrical, "l_b": c.l_b,
+              "linearSolverIterations": c.linear_solver_iterations,
+              "newtonReassembleThreshold": c.newton_reassemble_threshold,
+              "newtonReduction": c.newton_reduction,
+              "newtonMinLinearReduction": c.newton_min_linear_reduction,
+              "newtonMaxIterations": c.newton_max_iterations,
+              "newtonLineSearchMaxIteration": c.newton_line_search_max_iteration,
+              "c0": c.c0, "tau": c.tau, "outputFreq": c.output_freq, "nSteps": c.n_steps,
+              "potentialUpdateFreq": c.potential_update_freq, "n_surfaces": c.n_surfaces}
+    surfs = []
+    for i in range(c.n_surfaces):
+        s = c.surfaces[i]
+        surfs.append(Surface(s.coulomb_btype, s.coulomb_flux, s.coulomb_potential, s.plus_btype,
+                             s.plus_flux, s.plus_concentration, s.minus_btype, s.minus_flux,
+                             s.minus_concentration))
+    return Config(c.meshfile.decode(), system, surfs, int(c.defaulted))
+
+
+def defaulted_keys(cfg: Config):
+    return [k for i, k in enumerate(_SYSTEM_KEYS) if (cfg.defaulted_mask >> i) & 1]
+
+
+class Params:
+    def __init__(self, surfaces, l_b=1.0, c0=0.06, tau=1.0, cylindrical=0, pi=3.1415):
+        arr = (_Surface * max(1, len(surfaces)))()
+        for i, s in enumerate(surfaces):
+            arr[i] = _Surface(s.cb, s.cflux, s.cpot, s.pb, s.pflux, s.pconc, s.mb, s.mflux,
+                              s.mconc)
+        self._arr = arr
+        self.c = _Params(l_b, c0, tau, pi, int(cylindrical), len(surfaces),
+                         C.cast(arr, C.c_void_p).value)
+        self.surfaces = surfaces
+
+    @staticmethod
+    def from_config(cfg: Config, pi=3.1415):
+        s = cfg.system
+        return Params(cfg.surfaces, l_b=s["l_b"], c0=s["c0"], tau=s["tau"],
+                      cylindrical=s["cylindrical"], pi=pi)
+
+
+# ------------------------------------------------------------------------------------------------
+# host-only setup
+# ------------------------------------------------------------------------------------------------
+def setup_boundary(mesh: Mesh, params: Params, nfields, field0=0):
+    mask = np.zeros(nfields * mesh.nv, dtype=np.uint8)
+    load = np.zeros(nfields * mesh.nv, dtype=np.float64)
+    m = mesh.c()
+    _check(lib().pnp_setup_boundary(C.byref(m), C.byref(params.c), int(nfields), int(field0),
+                                    _ptr(mask), _ptr(load)))
+    return mask, load
+
+
+def setup_initial_state(mesh: Mesh, params: Params, phi_pb):
+    phi = np.ascontiguousarray(phi_pb, dtype=np.float64)
+    x0 = np.zeros(3 * mesh.nv)
+    m = mesh.c()
+    _check(lib().pnp_setup_initial_state(C.byref(m), C.byref(params.c), _ptr(phi), _ptr(x0)))
+    return x0
+
+
+class Layout:
+    """The partition/local layout pnp_create builds (host-only, for inspection/tests)."""
+
+    def __init__(self, mesh: Mesh, rank=0, nranks=1):
+        buf = C.c_void_p()
+        m = mesh.c()
+        _check(lib().pnp_layout_build(C.byref(m), int(rank), int(nranks), C.byref(buf)))
+        v = _Layout()
+        _check(lib().pnp_layout_view(buf, C.byref(v)))
+
+        def arr(p, n, dt=np.int32):
+            return np.ctypeslib.as_array(p, (n,)).astype(dt).copy() if n else np.zeros(0, dt)
+        self.n_owned, self.n_ghost = v.n_owned, v.n_ghost
+        self.ncolors, self.nchunks, self.max_slots = v.ncolors, v.nchunks, v.max_slots
+        self.nslots, self.nblocks = v.nslots, v.nblocks
+        self.l2g = arr(v.l2g, v.n_owned + v.n_ghost)
+        self.color_ptr = arr(v.color_ptr, v.ncolors + 1)
+        self.chunk_len = arr(v.chunk_len, v.nchunks)
+        self.chunk_off = arr(v.chunk_off, v.nchunks + 1)
+        self.colidx = arr(v.colidx, v.nslots)
+        self.rowmeta = arr(v.rowmeta, v.n_owned, np.uint64)
+        self.nbr_ranks = arr(v.nbr_ranks, v.nnbr)
+        self.recv_ptr = arr(v.recv_ptr, v.nnbr + 1)
+        self.send_ptr = arr(v.send_ptr, v.nnbr + 1)
+        self.send_idx = arr(v.send_idx, int(self.send_ptr[-1]) if v.nnbr else 0)
+        lib().pnp_layout_free(buf)
+
+    def row_len(self, i):
+        return int(self.rowmeta[i] & np.uint64(63))
+
+    def row_cols(self, i):
+        c, lane = divmod(i, 64)
+        L = self.row_len(i)
+        return [int(self.colidx[self.chunk_off[c] + s * 64 + lane]) for s in range(L)]
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU context
+# ------------------------------------------------------------------------------------------------
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(lib().pnp_rccl_unique_id(buf))
+    return buf.raw
+
+
+class Context:
+    """One GPU (one rank): mesh + parameters resident in HBM, one operator at a time."""
+
+    def __init__(self, mesh: Mesh, params: Params, device=0, rank=0, size=1, unique_id=None):
+        self.mesh, self.params = mesh, params
+        self._uid = C.create_string_buffer(unique_id, 128) if unique_id else None
+        comm = _Comm(rank, size, C.cast(self._uid, C.c_void_p).value if self._uid else None)
+        h = C.c_void_p()
+        m = mesh.c()
+        _check(lib().pnp_create(C.byref(m), C.byref(params.c), int(device), C.byref(comm),
+                                C.byref(h)))
+        self.h = h
+        self.nf = 0
+        self.rank, self.size = rank, size
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pnp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ck(self, rc):
+        _check(rc, self.h)
+
+    def info(self):
+        i = _Info()
+        self._ck(lib().pnp_get_info(self.h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in _Info._fields_}
+
+    def set_operator(self, kind, dt=0.0, z=0.0, field=0, phi=None, cp=None, cm=None, x_old=None):
+        keep = [np.ascontiguousarray(a, dtype=np.float64) if a is not None else None
+                for a in (phi, cp, cm, x_old)]
+        a = _OpArgs(kind, dt, z, field, *[None if k is None else k.ctypes.data for k in keep])
+        self._ck(lib().pnp_set_operator(self.h, C.byref(a)))
+        self.nf = 3 if kind in (OP_PNP, OP_PNP_IMPLICIT_EULER) else 1
+        self._op_keep = keep
+
+    def _vec(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.size != self.nf * self.mesh.nv:
+            raise PnpError(E_ARG, f"vector of size {x.size}, expected {self.nf * self.mesh.nv}")
+        return x
+
+    def residual(self, x):
+        x = self._vec(x)
+        r = np.zeros_like(x)
+        self._ck(lib().pnp_residual(self.h, _ptr(x), _ptr(r)))
+        return r
+
+    def jacobian(self, x, export=True):
+        x = self._vec(x)
+        self._ck(lib().pnp_jacobian(self.h, _ptr(x)))
+        if not export:
+            return None
+        import scipy.sparse as sp
+        nnz = C.c_int64()
+        self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), None, None, None))
+        n = self.nf * self.mesh.nv
+        rp = np.zeros(n + 1, dtype=np.int32)
+        col = np.zeros(nnz.value, dtype=np.int32)
+        val = np.zeros(nnz.value, dtype=np.float64)
+        self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), _ptr(rp), _ptr(col), _ptr(val)))
+        return sp.csr_matrix((val, col, rp), shape=(n, n))
+
+    def linear_solve(self, rhs, prec=PREC_NONE, reduction=1e-8, maxit=20000, check_every=8):
+        rhs = self._vec(rhs)
+        z = np.zeros_like(rhs)
+        o = _SolveOpts(prec, reduction, maxit, check_every)
+        r = _SolveResult()
+        rc = lib().pnp_linear_solve(self.h, _ptr(rhs), _ptr(z), C.byref(o), C.byref(r))
+        if rc not in (OK, E_BREAKDOWN):
+            self._ck(rc)
+        return z, {k: getattr(r, k) for k, _ in _SolveResult._fields_}
+
+    def newton(self, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
+               line_search_maxit=500, prec=PREC_NONE, linear_maxit=20000, check_every=8):
+        u = self._vec(u).copy()
+        o = _NewtonOpts(reduction, abs_limit, min_linear_reduction, maxit, line_search_maxit,
+                        _SolveOpts(prec, 0.0, linear_maxit, check_every))
+        r = _NewtonResult()
+        self._ck(lib().pnp_newton(self.h, _ptr(u), C.byref(o), C.byref(r)))
+        return u, {k: getattr(r, k) for k, _ in _NewtonResult._fields_}
+
+    def initial_state(self, phi_pb):
+        phi = np.ascontiguousarray(phi_pb, dtype=np.float64)
+        x0 = np.zeros(3 * self.mesh.nv)
+        self._ck(lib().pnp_initial_state(self.h, _ptr(phi), _ptr(x0)))
+        return x0
+
+    # device-resident hot path ------------------------------------------------------------------
+    def state_set(self, x):
+        x = self._vec(x)
+        self._ck(lib().pnp_state_set(self.h, _ptr(x)))
+
+    def state_get(self):
+        x = np.zeros(self.nf * self.mesh.nv)
+        self._ck(lib().pnp_state_get(self.h, _ptr(x)))
+        return x
+
+    def assemble_state(self, n=1):
+        self._ck(lib().pnp_assemble_state(self.h, int(n)))
+
+    def bicgstab_iterations(self, n, prec=PREC_NONE):
+        r = _SolveResult()
+        self._ck(lib().pnp_bicgstab_iterations(self.h, int(n), int(prec), C.byref(r)))
+        return {k: getattr(r, k) for k, _ in _SolveResult._fields_}
+
+    def timers(self, enable=None, reset=False):
+        if enable is not None:
+            self._ck(lib().pnp_timers_enable(self.h, int(bool(enable))))
+        if reset:
+            self._ck(lib().pnp_timers_reset(self.h))
+        t = _Timers()
+        self._ck(lib().pnp_timers_get(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in _Timers._fields_}
+
+
+def header_symbols():
+    """Function names declared in include/pnp_capi.h."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(pnp_\w+)\s*\(", txt, re.M)))

@@ -1,0 +1,260 @@
+/*
+ * pnp_capi.h — C ABI of the MI355X-native dune-pnp hot path (libpnp_amd.so).
+ *
+ * Replaces, for one GPU per context, what the reference gets from PDELab/ISTL on its hot path
+ * (SURVEY.md §8(b)):
+ *   - the LocalOperators PnpOperator / PnpTOperator / PBOperator / DiffusionOperator /
+ *     DiffusionTOperator / PoissonOperator   (src/pnp_operator.hh:22-325, src/pnp_toperator.hh:
+ *     10-106, src/pb_operator.hh:22-202, src/diffusion_operator.hh:18-178,
+ *     src/diffusion_toperator.hh:15-77, src/poisson_operator.hh:22-209)
+ *     and the GridOperator that loops them: GridOperator::residual / ::jacobian
+ *     (instantiated at src/stationary_pnp_from_pb.hh:165,315-321)            -> pnp_set_operator,
+ *                                                                  pnp_residual, pnp_jacobian
+ *   - the linear solver backends ISTLBackend_NOVLP_BCGS_NOPREC / _SSORk
+ *     (src/stationary_pnp_from_pb.hh:168-169,329-331)                     -> pnp_linear_solve
+ *   - PDELab Newton (src/stationary_pnp_from_pb.hh:355-369)                -> pnp_newton
+ *   - BCType / BCExtension / flux container setup (src/btype.hh:21-53, src/dirichlet_bc.hh:54-123,
+ *     src/stationary_pnp_from_pb.hh:131-156)                              -> pnp_create,
+ *                                                                          pnp_initial_state
+ * and the process-level pieces the driver needs: gmsh input (src/pnp_solver_main.cc:86-91) and
+ * the INI config (src/sysparams.cc:16-98).
+ *
+ * Conventions
+ *   - Every function returns PNP_OK (0) or a negative PNP_E_* code; pnp_last_error() gives the
+ *     message.  No C++ exception crosses this boundary.  "Not converged" is reported in the
+ *     result structs (like ISTL's InverseOperatorResult), not as an error.
+ *   - Vectors at this boundary use the reference's layout: lexicographic [phi | c+ | c-] over the
+ *     mesh's vertex order (GridFunctionSpaceLexicographicMapper, src/stationary_pnp_from_pb.hh:
+ *     228-231), length nfields*nv.  Internally the context keeps a vertex-interleaved, coloured,
+ *     Morton-ordered copy in HBM.
+ *   - Host pointers are borrowed for the duration of the call.  A context is single-thread-affine
+ *     and owns one HIP stream; every call is synchronous on return.
+ *   - Multi-GPU: one process (and one context) per GPU.  pnp_comm carries the RCCL unique id;
+ *     every rank passes the same global mesh and the library partitions it (RCB).
+ */
+#ifndef PNP_CAPI_H
+#define PNP_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNP_CAPI_VERSION 1
+
+enum {
+  PNP_OK = 0,
+  PNP_E_ARG = -1,
+  PNP_E_HIP = -2,
+  PNP_E_RCCL = -3,
+  PNP_E_BREAKDOWN = -4,  /* BiCGSTAB breakdown (ISTLError in the reference) */
+  PNP_E_NOT_CONVERGED = -5,
+  PNP_E_IO = -6,
+  PNP_E_MESH = -7,
+  PNP_E_STATE = -8       /* call order (e.g. no operator set) */
+};
+
+typedef struct pnp_ctx pnp_ctx;
+
+/* ---- mesh ---------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t nv;
+  const double *coords;      /* [nv][2] */
+  int32_t nt;
+  const int32_t *tri;        /* [nt][3], 0-based */
+  int32_t nbseg;
+  const int32_t *bseg;       /* [nbseg][2]; index = boundarySegmentIndex */
+  const int32_t *bseg_group; /* [nbseg]; physical group = boundaryIndexToEntity */
+} pnp_mesh;
+
+typedef struct pnp_mesh_buf pnp_mesh_buf; /* library-owned mesh */
+
+/* GmshReader equivalent (src/pnp_solver_main.cc:86-91): ASCII gmsh 2.x, P1 triangles. */
+int pnp_mesh_read_gmsh(const char *path, pnp_mesh_buf **out);
+/* k levels of uniform red refinement (midpoints; boundary segments split, groups kept) */
+int pnp_mesh_refine(const pnp_mesh *in, int32_t k, pnp_mesh_buf **out);
+/* view into a library-owned mesh (valid until pnp_mesh_free) */
+int pnp_mesh_view(const pnp_mesh_buf *m, pnp_mesh *view);
+void pnp_mesh_free(pnp_mesh_buf *m);
+
+/* ---- configuration (class Sysparams / Surface, src/sysparams.hh:9-48) ------------------------ */
+typedef struct {
+  int32_t coulomb_btype;  /* 0 Dirichlet, 1 Neumann (flux), 2 iPBS (treated as Neumann) */
+  double coulomb_flux, coulomb_potential;
+  int32_t plus_btype;
+  double plus_flux, plus_concentration;
+  int32_t minus_btype;
+  double minus_flux, minus_concentration;
+} pnp_surface;
+
+typedef struct {
+  double l_b, c0, tau;
+  double pi;           /* 3.1415 in the reference (quirk Q4); pass 3.141592653589793 to fix */
+  int32_t cylindrical; /* axisymmetric: r = y, integrands * 2*pi*y */
+  int32_t n_surfaces;
+  const pnp_surface *surfaces;
+} pnp_params;
+
+#define PNP_MAX_SURFACES 64
+typedef struct {
+  char meshfile[1024];   /* resolved relative to the .cfg directory */
+  int32_t n_surfaces, verbosity, cylindrical, linear_solver_iterations;
+  double l_b, newton_reassemble_threshold, newton_reduction, newton_min_linear_reduction;
+  int32_t newton_max_iterations, newton_line_search_max_iteration;
+  double c0, tau;
+  int32_t output_freq, n_steps, potential_update_freq;
+  pnp_surface surfaces[PNP_MAX_SURFACES];
+  uint32_t defaulted;    /* bitmask of [system] keys that were absent and defaulted */
+} pnp_config;
+
+/* Sysparams::readConfigFile (src/sysparams.cc:16-98); absent [system] keys get the documented
+ * defaults of test/pore_pnp/pore.cfg (the reference would abort: SURVEY.md §4). */
+int pnp_config_read(const char *path, pnp_config *out);
+
+/* ---- context ------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t rank, size;          /* this process' rank / number of GPUs (size 1: no RCCL) */
+  const void *rccl_unique_id;  /* 128-byte ncclUniqueId from rank 0 (ignored when size == 1) */
+} pnp_comm;
+
+int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
+               const pnp_comm *comm, pnp_ctx **out);
+void pnp_destroy(pnp_ctx *ctx);
+/* message of the last failure on ctx (or of the last failed pnp_create / mesh call if ctx NULL) */
+const char *pnp_last_error(const pnp_ctx *ctx);
+/* fills a 128-byte buffer with a fresh RCCL unique id (rank 0 calls this, then broadcasts) */
+int pnp_rccl_unique_id(void *out128);
+
+typedef struct {
+  int32_t nv_global, nv_owned, nv_ghost, nfields;
+  int32_t ncolors, nchunks, max_slots, nranks;
+  int64_t nblocks;       /* vertex-pair blocks of the owned rows (V + 2E on one GPU) */
+  int64_t nnz_reduced;   /* scalar nonzeros of the stored block pattern */
+  int64_t nslots;        /* SELL slots incl. padding */
+  int64_t device_bytes;
+} pnp_info;
+int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
+
+/* ---- operators (LocalOperator + GridOperator) ---------------------------------------------- */
+enum {
+  PNP_OP_PNP = 0,            /* PnpOperator (stationary 3-field)                              */
+  PNP_OP_PNP_IMPLICIT_EULER, /* M(u)-M(u_old) + dt*R_pnp(u), M = PnpTOperator (Q2 kept)        */
+  PNP_OP_PB,                 /* PBOperator                                                     */
+  PNP_OP_DIFF,               /* DiffusionOperator, frozen phi, valency z                       */
+  PNP_OP_DIFF_IMPLICIT_EULER,/* DiffusionTOperator mass + dt * DiffusionOperator              */
+  PNP_OP_POISSON             /* PoissonOperator, frozen c+, c-                                 */
+};
+
+typedef struct {
+  int32_t kind;
+  double dt;          /* implicit Euler step (PNP_IMPLICIT_EULER, DIFF_IMPLICIT_EULER) */
+  double z;           /* valency (DIFF*) */
+  int32_t field;      /* DIFF*: which BCType component constrains the ion (1 plus, 2 minus) */
+  const double *phi;  /* DIFF*: frozen potential [nv] */
+  const double *cp, *cm; /* POISSON: frozen concentrations [nv] */
+  const double *x_old;   /* *_IMPLICIT_EULER: previous time level, external layout */
+} pnp_op_args;
+
+int pnp_set_operator(pnp_ctx *ctx, const pnp_op_args *args);
+/* number of fields of the current operator (3 or 1) */
+int pnp_nfields(pnp_ctx *ctx);
+
+/* r = residual(x) with constrained rows zero (GridOperator::residual + constraints);
+ * x, r: host, external layout */
+int pnp_residual(pnp_ctx *ctx, const double *x, double *r);
+/* assemble the Jacobian at x into the context (GridOperator::jacobian + constrained rows ->
+ * identity).  Analytic derivative of the reference's residual (the reference differentiates
+ * numerically: NumericalJacobianVolume, eps 1e-7). */
+int pnp_jacobian(pnp_ctx *ctx, const double *x);
+/* copy the assembled Jacobian out as a CSR matrix in the external layout (sorted columns;
+ * only the stored block pattern, i.e. structurally-zero c+/c- couplings are omitted).
+ * Pass NULL arrays to query nnz first. */
+int pnp_jacobian_export(pnp_ctx *ctx, int64_t *nnz, int32_t *rowptr, int32_t *col, double *val);
+
+/* ---- linear solve (ISTL BiCGSTABSolver semantics) ----------------------------------------- */
+enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3 };
+typedef struct {
+  int32_t prec;       /* SSOR = one multicolour symmetric Gauss-Seidel sweep (k=1, w=1) */
+  double reduction;   /* stop when ||r|| < reduction * ||r0|| (checked every half step) */
+  int32_t maxit;
+  int32_t check_every; /* host convergence poll period in iterations (0: default 8) */
+} pnp_solve_opts;
+typedef struct {
+  int32_t converged, iterations, breakdown; /* iterations = ceil(half-step counter) */
+  double it_half, defect0, defect, reduction, elapsed;
+} pnp_solve_result;
+
+/* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */
+int pnp_linear_solve(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,
+                     pnp_solve_result *res);
+
+/* ---- Newton (PDELab Newton with hackbuschReuskenAcceptBest) -------------------------------- */
+typedef struct {
+  double reduction, abs_limit, min_linear_reduction;
+  int32_t maxit, line_search_maxit;
+  pnp_solve_opts linear;   /* reduction field ignored (set per step by Newton) */
+} pnp_newton_opts;
+typedef struct {
+  int32_t converged, iterations, linear_iterations, status; /* status: PNP_OK, or
+      PNP_E_NOT_CONVERGED (NewtonNotConverged / NewtonLinearSolverError / line search),
+      PNP_E_BREAKDOWN */
+  double first_defect, defect, elapsed, assemble_seconds, solve_seconds;
+} pnp_newton_result;
+int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
+
+/* BCExtension interpolation: x0 (3*nv, external layout) from the PB potential phi_pb (nv). */
+int pnp_initial_state(pnp_ctx *ctx, const double *phi_pb, double *x0);
+
+/* ---- device-resident hot path (benchmarks: inputs already in HBM) --------------------------- */
+/* upload x (external layout) into the context's state vector */
+int pnp_state_set(pnp_ctx *ctx, const double *x);
+int pnp_state_get(pnp_ctx *ctx, double *x);
+/* n fused residual+Jacobian assemblies of the state vector, on the device */
+int pnp_assemble_state(pnp_ctx *ctx, int32_t n);
+/* n BiCGSTAB iterations (no convergence stop) on J z = r of the last assembly */
+int pnp_bicgstab_iterations(pnp_ctx *ctx, int32_t n, int32_t prec, pnp_solve_result *res);
+
+/* per-phase device time from HIP events recorded on the context's stream (enable first) */
+typedef struct {
+  double assemble_ms, spmv_ms, prec_ms, blas_ms, halo_ms, allreduce_ms;
+  int64_t assemble_launches, spmv_launches, prec_launches, blas_launches;
+} pnp_timers;
+int pnp_timers_enable(pnp_ctx *ctx, int32_t on);
+int pnp_timers_get(pnp_ctx *ctx, pnp_timers *t);
+int pnp_timers_reset(pnp_ctx *ctx);
+
+
+/* ---- host-only setup / layout inspection (no GPU needed) ----------------------------------- */
+/* BCType mask (src/btype.hh:21-53) and alpha_boundary Neumann load (e.g. src/pnp_operator.hh:
+ * 276-313) for fields field0 .. field0+nfields-1, lexicographic [f*nv + v] */
+int pnp_setup_boundary(const pnp_mesh *mesh, const pnp_params *params, int32_t nfields,
+                       int32_t field0, uint8_t *mask, double *load);
+/* BCExtension + interpolate (src/dirichlet_bc.hh:54-123), element loop in tri[] order */
+int pnp_setup_initial_state(const pnp_mesh *mesh, const pnp_params *params, const double *phi_pb,
+                            double *x0);
+
+typedef struct pnp_layout_buf pnp_layout_buf;
+typedef struct {
+  int32_t n_owned, n_ghost, ncolors, nchunks, nnbr, max_slots;
+  int64_t nslots, nblocks;
+  const int32_t *l2g;          /* n_owned + n_ghost: local row/column -> global vertex */
+  const int32_t *color_ptr;    /* ncolors + 1 */
+  const int32_t *chunk_len;    /* nchunks */
+  const int32_t *chunk_off;    /* nchunks + 1 */
+  const int32_t *colidx;       /* nslots (SELL-64, see dune-pnp_amd/csrc/kernels.h) */
+  const uint64_t *rowmeta;     /* n_owned: fan length / closed / break bits */
+  const int32_t *nbr_ranks;    /* nnbr */
+  const int32_t *recv_ptr;     /* nnbr + 1: ghost ranges received from each neighbour */
+  const int32_t *send_ptr;     /* nnbr + 1 */
+  const int32_t *send_idx;     /* local owned rows sent to each neighbour */
+} pnp_layout;
+/* the partition + local layout pnp_create would build for (rank, nranks) */
+int pnp_layout_build(const pnp_mesh *mesh, int32_t rank, int32_t nranks, pnp_layout_buf **out);
+int pnp_layout_view(const pnp_layout_buf *b, pnp_layout *view);
+void pnp_layout_free(pnp_layout_buf *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

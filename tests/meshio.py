@@ -134,7 +134,7 @@ DEFAULTS = {  # documented defaults (SURVEY.md §5 "Config / flags"), from test/
     "verbosity": 0, "cylindrical": 0, "l_b": 1.0, "linearSolverIterations": 20000,
     "newtonReassembleThreshold": 0.0, "newtonReduction": 1e-9, "newtonMinLinearReduction": 1e-8,
     "newtonMaxIterations": 50, "newtonLineSearchMaxIteration": 500, "c0": 0.06, "tau": 1.0,
-    "printStiffnessMatrix": 0, "outputFreq": 10, "nSteps": 100, "potentialUpdateFreq": 1,
+    "outputFreq": 10, "nSteps": 100, "potentialUpdateFreq": 1,
 }
 
 

@@ -1,0 +1,239 @@
+"""GPU parity tests (-m gpu): the HIP path through the C ABI against the CPU oracle and the
+committed golden fixtures.  Tolerances:
+  residual                      ||dr||_inf <= 1e-12 ||r||_inf
+  Jacobian vs analytic oracle   |dJ|       <= 1e-12 max|J|
+  Jacobian vs FD oracle         rel        <= 1e-5 (reference-faithful forward differences)
+  converged Newton solution     ||du||_inf <= 1e-6 ||u||_inf, and both reach the reduction
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import meshio
+import oracle_py as O
+import pnp_amd as P
+from conftest import DATA
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+KIND_P = {"pnp": P.OP_PNP, "pnp_ie": P.OP_PNP_IMPLICIT_EULER, "pb": P.OP_PB,
+          "diff": P.OP_DIFF, "poisson": P.OP_POISSON}
+KIND_O = {"pnp": O.OP_PNP, "pnp_ie": O.OP_PNP_IE, "pb": O.OP_PB, "diff": O.OP_DIFF,
+          "poisson": O.OP_POISSON}
+
+
+def golden(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    mesh = P.Mesh(z["xy"], z["tri"], z["bseg"], z["bgroup"])
+    surfs = [P.Surface(int(s[0]), s[1], s[2], int(s[3]), s[4], s[5], int(s[6]), s[7], s[8])
+             for s in z["surfaces"]]
+    l_b, c0, tau, cyl, pi = z["params"]
+    par = P.Params(surfs, l_b=l_b, c0=c0, tau=tau, cylindrical=int(cyl), pi=pi)
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup),
+                    [meshio.Surface(*[getattr(s, f) for f in ("cb", "cflux", "cpot", "pb",
+                                                               "pflux", "pconc", "mb", "mflux",
+                                                               "mconc")]) for s in surfs],
+                    l_b=l_b, c0=c0, tau=tau, cylindrical=int(cyl), pi=pi)
+    return z, mesh, par, orc
+
+
+def set_ops(z, ctx, orc, kind):
+    kw_p, kw_o = {}, {}
+    if kind == "pnp_ie":
+        kw_p = dict(dt=float(z["params"][2]), x_old=z["pnp_ie_x_old"])
+        kw_o = dict(dt=float(z["params"][2]), x_old=np.ascontiguousarray(z["pnp_ie_x_old"]))
+    if kind == "diff":
+        kw_p = dict(z=-1.0, field=2, phi=z["diff_phi"])
+        kw_o = dict(z=-1.0, phi=np.ascontiguousarray(z["diff_phi"]))
+    if kind == "poisson":
+        kw_p = dict(cp=z["poisson_cp"], cm=z["poisson_cm"])
+        kw_o = dict(cp=np.ascontiguousarray(z["poisson_cp"]),
+                    cm=np.ascontiguousarray(z["poisson_cm"]))
+    ctx.set_operator(KIND_P[kind], **kw_p)
+    nf = 3 if kind.startswith("pnp") else 1
+    if kind == "diff":
+        mask = orc.mask(3)[2 * z["xy"].shape[0]:].copy()
+    else:
+        mask = orc.mask(nf)
+    op = orc.operator(KIND_O[kind], flux=orc.flux(), mask=np.ascontiguousarray(mask), **kw_o)
+    return op
+
+
+CASES = [("cylinder_k0", "pnp"), ("cylinder_k0", "pb"), ("pore_small_k0", "pnp"),
+         ("pore_small_k0", "pnp_ie"), ("pore_small_k0", "pb"), ("pore_small_k0", "diff"),
+         ("pore_small_k0", "poisson"), ("pore_pnp_k0", "pnp"), ("pore_pnp_k0", "pb"),
+         ("sphere_k0", "pb"), ("one_wall_k1", "pnp"), ("one_wall_k1", "pb")]
+
+
+@pytest.mark.parametrize("name,kind", CASES)
+def test_residual_parity(name, kind):
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    op = set_ops(z, ctx, orc, kind)
+    x = z[kind + "_x"]
+    r = ctx.residual(x)
+    ro = orc.residual(op, x)
+    scale = np.max(np.abs(ro))
+    assert np.max(np.abs(r - ro)) <= 1e-12 * scale
+    assert np.max(np.abs(r - z[kind + "_r"])) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("name,kind", [c for c in CASES if c[0] != "pore_pnp_k0"])
+def test_jacobian_parity(name, kind):
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    op = set_ops(z, ctx, orc, kind)
+    x = z[kind + "_x"]
+    J = ctx.jacobian(x)
+    Jo = orc.jacobian(op, x, fd=False)
+    scale = abs(Jo).max()
+    assert abs(J - Jo).max() <= 1e-12 * scale
+    Jfd = orc.jacobian(op, x, fd=True)
+    D = (J - Jfd).tocoo()
+    assert np.max(np.abs(D.data)) <= 1e-5 * scale
+    # constrained rows are identity rows
+    mask = op._keep[1] if len(op._keep) > 1 else None
+    Jc = J.tocsr()
+    nf = 3 if kind.startswith("pnp") else 1
+    m = (orc.mask(nf) if kind != "diff" else orc.mask(3)[2 * mesh.nv:])
+    for i in np.nonzero(m)[0][:50]:
+        row = Jc.getrow(i)
+        assert row.nnz >= 1 and np.isclose(row[0, i], 1.0)
+        assert np.allclose(np.delete(row.toarray()[0], i), 0.0)
+
+
+def test_residual_parity_full_size():
+    """Config-3 mesh (test/pore_pnp/pore.msh refined k=4, 2.2 M DOF): residual vs the oracle."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp/pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(4)
+    par = P.Params.from_config(cfg)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup),
+                    [meshio.Surface(*[getattr(q, f) for f in ("cb", "cflux", "cpot", "pb",
+                                                               "pflux", "pconc", "mb", "mflux",
+                                                               "mconc")]) for q in cfg.surfaces],
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    rng = np.random.default_rng(20261015)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    r = ctx.residual(x)
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    ro = orc.residual(op, x)
+    assert np.max(np.abs(r - ro)) <= 1e-12 * np.max(np.abs(ro))
+    # size-independent property: the Jacobian applied to a direction equals the directional
+    # derivative of the (bilinear) residual: R(x + d) - R(x) = J d + O(d^2) (exact for R
+    # quadratic: R(x+d) + R(x-d) - 2R(x) = 2 Q(d))
+    J = ctx.jacobian(x)
+    d = 1e-3 * rng.standard_normal(3 * nv)
+    d[op._keep[1] == 1] = 0.0
+    rp, rm = ctx.residual(x + d), ctx.residual(x - d)
+    lhs = 0.5 * (rp - rm)
+    assert np.max(np.abs(lhs - J @ d)) <= 1e-9 * np.max(np.abs(J @ d))
+
+
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI, P.PREC_SSOR])
+def test_linear_solve_reduces_residual(prec):
+    z, mesh, par, orc = golden("pore_small_k0")
+    ctx = P.Context(mesh, par)
+    op = set_ops(z, ctx, orc, "pnp")
+    x = z["pnp_x"]
+    J = ctx.jacobian(x)
+    rhs = ctx.residual(x)
+    sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-10, maxit=5000)
+    assert res["converged"] == 1, res
+    assert np.linalg.norm(J @ sol - rhs) <= 1.001e-10 * np.linalg.norm(rhs)
+    assert res["iterations"] == int(np.ceil(res["it_half"]))
+    # same system through the oracle's ISTL BiCGSTAB
+    xo, ro = O.bicgstab(orc.jacobian(op, x), rhs, prec=O.PREC_NONE, reduction=1e-10, maxit=5000)
+    assert np.max(np.abs(sol - xo)) <= 1e-6 * np.max(np.abs(xo))
+
+
+def test_bicgstab_nonprec_iteration_semantics_match_oracle():
+    """ISTL half-step semantics: NOPREC iterates match the oracle's iteration count (up to the
+    rounding-induced +-1 at the threshold) and solution."""
+    z, mesh, par, orc = golden("cylinder_k0")
+    ctx = P.Context(mesh, par)
+    op = set_ops(z, ctx, orc, "pnp")
+    x = z["pnp_x"]
+    J = ctx.jacobian(x)
+    rhs = ctx.residual(x)
+    sol, res = ctx.linear_solve(rhs, prec=P.PREC_NONE, reduction=1e-8, maxit=20000,
+                                check_every=1)
+    xo, ro = O.bicgstab(orc.jacobian(op, x), rhs, prec=O.PREC_NONE, reduction=1e-8, maxit=20000)
+    assert ro.converged and res["converged"]
+    assert abs(res["iterations"] - ro.iterations) <= 1
+    assert np.max(np.abs(sol - xo)) <= 1e-5 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("name,prec", [("cylinder_k0", P.PREC_SSOR), ("pore_small_k0", P.PREC_SSOR),
+                                       ("cylinder_k0", P.PREC_NONE)])
+def test_newton_pnp_matches_golden(name, prec):
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(z["newton_pnp_x0"], prec=prec, linear_maxit=20000)
+    assert res["status"] == 0 and res["converged"] == 1, res
+    ref = z["newton_pnp_u"]
+    assert np.max(np.abs(u - ref)) <= 1e-6 * np.max(np.abs(ref))
+    assert res["defect"] <= 1e-9 * res["first_defect"]
+
+
+@pytest.mark.parametrize("name", ["pore_small_k0", "sphere_k0", "one_wall_k1"])
+def test_newton_pb_matches_golden(name):
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PB)
+    u, res = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_SSOR)
+    assert res["converged"] == 1, res
+    ref = z["newton_pb_u"]
+    assert np.max(np.abs(u - ref)) <= 1e-6 * max(np.max(np.abs(ref)), 1e-12)
+
+
+def test_implicit_euler_step_matches_oracle():
+    """One implicit-Euler step of PnpOperator + PnpTOperator (config 4 semantics)."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    x_old = z["newton_pnp_x0"]
+    dt = 1.0
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=dt, x_old=x_old)
+    u, res = ctx.newton(x_old, prec=P.PREC_SSOR, reduction=1e-10)
+    assert res["converged"] == 1, res
+    op = orc.operator(O.OP_PNP_IE, flux=orc.flux(), mask=orc.mask(3), dt=dt,
+                      x_old=np.ascontiguousarray(x_old))
+    uo, ro = orc.newton(op, x_old, prec=O.PREC_ILU0, reduction=1e-10)
+    assert ro.converged
+    assert np.max(np.abs(u - uo)) <= 1e-6 * np.max(np.abs(uo))
+
+
+def test_nonprec_stationary_pnp_reports_linear_failure():
+    """Like the reference (NOPREC BiCGSTAB inside Newton, src/stationary_pnp_from_pb.hh:329-369)
+    the product reports the linear solver's failure instead of returning garbage."""
+    z, mesh, par, orc = golden("pore_pnp_k0")
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(z["pnp_x"], prec=P.PREC_NONE, linear_maxit=50)
+    assert res["status"] == P.E_NOT_CONVERGED and res["converged"] == 0
+
+
+def test_bench_path_fixed_iterations():
+    z, mesh, par, orc = golden("pore_pnp_k0")
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(z["pnp_x"])
+    ctx.timers(enable=True, reset=True)
+    ctx.assemble_state(3)
+    res = ctx.bicgstab_iterations(10, P.PREC_SSOR)
+    t = ctx.timers()
+    assert res["iterations"] == 10
+    assert t["assemble_launches"] == 3 and t["assemble_ms"] > 0
+    assert np.isfinite(res["defect"]) and res["defect"] < res["defect0"]
+    info = ctx.info()
+    assert info["nblocks"] == info["nv_owned"] + 2 * len(
+        set(map(tuple, np.sort(np.concatenate([mesh.tri[:, [0, 1]], mesh.tri[:, [1, 2]],
+                                               mesh.tri[:, [0, 2]]]), axis=1).tolist())))

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Guarded GPU session: each GPU step under its own time limit; a crash/abort/timeout in any
+# step ends the script (no further GPU work), ordinary test failures do not.
+# usage: tools/gpu_run.sh <tag> <step>...   steps: tests smoke bench prof
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139|-6|-11) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
+for step in "$@"; do
+  case $step in
+    tests)  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 600 -rf > "$OUT/tests.log" 2>&1; rc=$? ;;
+    smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$? ;;
+    bench)  timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1; rc=$? ;;
+    benchq) timeout -k 10 600 python bench.py --no-cpu --steps 10 > "$OUT/bench.log" 2>&1; rc=$? ;;
+    prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
+    *) echo "unknown step $step"; rc=0 ;;
+  esac
+  echo "step $step rc=$rc" | tee -a "$OUT/steps.txt"
+  tail -5 "$OUT/$step.log" 2>/dev/null
+  if fatal $rc; then echo "fatal rc=$rc in $step: stopping"; exit $rc; fi
+done
+exit 0
