@@ -150,6 +150,33 @@ class Problem:
         L.orc_csr_free(C.byref(A))
         return sp.csr_matrix((val, col, rp), shape=(n, n))
 
+    def time_fd_assembly(self, op, x, seconds):
+        """Reference-faithful assembly timing: PnpOperator residual + NumericalJacobianVolume
+        forward-difference Jacobian scattered into a prebuilt CSR (the BCRS pattern is built
+        once, like `M m(go)` at src/stationary_pnp_from_pb.hh:318-319). Returns (s/assembly, A)."""
+        import time
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        r = np.zeros(self.nfields(op) * self.nv)
+        A = OrcCsr()
+        L = lib()
+        L.orc_csr_pattern(C.byref(self.m), self.nfields(op), C.byref(A))
+        n, t0 = 0, time.perf_counter()
+        while True:
+            L.orc_op_residual(C.byref(self.m), C.byref(self.p), C.byref(op), _p(x), _p(r))
+            L.orc_op_jacobian(C.byref(self.m), C.byref(self.p), C.byref(op), _p(x), 1,
+                              C.byref(A))
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = (time.perf_counter() - t0) / n
+        import scipy.sparse as sp
+        rp = np.ctypeslib.as_array(A.rowptr, shape=(A.n + 1,)).copy()
+        col = np.ctypeslib.as_array(A.col, shape=(A.nnz,)).copy()
+        val = np.ctypeslib.as_array(A.val, shape=(A.nnz,)).copy()
+        n = A.n
+        L.orc_csr_free(C.byref(A))
+        return dt, sp.csr_matrix((val, col, rp), shape=(n, n))
+
     def newton(self, op, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
                line_search_maxit=500, linear_maxit=20000, prec=PREC_NONE, fd=False):
         u = np.ascontiguousarray(u, dtype=np.float64).copy()

@@ -154,9 +154,10 @@ def test_linear_solve_reduces_residual(prec):
     assert np.max(np.abs(sol - xo)) <= 1e-6 * np.max(np.abs(xo))
 
 
-def test_bicgstab_nonprec_iteration_semantics_match_oracle():
-    """ISTL half-step semantics: NOPREC iterates match the oracle's iteration count (up to the
-    rounding-induced +-1 at the threshold) and solution."""
+def test_bicgstab_nonprec_matches_oracle_on_long_run():
+    """NOPREC over ~200 iterations: the Krylov iterates depend on summation order (the product
+    sums dots in a different order and DOF layout than the oracle), so iteration counts agree
+    only statistically; the converged solutions agree."""
     z, mesh, par, orc = golden("cylinder_k0")
     ctx = P.Context(mesh, par)
     op = set_ops(z, ctx, orc, "pnp")
@@ -167,8 +168,35 @@ def test_bicgstab_nonprec_iteration_semantics_match_oracle():
                                 check_every=1)
     xo, ro = O.bicgstab(orc.jacobian(op, x), rhs, prec=O.PREC_NONE, reduction=1e-8, maxit=20000)
     assert ro.converged and res["converged"]
-    assert abs(res["iterations"] - ro.iterations) <= 1
+    assert abs(res["iterations"] - ro.iterations) <= 0.25 * ro.iterations
     assert np.max(np.abs(sol - xo)) <= 1e-5 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("reduction", [1e-3, 1e-6, 1e-9])
+def test_bicgstab_half_step_counting_matches_istl(reduction):
+    """Well-conditioned system (implicit-Euler diffusion with a small step: mass dominated), few
+    iterations, so rounding cannot move the stopping point: the ISTL half-step counter, the
+    iteration count and the convergence flag match the oracle exactly."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    nv = mesh.nv
+    phi = np.ascontiguousarray(z["diff_phi"])
+    xo_ = np.ascontiguousarray(z["pnp_ie_x_old"][nv:2 * nv])
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_DIFF_IMPLICIT_EULER, dt=1e-3, z=1.0, field=1, phi=phi, x_old=xo_)
+    op = orc.operator(O.OP_DIFF_IE, flux=orc.flux(), mask=np.ascontiguousarray(orc.mask(3)[nv:2 * nv]),
+                      dt=1e-3, z=1.0, phi=phi, x_old=xo_)
+    x = xo_.copy()
+    J = ctx.jacobian(x)
+    rhs = ctx.residual(x) + 0.01
+    rhs[op._keep[1] == 1] = 0.0
+    sol, res = ctx.linear_solve(rhs, prec=P.PREC_NONE, reduction=reduction, maxit=1000,
+                                check_every=1)
+    xo, ro = O.bicgstab(orc.jacobian(op, x), rhs, prec=O.PREC_NONE, reduction=reduction,
+                        maxit=1000)
+    assert res["converged"] == ro.converged == 1
+    assert res["it_half"] == ro.it_half
+    assert res["iterations"] == ro.iterations
+    assert np.max(np.abs(sol - xo)) <= 1e-9 * np.max(np.abs(xo))
 
 
 @pytest.mark.parametrize("name,prec", [("cylinder_k0", P.PREC_SSOR), ("pore_small_k0", P.PREC_SSOR),
