@@ -15,6 +15,8 @@
 // is exact (PnpOperator / PoissonOperator integrands are polynomials of degree <= 3, also with
 // the cylindrical 2*PI*y weight); PBOperator (sinh) and the PnpTOperator mass (a cubic under the
 // order-2 rule, src/pnp_toperator.hh:26) use the reference's quadrature points explicitly.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace pnp {
@@ -231,11 +233,11 @@ __device__ __forceinline__ void store_block(double *__restrict__ vb, int s, cons
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
-template <int OP, int JAC>
-__global__ __launch_bounds__(256) void k_assemble(DevLayout L, AsmArgs a) {
+template <int OP, int JAC, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
   constexpr int NF = T::NF, NV = T::NV;
-  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * blockDim.x + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = L.chunk_off[chunk];
@@ -262,38 +264,53 @@ __global__ __launch_bounds__(256) void k_assemble(DevLayout L, AsmArgs a) {
 #pragma unroll
   for (int v = 0; v < NV; v++) D[v] = P[v] = F[v] = 0;
 
+  // Software-pipelined fan walk.  Element s is (i, v_s, v_t) with t = s+1 (or 1 when a closed
+  // fan wraps); consecutive elements share v_{s+1}, so each neighbour's data (coordinates, NF
+  // dofs, frozen fields) is gathered once, one element ahead, and its column index two ahead.
+  auto next_slot = [&](int s) { return (s + 1 < len) ? s + 1 : (closed ? 1 : -1); };
+  auto load_nb = [&](int j, double2 &p, double *u, double &a0, double &a1) {
+    p = reinterpret_cast<const double2 *>(L.xy)[j];
+#pragma unroll
+    for (int f = 0; f < NF; f++) u[f] = a.x[size_t(j) * NF + f];
+    if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) a0 = a.aux0[j];
+    if constexpr (OP == OP_POISSON) a1 = a.aux1[j];
+  };
+  double2 pc, pn;               // coordinates of v_s (current) and v_t (next)
+  double uc[NF], un[NF];        // dofs of v_s, v_t
+  double ac0 = 0, ac1 = 0, an0 = 0, an1 = 0;
+  load_nb(cix[1 * kRows], pc, uc, ac0, ac1);
+  {
+    const int t1 = next_slot(1);
+    if (t1 > 0) load_nb(cix[t1 * kRows], pn, un, an0, an1);
+  }
+  int jn = -1;  // column index of the slot needed two elements ahead
+  {
+    const int t2 = next_slot(1) > 0 ? next_slot(next_slot(1)) : -1;
+    if (t2 > 0 && next_slot(1) != 1) jn = cix[t2 * kRows];
+  }
   for (int s = 1; s < len; ++s) {
-    const int t = (s + 1 < len) ? s + 1 : (closed ? 1 : -1);
+    const int t = next_slot(s);
+    // prefetch the data of the slot the next element needs, and the index after that
+    const int tn = (t > 0 && t != 1) ? next_slot(t) : -1;
+    double2 pp = pn;
+    double up[NF];
+    double ap0 = 0, ap1 = 0;
+    if (tn > 0) {
+      load_nb(jn, pp, up, ap0, ap1);
+      const int tnn = tn != 1 ? next_slot(tn) : -1;
+      jn = tnn > 0 ? cix[tnn * kRows] : -1;
+    }
     const bool elem = t > 0 && !((meta >> (8 + s)) & 1);
     if (elem) {
-      const int b = cix[s * kRows], c = cix[t * kRows];
-      const double2 pb2 = reinterpret_cast<const double2 *>(L.xy)[b];
-      const double2 pc2 = reinterpret_cast<const double2 *>(L.xy)[c];
-      double ub[NF], uc[NF];
-#pragma unroll
-      for (int f = 0; f < NF; f++) {
-        ub[f] = a.x[size_t(b) * NF + f];
-        uc[f] = a.x[size_t(c) * NF + f];
-      }
-      double ab = 0, ac = 0, qb = 0, qc = 0;
-      if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) {
-        ab = a.aux0[b];
-        ac = a.aux0[c];
-      }
-      if constexpr (OP == OP_POISSON) {
-        qb = a.aux1[b];
-        qc = a.aux1[c];
-      }
       Geo G;
-      geometry(pi2.x, pi2.y, pb2.x, pb2.y, pc2.x, pc2.y, G);
-      double Cs[NV], Ct[NV];
+      geometry(pi2.x, pi2.y, pc.x, pc.y, pn.x, pn.y, G);
+      double Ct[NV];
 #pragma unroll
-      for (int v = 0; v < NV; v++) Cs[v] = Ct[v] = 0;
-      element<OP, JAC>(a, G, pi2.y, pb2.y, pc2.y, ui, ub, uc, ai, ab, ac, aq, qb, qc, R, D, Cs,
+      for (int v = 0; v < NV; v++) Ct[v] = 0;
+      // P (pending block of slot s) receives this element's (i, v_s) contribution directly
+      element<OP, JAC>(a, G, pi2.y, pc.y, pn.y, ui, uc, un, ai, ac0, an0, aq, ac1, an1, R, D, P,
                        Ct);
       if constexpr (JAC) {
-#pragma unroll
-        for (int v = 0; v < NV; v++) P[v] += Cs[v];
         if (s == 1 && closed) {
 #pragma unroll
           for (int v = 0; v < NV; v++) F[v] = P[v];
@@ -307,6 +324,19 @@ __global__ __launch_bounds__(256) void k_assemble(DevLayout L, AsmArgs a) {
       store_block<OP>(vb, s, P, dm, false);
 #pragma unroll
       for (int v = 0; v < NV; v++) P[v] = 0;
+    }
+    // rotate: v_t becomes the current neighbour, the prefetched one the next
+    pc = pn;
+#pragma unroll
+    for (int f = 0; f < NF; f++) uc[f] = un[f];
+    ac0 = an0;
+    ac1 = an1;
+    if (tn > 0) {
+      pn = pp;
+#pragma unroll
+      for (int f = 0; f < NF; f++) un[f] = up[f];
+      an0 = ap0;
+      an1 = ap1;
     }
   }
   if constexpr (JAC) {
@@ -370,12 +400,20 @@ __global__ __launch_bounds__(256) void k_mass_apply(DevLayout L, double tau, dou
 hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
   dim3 grid((L.n_owned + 255) / 256), block(256);
-#define PNP_ASM_CASE(OPK)                                                      \
-  case OPK:                                                                    \
-    if (a.jac)                                                                 \
-      hipLaunchKernelGGL((k_assemble<OPK, 1>), grid, block, 0, s, L, a);       \
-    else                                                                       \
-      hipLaunchKernelGGL((k_assemble<OPK, 0>), grid, block, 0, s, L, a);       \
+  // occupancy variant (A/B knob, PNP_ASM_WAVES=3|4): 4 waves/SIMD caps the fused PNP kernel at
+  // 128 VGPRs (a few bytes of spill), 3 lets it keep ~134 without spilling
+  static const int waves = [] {
+    const char *e = getenv("PNP_ASM_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 3;
+  }();
+#define PNP_ASM_CASE(OPK)                                                          \
+  case OPK:                                                                        \
+    if (a.jac && waves == 3)                                                       \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 3>), grid, block, 0, s, L, a);        \
+    else if (a.jac)                                                                \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 4>), grid, block, 0, s, L, a);        \
+    else                                                                           \
+      hipLaunchKernelGGL((k_assemble<OPK, 0, 4>), grid, block, 0, s, L, a);        \
     break;
   switch (a.kind) {
     PNP_ASM_CASE(OP_PNP)

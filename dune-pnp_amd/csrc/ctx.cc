@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -64,7 +65,8 @@ struct pnp_ctx {
   pnp::LocalLayout L;
   pnp::DevLayout dl;
 
-  DBuf<int> d_chunk_len, d_chunk_off, d_colidx, d_l2g, d_send_idx;
+  DBuf<int> d_chunk_len, d_chunk_off, d_colidx, d_l2g, d_send_idx, d_color_idx;
+  DBuf<uint8_t> d_rowcolor;
   DBuf<uint64_t> d_rowmeta;
   DBuf<double> d_xy;
 
@@ -81,8 +83,12 @@ struct pnp_ctx {
   DBuf<pnp::Scalars> S;
   pnp::Scalars *hS = nullptr;  // pinned host mirror
 
-  // timers
+  // timers / debugging
   bool timing = false;
+  bool debug_trace = [] {
+    const char *e = std::getenv("PNP_DEBUG_BICGSTAB");
+    return e && std::atoi(e) != 0;
+  }();
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[T_NCAT];
   std::vector<hipEvent_t> ev_pool;
   double t_ms[T_NCAT] = {0};
@@ -183,6 +189,21 @@ struct pnp_ctx {
       return fail(PNP_E_RCCL, "ncclAllReduce");
     te(T_ALLRED, t0);
     return PNP_OK;
+  }
+
+  // S->red = sum of partials (all ranks), then the derive step of BiCGSTAB stage `stage`
+  int reduce_derive(int np, int k, int stage) {
+    hipError_t e;
+    if (nranks == 1) {
+      e = pnp::launch_reduce(partials.p, np, k, S.p, stream, stage);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
+    }
+    e = pnp::launch_reduce(partials.p, np, k, S.p, stream);
+    if (e != hipSuccess) return hipfail(e, "reduce");
+    int rc = allreduce_red(k);
+    if (rc) return rc;
+    e = pnp::launch_derive(S.p, stage, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "derive");
   }
 
   // norm over owned rows of a vector, synchronous
@@ -290,13 +311,10 @@ struct pnp_ctx {
     if (e != hipSuccess) return hipfail(e, "bicgstab scalars");
     hipEvent_t t0 = tb(T_BLAS);
     e = pnp::launch_dot(n, rs.p, rs.p, 0, partials.p, stream);
-    if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 1, S.p, stream);
     if (e != hipSuccess) return hipfail(e, "bicgstab norm0");
-    te(T_BLAS, t0);
-    int rc = allreduce_red(1);
+    int rc = reduce_derive(np, 1, 0);
     if (rc) return rc;
-    e = pnp::launch_derive(S.p, 0, stream);
-    if (e != hipSuccess) return hipfail(e, "derive");
+    te(T_BLAS, t0);
     int maxit = fixed > 0 ? fixed : o.maxit;
     int check = o.check_every > 0 ? o.check_every : 8;
     if (fixed > 0) check = fixed;
@@ -317,19 +335,15 @@ struct pnp_ctx {
       if ((rc = halo(const_cast<double *>(yin), nf))) return rc;
       t0 = tb(T_SPMV);
       e = pnp::launch_spmv(dl, nf, pat, vals.p, yin, v.p, 1, rt.p, partials.p, &nsp, stream);
-      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, nsp, 1, S.p, stream);
       if (e != hipSuccess) return hipfail(e, "spmv h");
       te(T_SPMV, t0);
-      if ((rc = allreduce_red(1))) return rc;
-      if ((e = pnp::launch_derive(S.p, 1, stream)) != hipSuccess) return hipfail(e, "derive");
+      if ((rc = reduce_derive(nsp, 1, 1))) return rc;
       // x += alpha y ; r -= alpha v ; ||r||
       t0 = tb(T_BLAS);
       e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials.p, stream);
-      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 1, S.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (1)");
+      if ((rc = reduce_derive(np, 1, 2))) return rc;
       te(T_BLAS, t0);
-      if ((rc = allreduce_red(1))) return rc;
-      if ((e = pnp::launch_derive(S.p, 2, stream)) != hipSuccess) return hipfail(e, "derive");
       // y = M^{-1} r ; t = A y ; <t,r>, <t,t>
       const double *yin2 = rs.p;
       if (prec != PNP_PREC_NONE) {
@@ -339,19 +353,24 @@ struct pnp_ctx {
       if ((rc = halo(const_cast<double *>(yin2), nf))) return rc;
       t0 = tb(T_SPMV);
       e = pnp::launch_spmv(dl, nf, pat, vals.p, yin2, t.p, 2, rs.p, partials.p, &nsp, stream);
-      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, nsp, 2, S.p, stream);
       if (e != hipSuccess) return hipfail(e, "spmv t");
       te(T_SPMV, t0);
-      if ((rc = allreduce_red(2))) return rc;
-      if ((e = pnp::launch_derive(S.p, 3, stream)) != hipSuccess) return hipfail(e, "derive");
+      if ((rc = reduce_derive(nsp, 2, 3))) return rc;
       // x += omega y ; r -= omega t ; ||r||, <rt, r>
       t0 = tb(T_BLAS);
       e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
-      if (e == hipSuccess) e = pnp::launch_reduce(partials.p, np, 2, S.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (2)");
+      if ((rc = reduce_derive(np, 2, 4))) return rc;
       te(T_BLAS, t0);
-      if ((rc = allreduce_red(2))) return rc;
-      if ((e = pnp::launch_derive(S.p, 4, stream)) != hipSuccess) return hipfail(e, "derive");
+      if (debug_trace) {
+        e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        std::fprintf(stderr,
+                     "bicgstab it=%d it_half=%.1f rho=%.6e rho_new=%.6e alpha=%.6e omega=%.6e "
+                     "h=%.6e norm=%.6e done=%d bd=%d\n",
+                     k + 1, hS->it_half, hS->rho, hS->rho_new, hS->alpha, hS->omega, hS->h,
+                     hS->norm, hS->done, hS->breakdown);
+      }
       if ((k + 1) % check == 0 || k + 1 == maxit) {
         e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipStreamSynchronize(stream);
@@ -564,9 +583,15 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = up(c->d_chunk_off, L.chunk_off, "chunk_off")) ||
       (rc = up(c->d_colidx, L.colidx, "colidx")) || (rc = up(c->d_rowmeta, L.rowmeta, "rowmeta")) ||
       (rc = up(c->d_xy, xy, "xy")) || (rc = up(c->d_l2g, L.l2g, "l2g")) ||
-      (rc = up(c->d_send_idx, L.send_idx, "send_idx"))) {
+      (rc = up(c->d_send_idx, L.send_idx, "send_idx")) ||
+      (rc = up(c->d_color_idx, L.color_idx, "color_idx")) ||
+      (rc = up(c->d_rowcolor, L.rowcolor, "rowcolor"))) {
     g_err = c->err;
     return rc;
+  }
+  {
+    const char *e = getenv("PNP_XCD_REMAP");
+    c->dl.xcd_remap = (e && atoi(e) == 1) ? 1 : 0;  // measured: off for assembly / SpMV
   }
   c->dl.n_owned = L.n_owned;
   c->dl.n_local = nloc;
@@ -577,6 +602,8 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   c->dl.colidx = c->d_colidx.p;
   c->dl.rowmeta = c->d_rowmeta.p;
   c->dl.xy = c->d_xy.p;
+  c->dl.color_idx = c->d_color_idx.p;
+  c->dl.rowcolor = c->d_rowcolor.p;
   // buffers
   size_t nv3 = 3 * size_t(nloc);
   auto al = [&](auto &buf, size_t n, const char *what) -> int {
@@ -591,7 +618,10 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
       (rc = al(c->ext, 3 * size_t(c->mesh.nv), "ext")) ||
       (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
-      (rc = al(c->partials, 2 * 4096, "partials")) || (rc = al(c->S, 2, "scalars")) ||
+      (rc = al(c->partials,
+               2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
+                                    size_t((L.n_owned + 255) / 256)) + 64,
+               "partials")) || (rc = al(c->S, 2, "scalars")) ||
       (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
       (rc = al(c->cvec, 3 * size_t(L.n_owned), "cvec")) || (rc = al(c->aux0, nloc, "aux0")) ||
       (rc = al(c->aux1, nloc, "aux1"))) {
@@ -1082,6 +1112,8 @@ extern "C" int pnp_layout_view(const pnp_layout_buf *b, pnp_layout *v) {
   v->nblocks = L.nblocks;
   v->l2g = L.l2g.data();
   v->color_ptr = L.color_ptr.data();
+  v->color_idx = L.color_idx.data();
+  v->rowcolor = L.rowcolor.data();
   v->chunk_len = L.chunk_len.data();
   v->chunk_off = L.chunk_off.data();
   v->colidx = L.colidx.data();

@@ -19,6 +19,16 @@ namespace pnp {
 
 constexpr int kRows = 64;  // rows per SELL chunk = one wavefront
 
+// XCD-aware block remap (cdna_hip_programming.md T1): consecutive workgroups are dealt
+// round-robin over the 8 XCDs; remap so that each XCD works on one contiguous 1/8 of the rows and
+// neighbouring rows' gathered data (x, coordinates) is reused from that XCD's L2.  Bijective for
+// any grid size.  Speed only: correctness never depends on placement.
+__device__ __forceinline__ int xcd_block(int b, int nwg, int on = 1) {
+  if (!on) return b;
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
 // ---- operator kinds / block patterns ----------------------------------------------------------
 enum OpKind : int {
   OP_PNP = 0,
@@ -52,11 +62,14 @@ __host__ __device__ constexpr int pat_index(int mask, int f, int g) {
 // ---- device views ----------------------------------------------------------------------------
 struct DevLayout {
   int n_owned = 0, n_local = 0, nchunks = 0, ncolors = 0;
+  int xcd_remap = 0;                // A/B knob (PNP_XCD_REMAP): see xcd_block
   const int *chunk_len = nullptr;
   const int *chunk_off = nullptr;   // nchunks + 1
   const int *colidx = nullptr;
   const uint64_t *rowmeta = nullptr;
   const double *xy = nullptr;       // [n_local][2]
+  const int *color_idx = nullptr;   // rows of each colour (see mesh.h LocalLayout)
+  const uint8_t *rowcolor = nullptr;
 };
 
 struct AsmArgs {
@@ -99,7 +112,7 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
 // preconditioners: v = M^{-1} d (v over owned rows)
 hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
                          double *v, hipStream_t s);
-hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
+hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,  // NOLINT
                       const double *vals, const double *d, double *v, hipStream_t s);
 
 // BLAS-1 over n = n_owned*nf entries
@@ -114,8 +127,10 @@ hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x,
 // partials of <a,b> (and <a,a> if two)
 hipError_t launch_dot(long long n, const double *a, const double *b, int two, double *partials,
                       hipStream_t s);
-// sum partials[nparts][k] -> S->red[0..k) (deterministic order)
-hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s);
+// sum partials[nparts][k] -> S->red[0..k) (deterministic order); derive_stage >= 0 also runs
+// the derive step in the same launch (single GPU: no allreduce in between)
+hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
+                         int derive_stage = -1);
 // derive scalars after a reduction; stage: 0 init (red: <r,r>), 1 after h, 2 after first half
 // norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>)
 hipError_t launch_derive(Scalars *S, int stage, hipStream_t s);

@@ -547,20 +547,23 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
     color[v] = c;
     ncolors = std::max(ncolors, c + 1);
   }
+  // colour-major order (rows of one colour contiguous, Morton order inside a colour), in
+  // windows of kOrderBlock rows sorted by slot count (longest first) so that SELL chunks carry
+  // little padding.  (A block-major order -- spatial blocks, colours inside -- was measured on
+  // MI355X: assembly -3 %, SpMV +-0, multicolour sweeps +12 %; colour-major kept.)
   std::stable_sort(owned.begin(), owned.end(), [&](int a, int b) { return color[a] < color[b]; });
   L.color_ptr.assign(ncolors + 1, 0);
   for (int v : owned) L.color_ptr[color[v] + 1]++;
   for (int c = 0; c < ncolors; c++) L.color_ptr[c + 1] += L.color_ptr[c];
-  // inside each colour: windows of 4096 rows sorted by slot count (longest first, stable) so
-  // that SELL chunks carry little padding
-  const int W = 4096;
   for (int c = 0; c < ncolors; c++)
-    for (int w0 = L.color_ptr[c]; w0 < L.color_ptr[c + 1]; w0 += W) {
-      int w1 = std::min(w0 + W, L.color_ptr[c + 1]);
+    for (int w0 = L.color_ptr[c]; w0 < L.color_ptr[c + 1]; w0 += kOrderBlock) {
+      int w1 = std::min(w0 + kOrderBlock, L.color_ptr[c + 1]);
       std::stable_sort(owned.begin() + w0, owned.begin() + w1, [&](int a, int b) {
         return meta_len(f.meta[a]) > meta_len(f.meta[b]);
       });
     }
+  L.color_idx.resize(owned.size());
+  std::iota(L.color_idx.begin(), L.color_idx.end(), 0);
   L.n_owned = int(owned.size());
   L.g2l.assign(nv, -1);
   L.l2g = owned;
@@ -582,6 +585,12 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
   for (int i = 0; i < L.n_ghost; i++) {
     L.g2l[ghosts[i]] = L.n_owned + i;
     L.l2g.push_back(ghosts[i]);
+  }
+  L.rowcolor.assign(L.n_owned + L.n_ghost, 255);
+  for (int i = 0; i < L.n_owned; i++) L.rowcolor[i] = uint8_t(color[owned[i]]);
+  if (ncolors > 254) {
+    err = "too many colours";
+    return false;
   }
   // halo lists
   std::vector<int> nbrs;

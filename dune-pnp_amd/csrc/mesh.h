@@ -68,15 +68,19 @@ void initial_state(const Mesh &m, const Params &p, const double *phi_pb, double 
 // RCB on vertex coordinates into nparts (deterministic); part[v] in [0, nparts)
 void rcb_partition(const Mesh &m, int nparts, std::vector<int> &part);
 
-constexpr int kChunk = 64;  // one wavefront of rows per SELL chunk
+constexpr int kChunk = 64;        // one wavefront of rows per SELL chunk
+constexpr int kOrderBlock = 4096;  // window of the slot-count sort
 
 struct LocalLayout {
   int rank = 0, nranks = 1;
   int n_owned = 0, n_ghost = 0;
   std::vector<int> l2g;            // local -> global vertex (owned then ghosts)
   std::vector<int> g2l;            // global -> local, -1 if absent (size nv)
-  // colours of the owned rows: rows [color_ptr[c], color_ptr[c+1]) have colour c
-  std::vector<int> color_ptr;
+  // Row order: colour-major (rows of colour c are [color_ptr[c], color_ptr[c+1])), Morton order
+  // inside a colour.  color_idx lists the rows of each colour in storage order (the identity for
+  // this order); rowcolor[i] is the colour of local row/column i (255 for ghosts).
+  std::vector<int> color_ptr, color_idx;
+  std::vector<uint8_t> rowcolor;
   // SELL-64: chunk c covers rows [64c, 64c+64), has chunk_len[c] slots; slot s of row r is at
   // position chunk_off[c] + s*64 + (r - 64c)
   int nchunks = 0;

@@ -130,6 +130,7 @@ class _Layout(C.Structure):
                 ("nchunks", C.c_int32), ("nnbr", C.c_int32), ("max_slots", C.c_int32),
                 ("nslots", C.c_int64), ("nblocks", C.c_int64),
                 ("l2g", C.POINTER(C.c_int32)), ("color_ptr", C.POINTER(C.c_int32)),
+                ("color_idx", C.POINTER(C.c_int32)), ("rowcolor", C.POINTER(C.c_uint8)),
                 ("chunk_len", C.POINTER(C.c_int32)), ("chunk_off", C.POINTER(C.c_int32)),
                 ("colidx", C.POINTER(C.c_int32)), ("rowmeta", C.POINTER(C.c_uint64)),
                 ("nbr_ranks", C.POINTER(C.c_int32)), ("recv_ptr", C.POINTER(C.c_int32)),
@@ -325,6 +326,8 @@ class Layout:
         self.nslots, self.nblocks = v.nslots, v.nblocks
         self.l2g = arr(v.l2g, v.n_owned + v.n_ghost)
         self.color_ptr = arr(v.color_ptr, v.ncolors + 1)
+        self.color_idx = arr(v.color_idx, v.n_owned)
+        self.rowcolor = arr(v.rowcolor, v.n_owned + v.n_ghost, np.uint8)
         self.chunk_len = arr(v.chunk_len, v.nchunks)
         self.chunk_off = arr(v.chunk_off, v.nchunks + 1)
         self.colidx = arr(v.colidx, v.nslots)

@@ -240,6 +240,8 @@ typedef struct {
   int64_t nslots, nblocks;
   const int32_t *l2g;          /* n_owned + n_ghost: local row/column -> global vertex */
   const int32_t *color_ptr;    /* ncolors + 1 */
+  const int32_t *color_idx;    /* n_owned: rows of colour c at [color_ptr[c], color_ptr[c+1]) */
+  const uint8_t *rowcolor;     /* n_owned + n_ghost (255 = ghost) */
   const int32_t *chunk_len;    /* nchunks */
   const int32_t *chunk_off;    /* nchunks + 1 */
   const int32_t *colidx;       /* nslots (SELL-64, see dune-pnp_amd/csrc/kernels.h) */

@@ -112,9 +112,12 @@ def test_fans_sell_and_colouring(rel, k):
     assert L.nblocks == mesh.nv + 2 * len(edges)
     tris = set(tuple(sorted(t)) for t in mesh.tri.tolist())
     seen = {}
-    color = np.empty(mesh.nv, dtype=np.int64)
+    color = L.rowcolor[:L.n_owned].astype(np.int64)
+    assert np.all(L.rowcolor[L.n_owned:] == 255)
     for c in range(L.ncolors):
-        color[L.color_ptr[c]:L.color_ptr[c + 1]] = c
+        rows = L.color_idx[L.color_ptr[c]:L.color_ptr[c + 1]]
+        assert np.all(color[rows] == c) and np.all(np.diff(rows) > 0)
+    assert sorted(L.color_idx.tolist()) == list(range(L.n_owned))
     for i in range(L.n_owned):
         g = L.l2g[i]
         cols = L.row_cols(i)

@@ -18,6 +18,11 @@ for step in "$@"; do
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
     pmcf)   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 tools/prof_target.py 4 10 10 > "$OUT/pmcf.log" 2>&1; rc=$? ;;
     pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
+    ab)     : > "$OUT/ab.log"; rc=0
+            for i in 1 2 3; do
+              timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
+              fatal $rc && break
+            done ;;
     *) echo "unknown step $step"; rc=0 ;;
   esac
   echo "step $step rc=$rc" | tee -a "$OUT/steps.txt"
