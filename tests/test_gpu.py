@@ -269,3 +269,28 @@ def test_bench_path_fixed_iterations():
     assert info["nblocks"] == info["nv_owned"] + 2 * len(
         set(map(tuple, np.sort(np.concatenate([mesh.tri[:, [0, 1]], mesh.tri[:, [1, 2]],
                                                mesh.tri[:, [0, 2]]]), axis=1).tolist())))
+
+
+def test_cpp_driver_matches_python_api(tmp_path):
+    """The C++ driver (PB Newton -> BCExtension -> PNP Newton, like src/stationary_pnp_from_pb.hh)
+    reproduces the same solve through the Python mirror of the C ABI."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    out = subprocess.run([exe, cfgp, "--prec", "ssor", "--out", str(tmp_path / "cyl")],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    u_drv = np.loadtxt(tmp_path / "cyl_pnp.dat").T.ravel()
+    cfg = P.read_config(cfgp)
+    mesh = P.Mesh.read_gmsh(cfg.meshfile)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    s = cfg.system
+    ctx.set_operator(P.OP_PB)
+    phi, _ = ctx.newton(np.zeros(mesh.nv), reduction=s["newtonReduction"],
+                        min_linear_reduction=s["newtonMinLinearReduction"], prec=P.PREC_SSOR)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(x0, reduction=s["newtonReduction"],
+                        min_linear_reduction=s["newtonMinLinearReduction"], prec=P.PREC_SSOR)
+    assert res["converged"] == 1
+    assert np.max(np.abs(u_drv - u)) <= 1e-8 * np.max(np.abs(u))

@@ -187,3 +187,20 @@ def test_create_without_gpu_fails_loudly():
     with pytest.raises(P.PnpError) as ei:
         P.Context(mesh, P.Params.from_config(cfg))
     assert ei.value.code == P.E_HIP
+
+
+def test_driver_builds_and_fails_loudly_without_gpu(tmp_path):
+    """dune-pnp_amd/driver/pnp_main.cc (the C++ driver over pnp_pdelab_adapter.hh) builds and,
+    without a GPU, exits with an error instead of computing anything on the CPU."""
+    import subprocess
+    import torch
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(P.LIB_PATH), "pnp_main"])
+    out = subprocess.run([exe, "--help"], capture_output=True, text=True)
+    assert out.returncode == 0 and "usage" in out.stdout
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    out = subprocess.run([exe, os.path.join(DATA, "cylinder_config.cfg")], capture_output=True,
+                         text=True)
+    assert out.returncode == 1 and "hip" in out.stderr.lower()
