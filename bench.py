@@ -155,11 +155,7 @@ def main():
     ctx.set_operator(P.OP_PB)
     phi_pb, pb_res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=P.PREC_SSOR,
                                 linear_maxit=20000)
-    if world > 1:  # each rank returns its owned entries; combine
-        import torch
-        t = torch.from_numpy(phi_pb)
-        dist.all_reduce(t)
-        phi_pb = t.numpy()
+    phi_pb = ctx.sync_vector(phi_pb, 1)  # each rank returns its owned entries; combine
     x0 = ctx.initial_state(phi_pb)
     ctx.set_operator(P.OP_PNP)
     ctx.state_set(x0)

@@ -5,6 +5,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -29,7 +32,9 @@ struct DBuf {
     release();
     n = count;
     if (count == 0) return hipSuccess;
-    return hipMalloc(&p, sizeof(T) * count);
+    hipError_t e = hipMalloc(&p, sizeof(T) * count);
+    if (e == hipSuccess) e = hipMemset(p, 0, sizeof(T) * count);  // no reliance on fresh pages
+    return e;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -52,12 +57,39 @@ struct pnp_mesh_buf {
   pnp::Mesh m;
 };
 
+// In-process communicator for tests on one GPU (pnp_comm::local_group): ranks are contexts in
+// one process, each driven by its own host thread.  Collectives are host barriers plus
+// device-to-device copies; every call synchronises, which is fine for correctness tests.
+struct LocalGroup {
+  int size = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long generation = 0;
+  std::vector<pnp_ctx *> members;
+  std::vector<std::vector<double>> host;  // per-rank published host values (allreduce)
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    long gen = generation;
+    if (++arrived == size) {
+      arrived = 0;
+      generation++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+static std::mutex g_groups_m;
+static std::map<std::string, std::shared_ptr<LocalGroup>> g_groups;
+
 struct pnp_ctx {
   std::string err;
   int device = 0;
   hipStream_t stream = nullptr;
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> lg;  // test transport instead of RCCL
 
   pnp::Mesh mesh;
   pnp::Params params;
@@ -73,7 +105,8 @@ struct pnp_ctx {
   // operator
   int kind = -1, nf = 0, pat = 0, nvb = 0;
   pnp::AsmArgs aa{};
-  DBuf<double> vals;
+  DBuf<double> vals, lu;  // matrix and its ILU(0) factors
+  bool lu_valid = false;
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
@@ -158,7 +191,9 @@ struct pnp_ctx {
   long long nown() const { return (long long)L.n_owned * nf; }
 
   int halo(double *vec, int nfv) {
-    if (nranks == 1 || L.nbr_ranks.empty()) return PNP_OK;
+    if (nranks == 1) return PNP_OK;
+    if (lg) return halo_local(vec, nfv);
+    if (L.nbr_ranks.empty()) return PNP_OK;
     hipEvent_t t0 = tb(T_HALO);
     int ns = int(L.send_idx.size());
     hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, stream);
@@ -180,13 +215,62 @@ struct pnp_ctx {
     return PNP_OK;
   }
 
+  int halo_local(double *vec, int nfv) {
+    int ns = int(L.send_idx.size());
+    hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "halo pack");
+    lg->barrier();  // every rank has packed
+    for (size_t q = 0; q < L.nbr_ranks.size(); q++) {
+      pnp_ctx *peer = lg->members[L.nbr_ranks[q]];
+      const pnp::LocalLayout &PL = peer->L;
+      size_t k = 0;
+      while (k < PL.nbr_ranks.size() && PL.nbr_ranks[k] != rank) k++;
+      if (k == PL.nbr_ranks.size()) return fail(PNP_E_STATE, "asymmetric halo");
+      size_t cnt = size_t(L.recv_ptr[q + 1] - L.recv_ptr[q]) * nfv;
+      if (cnt != size_t(PL.send_ptr[k + 1] - PL.send_ptr[k]) * nfv)
+        return fail(PNP_E_STATE, "halo size mismatch");
+      e = hipMemcpyAsync(vec + (size_t(L.n_owned) + L.recv_ptr[q]) * nfv,
+                         peer->sendbuf.p + size_t(PL.send_ptr[k]) * nfv, sizeof(double) * cnt,
+                         hipMemcpyDeviceToDevice, stream);
+      if (e != hipSuccess) return hipfail(e, "halo copy");
+    }
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "halo copy");
+    lg->barrier();  // nobody repacks before every copy out of the send buffers is done
+    return PNP_OK;
+  }
+
+  // in-place sum over ranks of k doubles in device memory
+  int allreduce_dev(double *d, int k) {
+    if (nranks == 1) return PNP_OK;
+    if (lg) {
+      std::vector<double> h(k);
+      hipError_t e = hipMemcpyAsync(h.data(), d, sizeof(double) * k, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return hipfail(e, "allreduce");
+      lg->host[rank] = h;
+      lg->barrier();
+      std::vector<double> sum(k, 0.0);
+      for (int r = 0; r < nranks; r++)  // fixed rank order: deterministic
+        for (int j = 0; j < k; j++) sum[j] += lg->host[r][j];
+      lg->barrier();
+      e = hipMemcpyAsync(d, sum.data(), sizeof(double) * k, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "allreduce");
+    }
+    if (ncclAllReduce(d, d, k, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
+      return fail(PNP_E_RCCL, "ncclAllReduce");
+    return PNP_OK;
+  }
+
   int allreduce_red(int k) {
     if (nranks == 1) return PNP_OK;
     hipEvent_t t0 = tb(T_ALLRED);
     double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p) +
                                              offsetof(pnp::Scalars, red));
-    if (ncclAllReduce(red, red, k, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
-      return fail(PNP_E_RCCL, "ncclAllReduce");
+    int rc = allreduce_dev(red, k);
+    if (rc) return rc;
     te(T_ALLRED, t0);
     return PNP_OK;
   }
@@ -220,8 +304,8 @@ struct pnp_ctx {
     if (nranks > 1) {
       double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p + 1) +
                                                offsetof(pnp::Scalars, red));
-      if (ncclAllReduce(red, red, 1, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
-        return fail(PNP_E_RCCL, "ncclAllReduce");
+      int rc = allreduce_dev(red, 1);
+      if (rc) return rc;
     }
     e = hipMemcpyAsync(hS + 1, S.p + 1, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
@@ -264,7 +348,23 @@ struct pnp_ctx {
     hipError_t e = pnp::launch_assemble(dl, aa, stream);
     if (e != hipSuccess) return hipfail(e, "assemble");
     te(T_ASM, t0);
-    if (jac) assembled = true;
+    if (jac) {
+      assembled = true;
+      lu_valid = false;
+    }
+    return PNP_OK;
+  }
+
+  // ILU(0) factors of the current matrix (once per assembly)
+  int ilu_factor() {
+    if (lu_valid) return PNP_OK;
+    hipEvent_t t0 = tb(T_PREC);
+    hipError_t e = hipMemcpyAsync(lu.p, vals.p, sizeof(double) * size_t(L.nslots) * nvb,
+                                  hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = pnp::launch_ilu0_factor(dl, L.color_ptr.data(), nf, pat, lu.p, stream);
+    if (e != hipSuccess) return hipfail(e, "ilu0 factorisation");
+    te(T_PREC, t0);
+    lu_valid = true;
     return PNP_OK;
   }
 
@@ -274,8 +374,10 @@ struct pnp_ctx {
     hipError_t e = hipSuccess;
     if (prec == PNP_PREC_JACOBI) {
       e = pnp::launch_jacobi(dl, nf, pat, vals.p, d, vout, stream);
-    } else if (prec == PNP_PREC_SSOR || prec == PNP_PREC_ILU0) {
+    } else if (prec == PNP_PREC_SSOR) {
       e = pnp::launch_sgs(dl, L.color_ptr.data(), nf, pat, vals.p, d, vout, stream);
+    } else if (prec == PNP_PREC_ILU0) {
+      e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lu.p, d, vout, stream);
     } else {
       e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
     }
@@ -319,6 +421,7 @@ struct pnp_ctx {
     int check = o.check_every > 0 ? o.check_every : 8;
     if (fixed > 0) check = fixed;
     int prec = o.prec;
+    if (prec == PNP_PREC_ILU0 && (rc = ilu_factor())) return rc;
     int nsp = 0;
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
@@ -529,8 +632,9 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   if (comm && comm->size > 1) {
     c->rank = comm->rank;
     c->nranks = comm->size;
-    if (comm->rank < 0 || comm->rank >= comm->size || !comm->rccl_unique_id) {
-      g_err = "invalid pnp_comm";
+    if (comm->rank < 0 || comm->rank >= comm->size ||
+        (!comm->rccl_unique_id && !comm->local_group)) {
+      g_err = "invalid pnp_comm (need an RCCL unique id or a local group)";
       return PNP_E_ARG;
     }
   }
@@ -555,7 +659,7 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     g_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return PNP_E_HIP;
   }
-  if (c->nranks > 1) {
+  if (c->nranks > 1 && comm->rccl_unique_id) {
     ncclUniqueId id;
     std::memcpy(&id, comm->rccl_unique_id, sizeof id);
     if (ncclCommInitRank(&c->comm, c->nranks, id, c->rank) != ncclSuccess) {
@@ -612,7 +716,8 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     if (e2 != hipSuccess) return cp->hipfail(e2, what);
     return PNP_OK;
   };
-  if ((rc = al(c->vals, size_t(L.nslots) * 8, "vals")) || (rc = al(c->x, nv3, "x")) ||
+  if ((rc = al(c->vals, size_t(L.nslots) * 8, "vals")) ||
+      (rc = al(c->lu, size_t(L.nslots) * 8, "lu")) || (rc = al(c->x, nv3, "x")) ||
       (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
       (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
       (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
@@ -632,6 +737,27 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     g_err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return PNP_E_HIP;
   }
+  if (c->nranks > 1 && !comm->rccl_unique_id) {  // join the in-process group
+    std::shared_ptr<LocalGroup> g;
+    {
+      std::lock_guard<std::mutex> lk(g_groups_m);
+      auto &slot = g_groups[comm->local_group];
+      if (!slot || slot->size != c->nranks) {
+        slot = std::make_shared<LocalGroup>();
+        slot->size = c->nranks;
+        slot->members.assign(c->nranks, nullptr);
+        slot->host.assign(c->nranks, {});
+      }
+      g = slot;
+      if (g->members[c->rank]) {
+        g_err = "rank already present in local group";
+        return PNP_E_ARG;
+      }
+      g->members[c->rank] = c.get();
+    }
+    c->lg = g;
+    g->barrier();  // all ranks created before any collective
+  }
   *out = c.release();
   return PNP_OK;
 }
@@ -640,6 +766,10 @@ extern "C" void pnp_destroy(pnp_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->lg) {
+    std::lock_guard<std::mutex> lk(g_groups_m);
+    ctx->lg->members[ctx->rank] = nullptr;
+  }
   delete ctx;
 }
 
@@ -690,6 +820,11 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
                               : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE : pnp::kPatScalar);
   c->nvb = pnp::popc9(c->pat);
   c->assembled = false;
+  c->lu_valid = false;
+  // SELL padding slots point at the row itself and are never written by the assembly, so they
+  // must hold zeros in the block layout of THIS operator (the SpMV multiplies them)
+  CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nvb, c->stream),
+     "clear matrix");
   const pnp::Mesh &m = c->mesh;
   const pnp::LocalLayout &L = c->L;
   int nf = c->nf;
@@ -844,6 +979,17 @@ extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const 
   return res->breakdown ? PNP_E_BREAKDOWN : PNP_OK;
 }
 
+extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double *v) {
+  if (!c || !d || !v || prec < PNP_PREC_NONE || prec > PNP_PREC_JACOBI) return PNP_E_ARG;
+  if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
+  hipSetDevice(c->device);
+  int rc;
+  if ((rc = c->upload_ext(d, c->nf, c->b.p, false))) return rc;
+  if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
+  if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
+  return c->download_ext(c->z.p, c->nf, v);
+}
+
 extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_newton_result *res) {
   if (!c || !u || !o || !res) return PNP_E_ARG;
   if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
@@ -940,6 +1086,22 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
   res->defect = defect;
   if ((rc = c->download_ext(c->x.p, c->nf, u))) return rc;
   res->elapsed = now_s() - t_start;
+  return PNP_OK;
+}
+
+extern "C" int pnp_sync_vector(pnp_ctx *c, double *v, int32_t nfields) {
+  if (!c || !v || nfields < 1 || nfields > 3) return PNP_E_ARG;
+  if (c->nranks == 1) return PNP_OK;
+  hipSetDevice(c->device);
+  size_t nv = size_t(c->mesh.nv), n = nv * nfields;
+  std::vector<double> mine(n, 0.0);
+  for (int i = 0; i < c->L.n_owned; i++)
+    for (int f = 0; f < nfields; f++) mine[f * nv + c->L.l2g[i]] = v[f * nv + c->L.l2g[i]];
+  CK(hipMemcpy(c->ext.p, mine.data(), sizeof(double) * n, hipMemcpyHostToDevice), "sync upload");
+  int rc = c->allreduce_dev(c->ext.p, int(n));
+  if (rc) return rc;
+  CK(hipStreamSynchronize(c->stream), "sync");
+  CK(hipMemcpy(v, c->ext.p, sizeof(double) * n, hipMemcpyDeviceToHost), "sync download");
   return PNP_OK;
 }
 

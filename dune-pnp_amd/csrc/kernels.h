@@ -114,6 +114,13 @@ hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals
                          double *v, hipStream_t s);
 hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,  // NOLINT
                       const double *vals, const double *d, double *v, hipStream_t s);
+// ILU(0) of the local (owned x owned) matrix on the stored block pattern, scalar elimination in
+// colour-major vertex order (fields ascending inside a vertex); lu = copy of vals on entry,
+// factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)
+hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
+                              double *lu, hipStream_t s);
+hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
+                             const double *lu, const double *d, double *v, hipStream_t s);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);

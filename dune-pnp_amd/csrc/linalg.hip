@@ -174,6 +174,157 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = vi[f];
 }
 
+
+// ------------------------------------------------------------------------------------------
+// multicolour ILU(0)
+// ------------------------------------------------------------------------------------------
+// Elimination order = colour-major vertex order (the storage order), fields ascending inside a
+// vertex; the pattern is the stored block pattern (ISTL bilu0 / SeqILU0 on this ordering).
+// Rows of one colour never couple, so each colour is one parallel launch: the rows it needs
+// (lower neighbours) were factorised by earlier launches.  Entry (f,g) of slot t of row i is
+// lu[(off_c + 64 t) * NV + 64 pat(f,g) + lane].
+template <int NF, int PAT>
+__global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int r1,
+                                                        double *__restrict__ lu) {
+  constexpr int NV = popc9(PAT);
+  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  if (row >= r1) return;
+  const int ci = row / kRows, li = row % kRows;
+  const int offi = L.chunk_off[ci], leni = int(L.rowmeta[row] & 63);
+  const int *__restrict__ cixi = L.colidx + offi + li;
+  double *__restrict__ vi = lu + size_t(offi) * NV + li;
+  auto A = [&](int t, int f, int g) -> double & {
+    return vi[(size_t(t) * NV + pat_index(PAT, f, g)) * kRows];
+  };
+  // 1) eliminate by the lower neighbours j in increasing index order
+  int prev = -1;
+  for (;;) {
+    int j = 0x7fffffff, s = -1;
+    for (int t = 1; t < leni; t++) {
+      const int c = cixi[t * kRows];
+      if (c < row && c > prev && c < j) {
+        j = c;
+        s = t;
+      }
+    }
+    if (s < 0) break;
+    prev = j;
+    const int cj = j / kRows, lj = j % kRows;
+    const int offj = L.chunk_off[cj], lenj = int(L.rowmeta[j] & 63);
+    const int *__restrict__ cixj = L.colidx + offj + lj;
+    const double *__restrict__ vj = lu + size_t(offj) * NV + lj;
+    auto U = [&](int t, int g, int h) -> double {
+      return vj[(size_t(t) * NV + pat_index(PAT, g, h)) * kRows];
+    };
+#pragma unroll
+    for (int g = 0; g < NF; g++) {
+      const double dinv = U(0, g, g);  // stored inverted
+#pragma unroll
+      for (int f = 0; f < NF; f++) {
+        if (pat_index(PAT, f, g) < 0) continue;
+        const double l = A(s, f, g) * dinv;
+        A(s, f, g) = l;
+        if (l == 0.0) continue;
+        // q = (j, h > g): block (i, j), slot s of row i, diagonal block of row j
+#pragma unroll
+        for (int h = g + 1; h < NF; h++)
+          if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
+            A(s, f, h) -= l * U(0, g, h);
+        // q = (m, h), m > j, m owned, in both rows (m = i included)
+        for (int t = 0; t < leni; t++) {
+          const int m = cixi[t * kRows];
+          if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;  // padding -> m == row
+          for (int u = 1; u < lenj; u++) {
+            if (cixj[u * kRows] != m) continue;
+#pragma unroll
+            for (int h = 0; h < NF; h++)
+              if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(t, f, h) -= l * U(u, g, h);
+            break;
+          }
+        }
+      }
+    }
+  }
+  // 2) inside the vertex: rows (i,f) eliminated by (i,g<f); invert the pivots
+#pragma unroll
+  for (int f = 0; f < NF; f++) {
+#pragma unroll
+    for (int g = 0; g < f; g++) {
+      if (pat_index(PAT, f, g) < 0) continue;
+      const double l = A(0, f, g) * A(0, g, g);  // A(0,g,g) already inverted
+      A(0, f, g) = l;
+#pragma unroll
+      for (int h = g + 1; h < NF; h++)
+        if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(0, f, h) -= l * A(0, g, h);
+      for (int t = 1; t < leni; t++) {
+        const int m = cixi[t * kRows];
+        if (m <= row || m >= L.n_owned) continue;
+#pragma unroll
+        for (int h = 0; h < NF; h++)
+          if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(t, f, h) -= l * A(t, g, h);
+      }
+    }
+    A(0, f, f) = 1.0 / A(0, f, f);
+  }
+}
+
+// forward (unit lower, colours ascending) and backward (upper, colours descending) sweeps
+template <int NF, int PAT, int FWD>
+__global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
+                                                       const double *__restrict__ lu,
+                                                       const double *__restrict__ d,
+                                                       double *__restrict__ v) {
+  constexpr int NV = popc9(PAT);
+  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  if (row >= r1) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
+  const int *__restrict__ cix = L.colidx + off + lane;
+  const double *__restrict__ vb = lu + size_t(off) * NV + lane;
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
+  for (int s = 1; s < len; s++) {
+    const int j = cix[s * kRows];
+    if (j >= L.n_owned || j == row) continue;
+    if (FWD ? (j > row) : (j < row)) continue;
+    double vj[NF];
+#pragma unroll
+    for (int g = 0; g < NF; g++) vj[g] = v[size_t(j) * NF + g];
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int g = 0; g < NF; g++) {
+        const int q = pat_index(PAT, f, g);
+        if (q >= 0) acc[f] -= vb[(size_t(s) * NV + q) * kRows] * vj[g];
+      }
+  }
+  double Dg[NV];
+#pragma unroll
+  for (int q = 0; q < NV; q++) Dg[q] = vb[size_t(q) * kRows];
+  if (FWD) {
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int g = 0; g < f; g++) {
+        const int q = pat_index(PAT, f, g);
+        if (q >= 0) acc[f] -= Dg[q] * acc[g];
+      }
+  } else {
+#pragma unroll
+    for (int ff = NF - 1; ff >= 0; ff--) {
+#pragma unroll
+      for (int h = ff + 1; h < NF; h++) {
+        const int q = pat_index(PAT, ff, h);
+        if (q >= 0) acc[ff] -= Dg[q] * acc[h];
+      }
+      acc[ff] *= Dg[pat_index(PAT, ff, ff)];
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = acc[f];
+}
+
 // ------------------------------------------------------------------------------------------
 // BLAS-1 and reductions
 // ------------------------------------------------------------------------------------------
@@ -409,6 +560,40 @@ hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const 
       if (n > 0)
         hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 0>), rows_grid(n), dim3(kBlock), 0, s, L,
                            cp[c], n, vals, d, v);
+    }
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat, double *lu,
+                              hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    for (int c = 0; c < L.ncolors; c++) {
+      int n = cp[c + 1] - cp[c];
+      if (n > 0)
+        hipLaunchKernelGGL((k_ilu0_factor<NFc, PATc>), rows_grid(n), dim3(kBlock), 0, s, L, cp[c],
+                           cp[c + 1], lu);
+    }
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lu,
+                             const double *d, double *v, hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    for (int c = 0; c < L.ncolors; c++) {
+      int n = cp[c + 1] - cp[c];
+      if (n > 0)
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 1>), rows_grid(n), dim3(kBlock), 0, s, L,
+                           cp[c], cp[c + 1], lu, d, v);
+    }
+    for (int c = L.ncolors - 1; c >= 0; c--) {
+      int n = cp[c + 1] - cp[c];
+      if (n > 0)
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 0>), rows_grid(n), dim3(kBlock), 0, s, L,
+                           cp[c], cp[c + 1], lu, d, v);
     }
   });
   return hipGetLastError();

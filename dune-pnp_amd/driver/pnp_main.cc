@@ -38,6 +38,7 @@ static void usage() {
 
 static void write_vector(const std::string &path, const V &v, int nv) {
   std::ofstream f(path);
+  f.precision(17);
   int nf = int(v.size()) / nv;
   for (int i = 0; i < nv; i++) {
     for (int k = 0; k < nf; k++) f << (k ? " " : "") << v[size_t(k) * nv + i];
@@ -78,7 +79,7 @@ int main(int argc, char **argv) {
     pnp_gpu::Mesh mesh(s.cfg.meshfile, refine);
     pnp_params params = s.params();
     std::vector<char> uid(128, 0);
-    pnp_comm comm{rank, world, nullptr};
+    pnp_comm comm{rank, world, nullptr, nullptr};
     if (world > 1) {  // RCCL unique-id bootstrap through a shared file
       const char *idf = std::getenv("PNP_RCCL_ID_FILE");
       if (!idf) throw pnp_gpu::Error(PNP_E_ARG, "WORLD_SIZE > 1 needs PNP_RCCL_ID_FILE");
@@ -119,6 +120,7 @@ int main(int argc, char **argv) {
     } catch (pnp_gpu::Error &e) {
       std::printf("Something has happened (%s)\n", e.what());  // :181-185
     }
+    ctx.sync(pbu, 1);  // owned entries of every rank -> global PB potential
     if (mode == "pb") {
       if (!out.empty() && rank == 0) write_vector(out + "_pb.dat", pbu, nv);
       return 0;
@@ -150,6 +152,7 @@ int main(int argc, char **argv) {
     } else if (mode == "instationary") {  // :409-431, implicit Euler, dt = tau
       int n = steps > 0 ? steps : 100;
       for (int i = 0; i < n; i++) {
+        if (i > 0) ctx.sync(u, 3);
         V uold = u;
         pnp_gpu::Operator lop(PNP_OP_PNP_IMPLICIT_EULER);
         lop.args.dt = s.cfg.tau;
@@ -174,6 +177,7 @@ int main(int argc, char **argv) {
       usage();
       return 1;
     }
+    ctx.sync(u, 3);
     if (!out.empty() && rank == 0) write_vector(out + "_pnp.dat", u, nv);
     return status;
   } catch (pnp_gpu::Error &e) {  // src/dune_pnp.cc:33-38

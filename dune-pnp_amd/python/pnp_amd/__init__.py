@@ -78,7 +78,8 @@ class _Config(C.Structure):
 
 
 class _Comm(C.Structure):
-    _fields_ = [("rank", C.c_int32), ("size", C.c_int32), ("rccl_unique_id", C.c_void_p)]
+    _fields_ = [("rank", C.c_int32), ("size", C.c_int32), ("rccl_unique_id", C.c_void_p),
+                ("local_group", C.c_char_p)]
 
 
 class _Info(C.Structure):
@@ -359,10 +360,13 @@ def rccl_unique_id() -> bytes:
 class Context:
     """One GPU (one rank): mesh + parameters resident in HBM, one operator at a time."""
 
-    def __init__(self, mesh: Mesh, params: Params, device=0, rank=0, size=1, unique_id=None):
+    def __init__(self, mesh: Mesh, params: Params, device=0, rank=0, size=1, unique_id=None,
+                 local_group=None):
         self.mesh, self.params = mesh, params
         self._uid = C.create_string_buffer(unique_id, 128) if unique_id else None
-        comm = _Comm(rank, size, C.cast(self._uid, C.c_void_p).value if self._uid else None)
+        self._grp = local_group.encode() if local_group else None
+        comm = _Comm(rank, size, C.cast(self._uid, C.c_void_p).value if self._uid else None,
+                     self._grp)
         h = C.c_void_p()
         m = mesh.c()
         _check(lib().pnp_create(C.byref(m), C.byref(params.c), int(device), C.byref(comm),
@@ -435,6 +439,13 @@ class Context:
             self._ck(rc)
         return z, {k: getattr(r, k) for k, _ in _SolveResult._fields_}
 
+    def prec_apply(self, d, prec):
+        """v = M^{-1} d for one preconditioner application on the last assembled Jacobian."""
+        d = self._vec(d)
+        v = np.zeros_like(d)
+        self._ck(lib().pnp_prec_apply(self.h, int(prec), _ptr(d), _ptr(v)))
+        return v
+
     def newton(self, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
                line_search_maxit=500, prec=PREC_NONE, linear_maxit=20000, check_every=8):
         u = self._vec(u).copy()
@@ -443,6 +454,13 @@ class Context:
         r = _NewtonResult()
         self._ck(lib().pnp_newton(self.h, _ptr(u), C.byref(o), C.byref(r)))
         return u, {k: getattr(r, k) for k, _ in _NewtonResult._fields_}
+
+    def sync_vector(self, v, nfields=None):
+        """Collective: global vector from every rank's owned entries (no-op on one GPU)."""
+        nf = nfields or (v.size // self.mesh.nv)
+        v = np.ascontiguousarray(v, dtype=np.float64).copy()
+        self._ck(lib().pnp_sync_vector(self.h, _ptr(v), int(nf)))
+        return v
 
     def initial_state(self, phi_pb):
         phi = np.ascontiguousarray(phi_pb, dtype=np.float64)

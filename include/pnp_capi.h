@@ -116,6 +116,11 @@ int pnp_config_read(const char *path, pnp_config *out);
 typedef struct {
   int32_t rank, size;          /* this process' rank / number of GPUs (size 1: no RCCL) */
   const void *rccl_unique_id;  /* 128-byte ncclUniqueId from rank 0 (ignored when size == 1) */
+  const char *local_group;     /* test transport: if non-NULL (and no RCCL id), the `size`
+                                  contexts created in THIS process with the same group name form
+                                  the communicator (one host thread per rank; device-to-device
+                                  copies + host barriers instead of RCCL).  Same partition, halo
+                                  and reduction code paths as RCCL. */
 } pnp_comm;
 
 int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
@@ -185,6 +190,13 @@ typedef struct {
   double it_half, defect0, defect, reduction, elapsed;
 } pnp_solve_result;
 
+/* v = M^{-1} d for one preconditioner application on the last assembled Jacobian (the
+ * Dune::Preconditioner::apply step inside ISTL's BiCGSTABSolver, istl/solvers.hh); d, v host,
+ * external layout, owned rows.  PNP_PREC_ILU0 factorises on first use after an assembly.
+ * Multicolour semantics: SSOR = one forward + one backward multicolour
+ * Gauss-Seidel sweep, ILU0 = ILU(0) of the stored block pattern in colour-major vertex order. */
+int pnp_prec_apply(pnp_ctx *ctx, int32_t prec, const double *d, double *v);
+
 /* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */
 int pnp_linear_solve(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,
                      pnp_solve_result *res);
@@ -202,6 +214,11 @@ typedef struct {
   double first_defect, defect, elapsed, assemble_seconds, solve_seconds;
 } pnp_newton_result;
 int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
+
+/* Multi-GPU: v (host, external layout, nfields*nv) holds this rank's owned entries (as returned
+ * by pnp_newton / pnp_linear_solve / pnp_residual); on return it holds the global vector on every
+ * rank (collective; a no-op on one GPU). */
+int pnp_sync_vector(pnp_ctx *ctx, double *v, int32_t nfields);
 
 /* BCExtension interpolation: x0 (3*nv, external layout) from the PB potential phi_pb (nv). */
 int pnp_initial_state(pnp_ctx *ctx, const double *phi_pb, double *x0);

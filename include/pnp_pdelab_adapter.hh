@@ -109,6 +109,11 @@ class Context {
   Context &operator=(const Context &) = delete;
   pnp_ctx *get() const { return ctx_; }
   int nv() const { return nv_; }
+  // multi-GPU: turn this rank's owned entries into the global vector (collective)
+  template <class V>
+  void sync(V &v, int nfields) const {
+    check(pnp_sync_vector(ctx_, data(v), nfields), ctx_);
+  }
 
  private:
   pnp_ctx *ctx_ = nullptr;

@@ -137,7 +137,7 @@ def test_residual_parity_full_size():
     assert np.max(np.abs(lhs - J @ d)) <= 1e-9 * np.max(np.abs(J @ d))
 
 
-@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI, P.PREC_SSOR])
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI, P.PREC_SSOR, P.PREC_ILU0])
 def test_linear_solve_reduces_residual(prec):
     """Jacobian at the converged (physical) PNP state of the golden Newton run: a well-posed
     system for all three preconditioners."""
@@ -204,7 +204,7 @@ def test_bicgstab_half_step_counting_matches_istl(reduction):
 
 
 @pytest.mark.parametrize("name,prec", [("cylinder_k0", P.PREC_SSOR), ("pore_small_k0", P.PREC_SSOR),
-                                       ("cylinder_k0", P.PREC_NONE)])
+                                       ("cylinder_k0", P.PREC_NONE), ("pore_small_k0", P.PREC_ILU0)])
 def test_newton_pnp_matches_golden(name, prec):
     z, mesh, par, orc = golden(name)
     ctx = P.Context(mesh, par)
@@ -294,3 +294,99 @@ def test_cpp_driver_matches_python_api(tmp_path):
                         min_linear_reduction=s["newtonMinLinearReduction"], prec=P.PREC_SSOR)
     assert res["converged"] == 1
     assert np.max(np.abs(u_drv - u)) <= 1e-8 * np.max(np.abs(u))
+
+
+# ---- multicolour ILU(0) --------------------------------------------------------------------------
+# stored block patterns (dune-pnp_amd/csrc/kernels.h kPatPnp / kPatPnpIE): PnpOperator has no
+# c+/c- coupling; PnpTOperator's c- mass term lands in the c+ rows (quirk Q2) -> (1,2) present
+PATS = {"pnp": [(f, g) for f in range(3) for g in range(3) if (f, g) not in ((1, 2), (2, 1))],
+        "pnp_ie": [(f, g) for f in range(3) for g in range(3) if (f, g) != (2, 1)],
+        "pb": [(0, 0)]}
+
+
+def _ilu0_dense(A, M):
+    """Textbook IKJ ILU(0) restricted to the pattern M (Saad, Alg. 10.4); pivots not inverted."""
+    A = A.copy()
+    n = A.shape[0]
+    for i in range(n):
+        for k in np.nonzero(M[i, :i])[0]:
+            A[i, k] /= A[k, k]
+            q = np.nonzero(M[i, k + 1:] & M[k, k + 1:])[0] + k + 1
+            A[i, q] -= A[i, k] * A[k, q]
+    return A
+
+
+@pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
+                                       ("pore_small_k0", "pb"), ("cylinder_k0", "pnp")])
+def test_ilu0_application_matches_textbook_ilu0(name, kind):
+    """pnp_prec_apply(ILU0) = (LU)^{-1} d with L, U the ILU(0) factors of the Jacobian on the
+    stored block pattern, ordered colour-major by vertex with fields ascending."""
+    import scipy.linalg as sla
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    set_ops(z, ctx, orc, kind)
+    nf = 3 if kind.startswith("pnp") else 1
+    A = ctx.jacobian(z[kind + "_x"]).toarray()
+    lay = P.Layout(mesh)
+    nv = mesh.nv
+    perm = np.array([f * nv + lay.l2g[r] for r in range(nv) for f in range(nf)])
+    Ap = A[np.ix_(perm, perm)]
+    M = np.zeros_like(Ap, dtype=bool)
+    pat = PATS[kind]
+    for r in range(nv):
+        for c in lay.row_cols(r):
+            for f, g in pat:
+                M[r * nf + f, c * nf + g] = True
+    assert not np.any(Ap[~M]), "Jacobian has entries outside the stored pattern"
+    F = _ilu0_dense(Ap, M)
+    d = np.random.default_rng(5).standard_normal(nf * nv)
+    y = sla.solve_triangular(np.tril(F, -1) + np.eye(len(F)), d[perm], lower=True)
+    v_ref = sla.solve_triangular(np.triu(F), y, lower=False)
+    v = ctx.prec_apply(d, P.PREC_ILU0)[perm]
+    assert np.max(np.abs(v - v_ref)) <= 1e-10 * np.max(np.abs(v_ref))
+
+
+def test_pb_then_pnp_on_refined_pore_converges_with_ilu0():
+    """The hard stationary case (test/pore_pnp, 24.1 V Dirichlet, refined once): BiCGSTAB with
+    SSOR/Jacobi breaks down on the first Newton step; ILU(0) converges.  The converged state is
+    checked with the oracle's residual."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PB)
+    phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0)
+    assert rpb["converged"] == 1, rpb
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(x0, prec=P.PREC_ILU0, reduction=1e-8)
+    assert res["converged"] == 1 and res["status"] == 0, res
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    r0 = np.linalg.norm(orc.residual(op, x0))
+    r1 = np.linalg.norm(orc.residual(op, u))
+    assert r1 <= 1e-8 * r0 * 1.01
+
+
+def test_operator_switch_leaves_no_stale_matrix_entries():
+    """PB Newton then PNP in one context (the driver sequence): the PNP solve must behave exactly
+    as in a fresh context (SELL padding slots hold zeros for the new block layout)."""
+    cfg = P.read_config(os.path.join(DATA, "cylinder_config.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PB)
+    phi, _ = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_SSOR)
+    x0 = ctx.initial_state(phi)
+    out = []
+    for c in (ctx, P.Context(mesh, par)):
+        c.set_operator(P.OP_PNP)
+        c.jacobian(x0, export=False)
+        r = c.residual(x0)
+        out.append(c.linear_solve(r, prec=P.PREC_SSOR, reduction=1e-8, maxit=2000))
+    (za, ra), (zb, rb) = out
+    assert ra["converged"] == rb["converged"] == 1
+    assert ra["it_half"] == rb["it_half"]
+    np.testing.assert_array_equal(za, zb)

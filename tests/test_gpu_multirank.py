@@ -1,0 +1,139 @@
+"""Multi-rank parity on ONE GPU (-m gpu): P contexts in one process, one host thread per rank,
+joined through the in-process test transport (pnp_comm.local_group).  This runs the same
+partition (RCB), ghost/halo exchange, owned-row reductions and block-Jacobi preconditioner code
+as the RCCL path; only the byte movement differs (device-to-device copies + host barriers
+instead of ncclSend/ncclRecv/ncclAllReduce).  Results must equal the single-rank ones."""
+import itertools
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import pnp_amd as P
+from conftest import DATA
+from test_gpu import golden
+
+pytestmark = pytest.mark.gpu
+_grp = itertools.count()
+
+
+def run_ranks(nranks, mesh, par, fn):
+    name = f"t{next(_grp)}"
+
+    def work(r):
+        ctx = P.Context(mesh, par, device=0, rank=r, size=nranks, local_group=name)
+        try:
+            return fn(ctx, r)
+        finally:
+            ctx.close()
+    with ThreadPoolExecutor(nranks) as ex:
+        return list(ex.map(work, range(nranks)))
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_residual_and_jacobian_partitioned(nranks):
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["pnp_x"]
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PNP)
+        res = ctx.residual(x)
+        J = ctx.jacobian(x)
+        return res, J, ctx.info()
+    outs = run_ranks(nranks, mesh, par, fn)
+    r = sum(o[0] for o in outs)
+    J = sum(o[1] for o in outs)
+    assert sum(o[2]["nv_owned"] for o in outs) == mesh.nv
+    assert all(o[2]["nv_ghost"] > 0 for o in outs)
+    ctx1 = P.Context(mesh, par)
+    ctx1.set_operator(P.OP_PNP)
+    r1, J1 = ctx1.residual(x), ctx1.jacobian(x)
+    assert np.max(np.abs(r - r1)) <= 1e-13 * np.max(np.abs(r1))
+    assert abs(J - J1).max() <= 1e-13 * abs(J1).max()
+
+
+@pytest.mark.parametrize("nranks,prec", [(2, P.PREC_NONE), (2, P.PREC_SSOR), (4, P.PREC_SSOR),
+                                         (4, P.PREC_JACOBI), (2, P.PREC_ILU0), (4, P.PREC_ILU0)])
+def test_linear_solve_partitioned(nranks, prec):
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["newton_pnp_u"]
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PNP)
+        J = ctx.jacobian(x)
+        rhs = ctx.sync_vector(ctx.residual(x))
+        sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-10, maxit=5000)
+        return ctx.sync_vector(sol), res, J, rhs
+    outs = run_ranks(nranks, mesh, par, fn)
+    J = sum(o[2] for o in outs)
+    rhs = outs[0][3]
+    for sol, res, _, _ in outs:
+        assert res["converged"] == 1, res
+        assert np.linalg.norm(J @ sol - rhs) <= 1.001e-10 * np.linalg.norm(rhs)
+    # every rank sees the same global scalars
+    assert len({o[1]["iterations"] for o in outs}) == 1
+    np.testing.assert_array_equal(outs[0][0], outs[-1][0])
+
+
+@pytest.mark.parametrize("nranks,prec", [(2, P.PREC_SSOR), (4, P.PREC_SSOR), (4, P.PREC_ILU0)])
+def test_newton_partitioned_matches_single_rank(nranks, prec):
+    z, mesh, par, orc = golden("pore_small_k0")
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PNP)
+        u, res = ctx.newton(z["newton_pnp_x0"], prec=prec)
+        return ctx.sync_vector(u), res
+    outs = run_ranks(nranks, mesh, par, fn)
+    ref = z["newton_pnp_u"]
+    for u, res in outs:
+        assert res["converged"] == 1 and res["status"] == 0, res
+        assert np.max(np.abs(u - ref)) <= 1e-6 * np.max(np.abs(ref))
+
+
+def test_pb_then_pnp_partitioned_on_refined_mesh():
+    """The driver sequence (PB Newton -> BCExtension -> PNP Newton) on test/cylinder.msh refined
+    once, 4 ranks vs 1 rank."""
+    cfg = P.read_config(os.path.join(DATA, "cylinder_config.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+
+    def seq(ctx, r):
+        ctx.set_operator(P.OP_PB)
+        phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_SSOR)
+        phi = ctx.sync_vector(phi, 1)
+        x0 = ctx.initial_state(phi)
+        ctx.set_operator(P.OP_PNP)
+        u, res = ctx.newton(x0, prec=P.PREC_SSOR)
+        return ctx.sync_vector(u), res, rpb
+    outs = run_ranks(4, mesh, par, seq)
+    ctx1 = P.Context(mesh, par)
+    u1, res1, _ = seq(ctx1, 0)
+    assert res1["converged"] == 1, res1
+    for u, res, rpb in outs:
+        assert rpb["converged"] == 1 and res["converged"] == 1, (rpb, res)
+        assert np.max(np.abs(u - u1)) <= 1e-6 * np.max(np.abs(u1))
+
+
+def test_pb_then_pnp_partitioned_on_refined_pore_ilu0():
+    """The hard pore case (24.1 V, refined once) on 4 ranks with block-Jacobi ILU(0)."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+
+    def seq(ctx, r):
+        ctx.set_operator(P.OP_PB)
+        phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0)
+        phi = ctx.sync_vector(phi, 1)
+        x0 = ctx.initial_state(phi)
+        ctx.set_operator(P.OP_PNP)
+        u, res = ctx.newton(x0, prec=P.PREC_ILU0, reduction=1e-8)
+        return ctx.sync_vector(u), res, rpb
+    outs = run_ranks(4, mesh, par, seq)
+    ctx1 = P.Context(mesh, par)
+    u1, res1, _ = seq(ctx1, 0)
+    assert res1["converged"] == 1, res1
+    for u, res, rpb in outs:
+        assert rpb["converged"] == 1 and res["converged"] == 1, (rpb, res)
+        assert np.max(np.abs(u - u1)) <= 1e-5 * np.max(np.abs(u1))
