@@ -233,7 +233,12 @@ __device__ __forceinline__ void store_block(double *__restrict__ vb, int s, cons
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
-template <int OP, int JAC, int MINW>
+// FANR > 0: the row's column indices (fans of at most FANR - 1 neighbours) are loaded once into
+// registers, so the fan walk issues no dependent index loads.  On gfx9-family ISAs vmcnt counts
+// loads and stores in issue order: an index load issued behind an element's SELL block stores
+// could not be consumed before those stores drained (the FANR = 0 path waits vmcnt(0) per
+// element).
+template <int OP, int JAC, int MINW, int FANR>
 __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
   constexpr int NF = T::NF, NV = T::NV;
@@ -278,13 +283,26 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   double2 pc, pn;               // coordinates of v_s (current) and v_t (next)
   double uc[NF], un[NF];        // dofs of v_s, v_t
   double ac0 = 0, ac1 = 0, an0 = 0, an1 = 0;
-  load_nb(cix[1 * kRows], pc, uc, ac0, ac1);
+  constexpr int NC = FANR > 0 ? FANR : 1;
+  int cj[NC];
+  if constexpr (FANR > 0) {
+#pragma unroll
+    for (int k = 1; k < FANR; k++) cj[k] = k < len ? cix[k * kRows] : row;
+  }
+  // column of slot k (FANR path: k is the wave-uniform s + c, or 1 after a wrap)
+  auto col = [&](int k) -> int {
+    if constexpr (FANR > 0)
+      return cj[k];
+    else
+      return cix[k * kRows];
+  };
+  load_nb(col(1), pc, uc, ac0, ac1);
   {
     const int t1 = next_slot(1);
-    if (t1 > 0) load_nb(cix[t1 * kRows], pn, un, an0, an1);
+    if (t1 > 0) load_nb(t1 == 1 ? col(1) : col(2), pn, un, an0, an1);
   }
-  int jn = -1;  // column index of the slot needed two elements ahead
-  {
+  int jn = -1;  // FANR = 0: column index of the slot needed two elements ahead
+  if constexpr (FANR == 0) {
     const int t2 = next_slot(1) > 0 ? next_slot(next_slot(1)) : -1;
     if (t2 > 0 && next_slot(1) != 1) jn = cix[t2 * kRows];
   }
@@ -296,9 +314,13 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
     double up[NF];
     double ap0 = 0, ap1 = 0;
     if (tn > 0) {
-      load_nb(jn, pp, up, ap0, ap1);
-      const int tnn = tn != 1 ? next_slot(tn) : -1;
-      jn = tnn > 0 ? cix[tnn * kRows] : -1;
+      if constexpr (FANR > 0) {
+        load_nb(tn == 1 ? col(1) : col(s + 2), pp, up, ap0, ap1);  // tn is s + 2 or a wrap to 1
+      } else {
+        load_nb(jn, pp, up, ap0, ap1);
+        const int tnn = tn != 1 ? next_slot(tn) : -1;
+        jn = tnn > 0 ? cix[tnn * kRows] : -1;
+      }
     }
     const bool elem = t > 0 && !((meta >> (8 + s)) & 1);
     if (elem) {
@@ -406,14 +428,24 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     const char *e = getenv("PNP_ASM_WAVES");
     return (e && atoi(e) == 4) ? 4 : 3;
   }();
+  // fans up to 11 neighbours keep their column indices in registers (all meshes seen: <= 8)
+  static const bool fanr_ok = [] {  // A/B knob: PNP_ASM_FANR=0 forces the index-load path
+    const char *e = getenv("PNP_ASM_FANR");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool fanr = fanr_ok && L.max_slots <= 12;
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
-    if (a.jac && waves == 3)                                                       \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 3>), grid, block, 0, s, L, a);        \
+    if (!fanr && a.jac)                                                            \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
+    else if (!fanr)                                                                \
+      hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
+    else if (a.jac && waves == 3)                                                  \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
     else if (a.jac)                                                                \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 4>), grid, block, 0, s, L, a);        \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 4, 12>), grid, block, 0, s, L, a);    \
     else                                                                           \
-      hipLaunchKernelGGL((k_assemble<OPK, 0, 4>), grid, block, 0, s, L, a);        \
+      hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, L, a);    \
     break;
   switch (a.kind) {
     PNP_ASM_CASE(OP_PNP)

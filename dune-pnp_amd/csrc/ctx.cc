@@ -44,7 +44,7 @@ struct DBuf {
   ~DBuf() { release(); }
 };
 
-enum TimerCat { T_ASM = 0, T_SPMV, T_PREC, T_BLAS, T_HALO, T_ALLRED, T_NCAT };
+enum TimerCat { T_ASM = 0, T_SPMV, T_PREC, T_BLAS, T_HALO, T_ALLRED, T_FACT, T_NCAT };
 
 double now_s() {
   using namespace std::chrono;
@@ -107,6 +107,12 @@ struct pnp_ctx {
   pnp::AsmArgs aa{};
   DBuf<double> vals, lu;  // matrix and its ILU(0) factors
   bool lu_valid = false;
+  // triangular split storage (DevLayout l*/u*): lvals/uvals hold either the matrix (SSOR) or the
+  // ILU(0) factors; split_of says which is current (0 none, 1 matrix, 2 factors)
+  DBuf<int> d_lchunk_len, d_lchunk_off, d_lcolidx, d_lsrc, d_uchunk_len, d_uchunk_off, d_ucolidx,
+      d_usrc;
+  DBuf<double> lvals, uvals, tsgs;
+  int split_of = 0;
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
@@ -351,6 +357,7 @@ struct pnp_ctx {
     if (jac) {
       assembled = true;
       lu_valid = false;
+      split_of = 0;
     }
     return PNP_OK;
   }
@@ -358,26 +365,44 @@ struct pnp_ctx {
   // ILU(0) factors of the current matrix (once per assembly)
   int ilu_factor() {
     if (lu_valid) return PNP_OK;
-    hipEvent_t t0 = tb(T_PREC);
+    hipEvent_t t0 = tb(T_FACT);
     hipError_t e = hipMemcpyAsync(lu.p, vals.p, sizeof(double) * size_t(L.nslots) * nvb,
                                   hipMemcpyDeviceToDevice, stream);
     if (e == hipSuccess) e = pnp::launch_ilu0_factor(dl, L.color_ptr.data(), nf, pat, lu.p, stream);
     if (e != hipSuccess) return hipfail(e, "ilu0 factorisation");
-    te(T_PREC, t0);
+    te(T_FACT, t0);
     lu_valid = true;
+    split_of = 0;
+    return PNP_OK;
+  }
+
+  // bring the split storage up to date with the matrix (which = 1) or the factors (which = 2)
+  int split(int which) {
+    if (split_of == which) return PNP_OK;
+    hipEvent_t t0 = tb(T_FACT);
+    hipError_t e = pnp::launch_split(nvb, which == 2 ? lu.p : vals.p, d_lsrc.p, (long long)d_lsrc.n,
+                                     d_usrc.p, (long long)d_usrc.n, lvals.p, uvals.p, stream);
+    if (e != hipSuccess) return hipfail(e, "split");
+    te(T_FACT, t0);
+    split_of = which;
     return PNP_OK;
   }
 
   // v = M^{-1} d over owned rows (v sized n_local)
   int precond(int prec, const double *d, double *vout) {
+    int rc;
+    if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     hipEvent_t t0 = tb(T_PREC);
     hipError_t e = hipSuccess;
     if (prec == PNP_PREC_JACOBI) {
       e = pnp::launch_jacobi(dl, nf, pat, vals.p, d, vout, stream);
     } else if (prec == PNP_PREC_SSOR) {
-      e = pnp::launch_sgs(dl, L.color_ptr.data(), nf, pat, vals.p, d, vout, stream);
+      e = pnp::launch_sgs(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout, tsgs.p,
+                          stream);
     } else if (prec == PNP_PREC_ILU0) {
-      e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lu.p, d, vout, stream);
+      e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout,
+                                 stream);
     } else {
       e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
     }
@@ -421,7 +446,8 @@ struct pnp_ctx {
     int check = o.check_every > 0 ? o.check_every : 8;
     if (fixed > 0) check = fixed;
     int prec = o.prec;
-    if (prec == PNP_PREC_ILU0 && (rc = ilu_factor())) return rc;
+    if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
+    if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
     int nsp = 0;
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
@@ -683,6 +709,65 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     return PNP_OK;
   };
   int rc;
+  // triangular split of the owned-column pattern (DevLayout l*/u*)
+  std::vector<int> lcl(L.nchunks), lco(L.nchunks + 1, 0), ucl(L.nchunks), uco(L.nchunks + 1, 0);
+  for (int ch = 0; ch < L.nchunks; ch++) {
+    int ml = 0, mu = 1;
+    for (int ln = 0; ln < 64; ln++) {
+      int row = 64 * ch + ln;
+      if (row >= L.n_owned) break;
+      int len = int(L.rowmeta[row] & 63), nl = 0, nu = 1;
+      for (int sl = 1; sl < len; sl++) {
+        int j = L.colidx[size_t(L.chunk_off[ch]) + 64 * sl + ln];
+        if (j >= L.n_owned || j == row) continue;
+        (j < row ? nl : nu)++;
+      }
+      ml = std::max(ml, nl);
+      mu = std::max(mu, nu);
+    }
+    lcl[ch] = ml;
+    ucl[ch] = mu;
+    lco[ch + 1] = lco[ch] + 64 * ml;
+    uco[ch + 1] = uco[ch] + 64 * mu;
+  }
+  std::vector<int> lcol(lco[L.nchunks]), lsrc(lco[L.nchunks], -1), ucol(uco[L.nchunks]),
+      usrc(uco[L.nchunks], -1);
+  for (int ch = 0; ch < L.nchunks; ch++)
+    for (int ln = 0; ln < 64; ln++) {
+      int row = 64 * ch + ln;
+      for (int sl = 0; sl < lcl[ch]; sl++) lcol[size_t(lco[ch]) + 64 * sl + ln] = row;
+      for (int sl = 0; sl < ucl[ch]; sl++) ucol[size_t(uco[ch]) + 64 * sl + ln] = row;
+      if (row >= L.n_owned) continue;
+      int len = int(L.rowmeta[row] & 63), kl = 0, ku = 1;
+      usrc[size_t(uco[ch]) + ln] = L.chunk_off[ch] + ln;  // slot 0: the diagonal block
+      for (int sl = 1; sl < len; sl++) {
+        int pos = L.chunk_off[ch] + 64 * sl + ln;
+        int j = L.colidx[pos];
+        if (j >= L.n_owned || j == row) continue;
+        if (j < row) {
+          lcol[size_t(lco[ch]) + 64 * kl + ln] = j;
+          lsrc[size_t(lco[ch]) + 64 * kl + ln] = pos;
+          kl++;
+        } else {
+          ucol[size_t(uco[ch]) + 64 * ku + ln] = j;
+          usrc[size_t(uco[ch]) + 64 * ku + ln] = pos;
+          ku++;
+        }
+      }
+    }
+  if ((rc = up(c->d_lchunk_len, lcl, "lchunk_len")) || (rc = up(c->d_lchunk_off, lco, "lchunk_off")) ||
+      (rc = up(c->d_lcolidx, lcol, "lcolidx")) || (rc = up(c->d_lsrc, lsrc, "lsrc")) ||
+      (rc = up(c->d_uchunk_len, ucl, "uchunk_len")) || (rc = up(c->d_uchunk_off, uco, "uchunk_off")) ||
+      (rc = up(c->d_ucolidx, ucol, "ucolidx")) || (rc = up(c->d_usrc, usrc, "usrc"))) {
+    g_err = c->err;
+    return rc;
+  }
+  c->dl.lchunk_len = c->d_lchunk_len.p;
+  c->dl.lchunk_off = c->d_lchunk_off.p;
+  c->dl.lcolidx = c->d_lcolidx.p;
+  c->dl.uchunk_len = c->d_uchunk_len.p;
+  c->dl.uchunk_off = c->d_uchunk_off.p;
+  c->dl.ucolidx = c->d_ucolidx.p;
   if ((rc = up(c->d_chunk_len, L.chunk_len, "chunk_len")) ||
       (rc = up(c->d_chunk_off, L.chunk_off, "chunk_off")) ||
       (rc = up(c->d_colidx, L.colidx, "colidx")) || (rc = up(c->d_rowmeta, L.rowmeta, "rowmeta")) ||
@@ -700,6 +785,7 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   c->dl.n_owned = L.n_owned;
   c->dl.n_local = nloc;
   c->dl.nchunks = L.nchunks;
+  c->dl.max_slots = L.chunk_len.empty() ? 0 : *std::max_element(L.chunk_len.begin(), L.chunk_len.end());
   c->dl.ncolors = int(L.color_ptr.size()) - 1;
   c->dl.chunk_len = c->d_chunk_len.p;
   c->dl.chunk_off = c->d_chunk_off.p;
@@ -717,7 +803,9 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     return PNP_OK;
   };
   if ((rc = al(c->vals, size_t(L.nslots) * 8, "vals")) ||
-      (rc = al(c->lu, size_t(L.nslots) * 8, "lu")) || (rc = al(c->x, nv3, "x")) ||
+      (rc = al(c->lu, size_t(L.nslots) * 8, "lu")) ||
+      (rc = al(c->lvals, c->d_lsrc.n * 8, "lvals")) || (rc = al(c->uvals, c->d_usrc.n * 8, "uvals")) ||
+      (rc = al(c->tsgs, nv3, "sgs scratch")) || (rc = al(c->x, nv3, "x")) ||
       (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
       (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
       (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
@@ -821,6 +909,7 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   c->nvb = pnp::popc9(c->pat);
   c->assembled = false;
   c->lu_valid = false;
+  c->split_of = 0;
   // SELL padding slots point at the row itself and are never written by the assembly, so they
   // must hold zeros in the block layout of THIS operator (the SpMV multiplies them)
   CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nvb, c->stream),
@@ -1173,6 +1262,8 @@ extern "C" int pnp_timers_get(pnp_ctx *c, pnp_timers *t) {
   t->spmv_launches = c->t_n[T_SPMV];
   t->prec_launches = c->t_n[T_PREC];
   t->blas_launches = c->t_n[T_BLAS];
+  t->factor_ms = c->t_ms[T_FACT];
+  t->factor_launches = c->t_n[T_FACT];
   return PNP_OK;
 }
 

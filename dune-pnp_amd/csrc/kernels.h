@@ -62,6 +62,7 @@ __host__ __device__ constexpr int pat_index(int mask, int f, int g) {
 // ---- device views ----------------------------------------------------------------------------
 struct DevLayout {
   int n_owned = 0, n_local = 0, nchunks = 0, ncolors = 0;
+  int max_slots = 0;                // max chunk_len (fan length + 1)
   int xcd_remap = 0;                // A/B knob (PNP_XCD_REMAP): see xcd_block
   const int *chunk_len = nullptr;
   const int *chunk_off = nullptr;   // nchunks + 1
@@ -70,6 +71,12 @@ struct DevLayout {
   const double *xy = nullptr;       // [n_local][2]
   const int *color_idx = nullptr;   // rows of each colour (see mesh.h LocalLayout)
   const uint8_t *rowcolor = nullptr;
+  // triangular split of the owned-column pattern, SELL-64 each (same row order and chunks):
+  // L = strictly lower slots (columns of earlier colours), U = slot 0 diagonal + upper slots.
+  // Padding slots point at the row itself with zero values.  The sweeps read only the half
+  // they need (in the full SELL the lanes of a cache line disagree on lower/upper).
+  const int *lchunk_len = nullptr, *lchunk_off = nullptr, *lcolidx = nullptr;
+  const int *uchunk_len = nullptr, *uchunk_off = nullptr, *ucolidx = nullptr;
 };
 
 struct AsmArgs {
@@ -112,15 +119,21 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
 // preconditioners: v = M^{-1} d (v over owned rows)
 hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
                          double *v, hipStream_t s);
+// symmetric multicolour Gauss-Seidel on the split matrix (lv, uv); t = scratch [n_owned * nf]
 hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,  // NOLINT
-                      const double *vals, const double *d, double *v, hipStream_t s);
+                      const double *lv, const double *uv, const double *d, double *v, double *t,
+                      hipStream_t s);
+// copy a full-SELL matrix (vals or ILU factors) into the L / U split storage
+hipError_t launch_split(int nv, const double *src, const int *lsrc, long long ln, const int *usrc,
+                        long long un, double *lv, double *uv, hipStream_t s);
 // ILU(0) of the local (owned x owned) matrix on the stored block pattern, scalar elimination in
 // colour-major vertex order (fields ascending inside a vertex); lu = copy of vals on entry,
 // factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)
 hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                               double *lu, hipStream_t s);
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
-                             const double *lu, const double *d, double *v, hipStream_t s);
+                             const double *lv, const double *uv, const double *d, double *v,
+                             hipStream_t s);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);

@@ -12,6 +12,9 @@
 //   coupling among themselves, so each colour is one fully parallel launch (forward: colours
 //   ascending, backward: descending); couplings to ghost rows are dropped (block-Jacobi across
 //   GPUs, like the reference's non-overlapping SSOR on the local matrix).
+#include <cstdio>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace pnp {
@@ -122,58 +125,127 @@ __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__
 // colour in parallel (they are never adjacent), the NF fields of a row in sequence (ascending
 // forward, descending backward).  The forward sweep starts from v = 0 (ISTL SeqSSOR applies to y = 0): rows of
 // later colours are still zero and are skipped, the row's own value is not read.
-template <int NF, int PAT, int FWD>
+// Row setup shared by the split sweeps: the row's slots in the L (FWD) or U (!FWD) storage.
+struct SplitRow {
+  const int *cix;
+  const double *vb;  // values of slot s, entry q: vb[(s * NV + q) * kRows]
+  const double *dg;  // diagonal block (U slot 0): dg[q * kRows]
+  int len;
+};
+
+template <int NV, int FWD>
+__device__ __forceinline__ SplitRow split_row(const DevLayout &L, const double *lv,
+                                              const double *uv, int row, bool live) {
+  const int chunk = row / kRows, lane = row % kRows;
+  const int uoff = L.uchunk_off[chunk];
+  SplitRow r;
+  r.dg = uv + size_t(uoff) * NV + lane;
+  if (FWD) {
+    const int off = L.lchunk_off[chunk];
+    r.cix = L.lcolidx + off + lane;
+    r.vb = lv + size_t(off) * NV + lane;
+    r.len = live ? L.lchunk_len[chunk] : 0;
+  } else {
+    r.cix = L.ucolidx + uoff + lane;
+    r.vb = r.dg;
+    r.len = live ? L.uchunk_len[chunk] : 0;
+  }
+  return r;
+}
+
+// acc[f] -= sum over the row's slots [s0, len) of A_(f,g) v_j[g]; LPR lanes per row (adjacent
+// lanes, slots interleaved), partial sums combined across the row's lanes.  A colour holds ~1/6
+// of the rows (~2 waves per SIMD at config 3), so latency is hidden inside the thread: the
+// column indices of B slots are loaded together, then their gathers and values together.
+template <int NF, int PAT, int LPR, int B>
+__device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, int row,
+                                              const double *__restrict__ v, double (&acc)[NF]) {
+  constexpr int NV = popc9(PAT);
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0.0;
+  for (int sb = s0 + q; sb < R.len; sb += B * LPR) {
+    int j[B];
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int s = sb + b * LPR;
+      j[b] = s < R.len ? R.cix[s * kRows] : row;
+    }
+    double vj[B][NF], a[B][NV];
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int s = sb + b * LPR;
+      const bool use = j[b] != row;  // padding: zero values, v[row] may be stale
+#pragma unroll
+      for (int g = 0; g < NF; g++) vj[b][g] = use ? v[size_t(j[b]) * NF + g] : 0.0;
+#pragma unroll
+      for (int qq = 0; qq < NV; qq++)
+        a[b][qq] = use ? R.vb[(size_t(s) * NV + qq) * kRows] : 0.0;
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++)
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int qq = pat_index(PAT, f, g);
+          if (qq >= 0) acc[f] -= a[b][qq] * vj[b][g];
+        }
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1)
+#pragma unroll
+    for (int f = 0; f < NF; f++) acc[f] += __shfl_xor(acc[f], o, 64);
+}
+
+// one colour of a symmetric Gauss-Seidel sweep (ISTL SeqSSOR, w = 1, from v = 0), rows of the
+// colour in parallel (never adjacent), the NF fields of a row in sequence (ascending forward,
+// descending backward).  Forward: t_i = d_i - sum_{j lower} A_ij v_j, then the block-lower
+// solve; backward: v_i += D_i^{-1}(t_i - sum_{j upper} A_ij v_j - D_i v_i), field by field.
+template <int NF, int PAT, int FWD, int LPR, int B>
 __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int nk,
-                                                      const double *__restrict__ vals,
+                                                      const double *__restrict__ lv,
+                                                      const double *__restrict__ uv,
                                                       const double *__restrict__ d,
-                                                      double *__restrict__ v) {
+                                                      double *__restrict__ v,
+                                                      double *__restrict__ t) {
   constexpr int NV = popc9(PAT);
   // XCD remap pays here (+5 % measured): a colour's rows are a contiguous range
-  const int k = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
-  if (k >= nk) return;
-  const int row = k0 + k;  // colour-major order: the colour's rows are [k0, k0 + nk)
-  const int chunk = row / kRows, lane = row % kRows;
-  const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
-  const int *__restrict__ cix = L.colidx + off + lane;
-  const double *__restrict__ vb = vals + size_t(off) * NV + lane;
-  double rhs[NF];
+  const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  const int k = gt / LPR, q = gt % LPR;
+  const bool live = k < nk;
+  const int row = k0 + (live ? k : 0);  // colour-major order: the colour's rows are [k0, k0+nk)
+  const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
+  double acc[NF];
+  split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
+  if (!live || q != 0) return;
+  double rhs[NF], vi[NF], Dg[NV];
 #pragma unroll
-  for (int f = 0; f < NF; f++) rhs[f] = d[size_t(row) * NF + f];
-  for (int s = 1; s < len; s++) {
-    const int j = cix[s * kRows];
-    if (j >= L.n_owned || j == row) continue;       // ghost (block-Jacobi) or padding
-    if (FWD && j > row) continue;                    // later colours are still zero
-    double vj[NF];
-#pragma unroll
-    for (int g = 0; g < NF; g++) vj[g] = v[size_t(j) * NF + g];
-#pragma unroll
-    for (int f = 0; f < NF; f++)
-#pragma unroll
-      for (int g = 0; g < NF; g++) {
-        const int q = pat_index(PAT, f, g);
-        if (q >= 0) rhs[f] -= vb[(size_t(s) * NV + q) * kRows] * vj[g];
-      }
+  for (int f = 0; f < NF; f++) {
+    if (FWD) {
+      rhs[f] = d[size_t(row) * NF + f] + acc[f];
+      t[size_t(row) * NF + f] = rhs[f];
+      vi[f] = 0.0;
+    } else {
+      rhs[f] = t[size_t(row) * NF + f] + acc[f];
+      vi[f] = v[size_t(row) * NF + f];
+    }
   }
-  double vi[NF], Dg[NV];
 #pragma unroll
-  for (int f = 0; f < NF; f++) vi[f] = FWD ? 0.0 : v[size_t(row) * NF + f];
-#pragma unroll
-  for (int q = 0; q < NV; q++) Dg[q] = vb[size_t(q) * kRows];
+  for (int qq = 0; qq < NV; qq++) Dg[qq] = R.dg[size_t(qq) * kRows];
 #pragma unroll
   for (int ff = 0; ff < NF; ff++) {
     const int f = FWD ? ff : NF - 1 - ff;
     double r = rhs[f];
 #pragma unroll
     for (int g = 0; g < NF; g++) {
-      const int q = pat_index(PAT, f, g);
-      if (q >= 0) r -= Dg[q] * vi[g];
+      const int qq = pat_index(PAT, f, g);
+      if (qq >= 0) r -= Dg[qq] * vi[g];
     }
     vi[f] += r / Dg[pat_index(PAT, f, f)];
   }
 #pragma unroll
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = vi[f];
 }
-
 
 // ------------------------------------------------------------------------------------------
 // multicolour ILU(0)
@@ -268,61 +340,76 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
   }
 }
 
-// forward (unit lower, colours ascending) and backward (upper, colours descending) sweeps
-template <int NF, int PAT, int FWD>
+// forward (unit lower, colours ascending) and backward (upper, colours descending) sweeps over
+// the split factors; LPR lanes per row as in k_sgs_color
+template <int NF, int PAT, int FWD, int LPR, int B>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
-                                                       const double *__restrict__ lu,
+                                                       const double *__restrict__ lv,
+                                                       const double *__restrict__ uv,
                                                        const double *__restrict__ d,
                                                        double *__restrict__ v) {
   constexpr int NV = popc9(PAT);
-  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
-  if (row >= r1) return;
-  const int chunk = row / kRows, lane = row % kRows;
-  const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
-  const int *__restrict__ cix = L.colidx + off + lane;
-  const double *__restrict__ vb = lu + size_t(off) * NV + lane;
+  const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  const int k = gt / LPR, q = gt % LPR;
+  const bool live = r0 + k < r1;
+  const int row = live ? r0 + k : r0;
+  const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
   double acc[NF];
+  split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
+  if (!live || q != 0) return;
 #pragma unroll
-  for (int f = 0; f < NF; f++) acc[f] = FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
-  for (int s = 1; s < len; s++) {
-    const int j = cix[s * kRows];
-    if (j >= L.n_owned || j == row) continue;
-    if (FWD ? (j > row) : (j < row)) continue;
-    double vj[NF];
-#pragma unroll
-    for (int g = 0; g < NF; g++) vj[g] = v[size_t(j) * NF + g];
-#pragma unroll
-    for (int f = 0; f < NF; f++)
-#pragma unroll
-      for (int g = 0; g < NF; g++) {
-        const int q = pat_index(PAT, f, g);
-        if (q >= 0) acc[f] -= vb[(size_t(s) * NV + q) * kRows] * vj[g];
-      }
-  }
+  for (int f = 0; f < NF; f++) acc[f] += FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
   double Dg[NV];
 #pragma unroll
-  for (int q = 0; q < NV; q++) Dg[q] = vb[size_t(q) * kRows];
+  for (int qq = 0; qq < NV; qq++) Dg[qq] = R.dg[size_t(qq) * kRows];
   if (FWD) {
 #pragma unroll
     for (int f = 0; f < NF; f++)
 #pragma unroll
       for (int g = 0; g < f; g++) {
-        const int q = pat_index(PAT, f, g);
-        if (q >= 0) acc[f] -= Dg[q] * acc[g];
+        const int qq = pat_index(PAT, f, g);
+        if (qq >= 0) acc[f] -= Dg[qq] * acc[g];
       }
   } else {
 #pragma unroll
     for (int ff = NF - 1; ff >= 0; ff--) {
 #pragma unroll
       for (int h = ff + 1; h < NF; h++) {
-        const int q = pat_index(PAT, ff, h);
-        if (q >= 0) acc[ff] -= Dg[q] * acc[h];
+        const int qq = pat_index(PAT, ff, h);
+        if (qq >= 0) acc[ff] -= Dg[qq] * acc[h];
       }
       acc[ff] *= Dg[pat_index(PAT, ff, ff)];
     }
   }
 #pragma unroll
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = acc[f];
+}
+
+// full SELL -> split storage; position p of the split layout takes the NV values of source
+// position src[p] (same row, so the same lane), or zeros for padding (src < 0)
+__global__ __launch_bounds__(kBlock) void k_split(int nv, const double *__restrict__ src,
+                                                  const int *__restrict__ lsrc, long long ln,
+                                                  const int *__restrict__ usrc, long long un,
+                                                  double *__restrict__ lv,
+                                                  double *__restrict__ uv) {
+  long long p = blockIdx.x * (long long)kBlock + threadIdx.x;
+  const int *ps = lsrc;
+  double *dst = lv;
+  if (p >= ln) {
+    p -= ln;
+    if (p >= un) return;
+    ps = usrc;
+    dst = uv;
+  }
+  const long long lane = p & (kRows - 1);
+  const long long base = (p - lane) * nv + lane;
+  const int sp = ps[p];
+  if (sp < 0) {
+    for (int q = 0; q < nv; q++) dst[base + q * kRows] = 0.0;
+  } else {
+    const long long sb = (sp - lane) * nv + lane;
+    for (int q = 0; q < nv; q++) dst[base + q * kRows] = src[sb + q * kRows];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -543,25 +630,85 @@ hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals
   return hipGetLastError();
 }
 
-hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const double *vals,
-                      const double *d, double *v, hipStream_t s) {
+// sweep kernel shape: lanes per row x slot batch (PNP_SWEEP = "LPRxB", e.g. 2x4; A/B knob)
+static int sweep_cfg() {
+  static const int v = [] {
+    const char *e = std::getenv("PNP_SWEEP");
+    int l = 1, b = 4;
+    if (e && std::sscanf(e, "%dx%d", &l, &b) != 2) l = 1, b = 4;
+    int code = l * 16 + b;
+    switch (code) {
+      case 1 * 16 + 1: case 1 * 16 + 2: case 1 * 16 + 4: case 1 * 16 + 8:
+      case 2 * 16 + 1: case 2 * 16 + 2: case 2 * 16 + 4: case 4 * 16 + 1: case 4 * 16 + 2:
+        return code;
+      default:
+        return 1 * 16 + 4;
+    }
+  }();
+  return v;
+}
+
+#define PNP_LPR_DISPATCH(CALL)           \
+  do {                                   \
+    switch (sweep_cfg()) {               \
+      case 17: {                         \
+        constexpr int LPRc = 1, Bc = 1;  \
+        CALL;                            \
+      } break;                           \
+      case 18: {                         \
+        constexpr int LPRc = 1, Bc = 2;  \
+        CALL;                            \
+      } break;                           \
+      case 24: {                         \
+        constexpr int LPRc = 1, Bc = 8;  \
+        CALL;                            \
+      } break;                           \
+      case 33: {                         \
+        constexpr int LPRc = 2, Bc = 1;  \
+        CALL;                            \
+      } break;                           \
+      case 34: {                         \
+        constexpr int LPRc = 2, Bc = 2;  \
+        CALL;                            \
+      } break;                           \
+      case 36: {                         \
+        constexpr int LPRc = 2, Bc = 4;  \
+        CALL;                            \
+      } break;                           \
+      case 65: {                         \
+        constexpr int LPRc = 4, Bc = 1;  \
+        CALL;                            \
+      } break;                           \
+      case 66: {                         \
+        constexpr int LPRc = 4, Bc = 2;  \
+        CALL;                            \
+      } break;                           \
+      default: {                         \
+        constexpr int LPRc = 1, Bc = 4;  \
+        CALL;                            \
+      } break;                           \
+    }                                    \
+  } while (0)
+
+hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
+                      const double *uv, const double *d, double *v, double *t, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
   // the forward sweep writes every owned row exactly once and reads only rows of earlier
   // colours, so v needs no zeroing (ISTL starts the sweep from v = 0)
-  PNP_PAT_DISPATCH(nf, pat, {
+  PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
     for (int c = 0; c < L.ncolors; c++) {
       int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 1>), rows_grid(n), dim3(kBlock), 0, s, L,
-                           cp[c], n, vals, d, v);
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 1, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
+                           0, s, L, cp[c], n, lv, uv, d, v, t);
     }
     for (int c = L.ncolors - 1; c >= 0; c--) {
       int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 0>), rows_grid(n), dim3(kBlock), 0, s, L,
-                           cp[c], n, vals, d, v);
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 0, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
+                           0, s, L, cp[c], n, lv, uv, d, v, t);
     }
-  });
+  }));
   return hipGetLastError();
 }
 
@@ -579,23 +726,32 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
   return hipGetLastError();
 }
 
-hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lu,
-                             const double *d, double *v, hipStream_t s) {
+hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
+                             const double *uv, const double *d, double *v, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
-  PNP_PAT_DISPATCH(nf, pat, {
+  PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
     for (int c = 0; c < L.ncolors; c++) {
       int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 1>), rows_grid(n), dim3(kBlock), 0, s, L,
-                           cp[c], cp[c + 1], lu, d, v);
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 1, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
+                           0, s, L, cp[c], cp[c + 1], lv, uv, d, v);
     }
     for (int c = L.ncolors - 1; c >= 0; c--) {
       int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 0>), rows_grid(n), dim3(kBlock), 0, s, L,
-                           cp[c], cp[c + 1], lu, d, v);
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 0, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
+                           0, s, L, cp[c], cp[c + 1], lv, uv, d, v);
     }
-  });
+  }));
+  return hipGetLastError();
+}
+
+hipError_t launch_split(int nv, const double *src, const int *lsrc, long long ln, const int *usrc,
+                        long long un, double *lv, double *uv, hipStream_t s) {
+  const long long n = ln + un;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, nv,
+                     src, lsrc, ln, usrc, un, lv, uv);
   return hipGetLastError();
 }
 

@@ -123,7 +123,8 @@ class _Timers(C.Structure):
     _fields_ = [("assemble_ms", C.c_double), ("spmv_ms", C.c_double), ("prec_ms", C.c_double),
                 ("blas_ms", C.c_double), ("halo_ms", C.c_double), ("allreduce_ms", C.c_double),
                 ("assemble_launches", C.c_int64), ("spmv_launches", C.c_int64),
-                ("prec_launches", C.c_int64), ("blas_launches", C.c_int64)]
+                ("prec_launches", C.c_int64), ("blas_launches", C.c_int64),
+                ("factor_ms", C.c_double), ("factor_launches", C.c_int64)]
 
 
 class _Layout(C.Structure):

@@ -236,6 +236,8 @@ int pnp_bicgstab_iterations(pnp_ctx *ctx, int32_t n, int32_t prec, pnp_solve_res
 typedef struct {
   double assemble_ms, spmv_ms, prec_ms, blas_ms, halo_ms, allreduce_ms;
   int64_t assemble_launches, spmv_launches, prec_launches, blas_launches;
+  double factor_ms;          /* ILU(0) factorisations (once per assembly), not in prec_ms */
+  int64_t factor_launches;
 } pnp_timers;
 int pnp_timers_enable(pnp_ctx *ctx, int32_t on);
 int pnp_timers_get(pnp_ctx *ctx, pnp_timers *t);
