@@ -89,6 +89,12 @@ struct OpTraits {
   static constexpr int NF = (OP == OP_PNP || OP == OP_PNP_IE) ? 3 : 1;
   static constexpr int PAT = OP == OP_PNP ? kPatPnp : (OP == OP_PNP_IE ? kPatPnpIE : kPatScalar);
   static constexpr int NV = popc9(PAT);
+  // independent coefficients of one block (i, j) while it accumulates over the fan:
+  //   PNP: k0 = sum G_ij W, k1 = sum kappa M_ij, k2 = sum G_ij S+, k3 = sum G_ij S-,
+  //        k4 = sum (grad phi . grad psi_i) m_j, (PNP_IE) k5 = sum tau M2_ij, scaled by dt;
+  //   stored values: (0,0) k0, (0,1) k1, (0,2) -k1, (1,0) -k2, (1,1) k0 - k4 (+k5),
+  //   (1,2) k5, (2,0) k3, (2,2) k0 + k4   (expand_block)
+  static constexpr int NK = OP == OP_PNP ? 5 : (OP == OP_PNP_IE ? 6 : 1);
 };
 
 // Contributions of element (i, b, c) to row i: residual res[NF], blocks (i,i), (i,b), (i,c).
@@ -98,8 +104,6 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
                                         const double *uc, double pi_, double pb_, double pc_,
                                         double qi, double qb, double qc, double *res, double *Bd,
                                         double *Bb, double *Bc) {
-  using T = OpTraits<OP>;
-  constexpr int PAT = T::PAT;
   const double PI = a.pi;
   double Gii = G.gi0 * G.gi0 + G.gi1 * G.gi1;
   double Gib = G.gb0 * G.gi0 + G.gb1 * G.gi1;
@@ -129,17 +133,12 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
     }
     if constexpr (JAC) {
       auto blk = [&](double *B, double Gij, double Mij, double mj, double M2ij) {
-        B[pat_index(PAT, 0, 0)] += sc * Gij * I.W;
-        B[pat_index(PAT, 0, 1)] += sc * kap * Mij;
-        B[pat_index(PAT, 0, 2)] -= sc * kap * Mij;
-        B[pat_index(PAT, 1, 0)] -= sc * Gij * Sp;
-        B[pat_index(PAT, 1, 1)] += sc * (Gij * I.W - gp * mj);
-        B[pat_index(PAT, 2, 0)] += sc * Gij * Sm;
-        B[pat_index(PAT, 2, 2)] += sc * (Gij * I.W + gp * mj);
-        if constexpr (OP == OP_PNP_IE) {
-          B[pat_index(PAT, 1, 1)] += a.tau * M2ij;
-          B[pat_index(PAT, 1, 2)] += a.tau * M2ij;
-        }
+        B[0] += sc * Gij * I.W;
+        B[1] += sc * kap * Mij;
+        B[2] += sc * Gij * Sp;
+        B[3] += sc * Gij * Sm;
+        B[4] += sc * gp * mj;
+        if constexpr (OP == OP_PNP_IE) B[5] += a.tau * M2ij;
       };
       blk(Bd, Gii, I.Mii, I.mi, M2ii);
       blk(Bb, Gib, I.Mib, I.mb, M2ib);
@@ -215,21 +214,44 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
 }
 
 
+// block coefficients (OpTraits::NK) -> the NV stored values of the block pattern
 template <int OP>
-__device__ __forceinline__ void store_block(double *__restrict__ vb, int s, const double *B,
-                                            unsigned dm, bool diag) {
+__device__ __forceinline__ void expand_block(const double *K, double *B) {
+  using T = OpTraits<OP>;
+  constexpr int PAT = T::PAT;
+  if constexpr (OP == OP_PNP || OP == OP_PNP_IE) {
+    B[pat_index(PAT, 0, 0)] = K[0];
+    B[pat_index(PAT, 0, 1)] = K[1];
+    B[pat_index(PAT, 0, 2)] = -K[1];
+    B[pat_index(PAT, 1, 0)] = -K[2];
+    B[pat_index(PAT, 1, 1)] = K[0] - K[4];
+    B[pat_index(PAT, 2, 0)] = K[3];
+    B[pat_index(PAT, 2, 2)] = K[0] + K[4];
+    if constexpr (OP == OP_PNP_IE) {
+      B[pat_index(PAT, 1, 1)] += K[5];
+      B[pat_index(PAT, 1, 2)] = K[5];
+    }
+  } else {
+    B[0] = K[0];
+  }
+}
+
+template <int OP>
+__device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, int s,
+                                            const double *Kc, unsigned dm, bool diag) {
   using T = OpTraits<OP>;
   constexpr int PAT = T::PAT, NV = T::NV, NF = T::NF;
+  double B[NV];
+  expand_block<OP>(Kc, B);
 #pragma unroll
   for (int f = 0; f < NF; f++)
 #pragma unroll
     for (int g = 0; g < NF; g++) {
       const int v = pat_index(PAT, f, g);
       if (v < 0) continue;
-      double val = B[v];
-      if ((dm >> f) & 1) val = (diag && f == g) ? 1.0 : 0.0;  // constrained row -> identity
-      vb[(size_t(s) * NV + v) * kRows] = val;
+      if ((dm >> f) & 1) B[v] = (diag && f == g) ? 1.0 : 0.0;  // constrained row -> identity
     }
+  store_vals<NV>(vc + size_t(s) * NV * kRows, lane, B);
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
@@ -241,7 +263,7 @@ __device__ __forceinline__ void store_block(double *__restrict__ vb, int s, cons
 template <int OP, int JAC, int MINW, int FANR>
 __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
-  constexpr int NF = T::NF, NV = T::NV;
+  constexpr int NF = T::NF, NV = T::NV, NK = T::NK;
   const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * blockDim.x + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
@@ -250,7 +272,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   const int len = int(meta & 63);
   const bool closed = (meta >> 6) & 1;
   const int *__restrict__ cix = L.colidx + off + lane;
-  double *__restrict__ vb = a.vals + size_t(off) * NV + lane;
+  double *__restrict__ vc = a.vals + size_t(off) * NV;  // chunk base, see vin()
 
   const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
   double ui[NF];
@@ -263,11 +285,11 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 #pragma unroll
   for (int f = 0; f < NF; f++) dm |= unsigned(a.dmask[size_t(row) * NF + f] != 0) << f;
 
-  double R[NF], D[NV], P[NV], F[NV];
+  double R[NF], D[NK], P[NK], F[NK];  // block coefficients, see OpTraits::NK
 #pragma unroll
   for (int f = 0; f < NF; f++) R[f] = 0;
 #pragma unroll
-  for (int v = 0; v < NV; v++) D[v] = P[v] = F[v] = 0;
+  for (int v = 0; v < NK; v++) D[v] = P[v] = F[v] = 0;
 
   // Software-pipelined fan walk.  Element s is (i, v_s, v_t) with t = s+1 (or 1 when a closed
   // fan wraps); consecutive elements share v_{s+1}, so each neighbour's data (coordinates, NF
@@ -326,26 +348,26 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
     if (elem) {
       Geo G;
       geometry(pi2.x, pi2.y, pc.x, pc.y, pn.x, pn.y, G);
-      double Ct[NV];
+      double Ct[NK];
 #pragma unroll
-      for (int v = 0; v < NV; v++) Ct[v] = 0;
+      for (int v = 0; v < NK; v++) Ct[v] = 0;
       // P (pending block of slot s) receives this element's (i, v_s) contribution directly
       element<OP, JAC>(a, G, pi2.y, pc.y, pn.y, ui, uc, un, ai, ac0, an0, aq, ac1, an1, R, D, P,
                        Ct);
       if constexpr (JAC) {
         if (s == 1 && closed) {
 #pragma unroll
-          for (int v = 0; v < NV; v++) F[v] = P[v];
+          for (int v = 0; v < NK; v++) F[v] = P[v];
         } else {
-          store_block<OP>(vb, s, P, dm, false);
+          store_block<OP>(vc, lane, s, P, dm, false);
         }
 #pragma unroll
-        for (int v = 0; v < NV; v++) P[v] = Ct[v];
+        for (int v = 0; v < NK; v++) P[v] = Ct[v];
       }
     } else if constexpr (JAC) {
-      store_block<OP>(vb, s, P, dm, false);
+      store_block<OP>(vc, lane, s, P, dm, false);
 #pragma unroll
-      for (int v = 0; v < NV; v++) P[v] = 0;
+      for (int v = 0; v < NK; v++) P[v] = 0;
     }
     // rotate: v_t becomes the current neighbour, the prefetched one the next
     pc = pn;
@@ -364,10 +386,10 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   if constexpr (JAC) {
     if (closed) {
 #pragma unroll
-      for (int v = 0; v < NV; v++) F[v] += P[v];
-      store_block<OP>(vb, 1, F, dm, false);
+      for (int v = 0; v < NK; v++) F[v] += P[v];
+      store_block<OP>(vc, lane, 1, F, dm, false);
     }
-    store_block<OP>(vb, 0, D, dm, true);
+    store_block<OP>(vc, lane, 0, D, dm, true);
   }
 #pragma unroll
   for (int f = 0; f < NF; f++) {

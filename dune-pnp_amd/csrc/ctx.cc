@@ -113,6 +113,7 @@ struct pnp_ctx {
       d_usrc;
   DBuf<double> lvals, uvals, tsgs;
   int split_of = 0;
+  DBuf<int> d_blkmap;
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
@@ -762,6 +763,26 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     g_err = c->err;
     return rc;
   }
+  {  // spatial block order (DevLayout::blkmap); A/B knob PNP_BLKMAP=0 disables it
+    const char *e = getenv("PNP_BLKMAP");
+    if (!(e && atoi(e) == 0) && L.n_owned > 0) {
+      int nblk = (L.n_owned + 255) / 256;
+      std::vector<double> key(nblk);
+      for (int b = 0; b < nblk; b++) {
+        int r = 256 * b, cc = L.rowcolor[r];
+        double lo = L.color_ptr[cc], hi = L.color_ptr[cc + 1];
+        key[b] = (r - lo) / std::max(1.0, hi - lo);
+      }
+      std::vector<int> order(nblk);
+      for (int b = 0; b < nblk; b++) order[b] = b;
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
+      if ((rc = up(c->d_blkmap, order, "blkmap"))) {
+        g_err = c->err;
+        return rc;
+      }
+      c->dl.blkmap = c->d_blkmap.p;
+    }
+  }
   c->dl.lchunk_len = c->d_lchunk_len.p;
   c->dl.lchunk_off = c->d_lchunk_off.p;
   c->dl.lcolidx = c->d_lcolidx.p;
@@ -1036,8 +1057,7 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
           int v = pnp::pat_index(c->pat, f, g);
           if (v < 0) continue;
           double value =
-              hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NV + size_t(v) * pnp::kRows +
-                 lane];
+              hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NV + pnp::vin(NV, v, lane)];
           tmp.push_back({g * nv + L.l2g[j], value});
         }
       }

@@ -29,6 +29,41 @@ __device__ __forceinline__ int xcd_block(int b, int nwg, int on = 1) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
+// ---- SELL value layout --------------------------------------------------------------------------
+// Slot s of chunk c holds NV values for each of the chunk's 64 rows, at doubles
+// [(chunk_off[c] + 64 s) * NV, +64 NV).  Inside a slot, value pairs (q, q+1) (q even, q+1 < NV)
+// are interleaved per row as 16-B records, so one dwordx4 per lane moves a pair (dwordx2 stores
+// are store-issue bound); an odd last value is row-contiguous.
+__host__ __device__ constexpr int vin(int nv, int q, int lane) {
+  return q < (nv & ~1) ? (q >> 1) * 2 * kRows + 2 * lane + (q & 1) : (nv - 1) * kRows + lane;
+}
+
+// the NV values of one (row, slot): sb = slot base (vals + (chunk_off + 64 s) * NV)
+template <int NV>
+__device__ __forceinline__ void load_vals(const double *__restrict__ sb, int lane, double *B) {
+#pragma unroll
+  for (int q = 0; q + 1 < NV; q += 2) {
+    const double2 t = reinterpret_cast<const double2 *>(sb + (q >> 1) * 2 * kRows)[lane];
+    B[q] = t.x;
+    B[q + 1] = t.y;
+  }
+  if constexpr (NV & 1) B[NV - 1] = sb[(NV - 1) * kRows + lane];
+}
+
+template <int NV>
+__device__ __forceinline__ void store_vals(double *__restrict__ sb, int lane, const double *B) {
+#pragma unroll
+  for (int q = 0; q + 1 < NV; q += 2)
+    reinterpret_cast<double2 *>(sb + (q >> 1) * 2 * kRows)[lane] = make_double2(B[q], B[q + 1]);
+  if constexpr (NV & 1) sb[(NV - 1) * kRows + lane] = B[NV - 1];
+}
+
+// 256-row block processed by workgroup b of a whole-matrix launch of nwg workgroups
+template <class DL>
+__device__ __forceinline__ int row_block(const DL &L, int b, int nwg) {
+  return L.blkmap ? L.blkmap[xcd_block(b, nwg, 1)] : xcd_block(b, nwg, L.xcd_remap);
+}
+
 // ---- operator kinds / block patterns ----------------------------------------------------------
 enum OpKind : int {
   OP_PNP = 0,
@@ -71,6 +106,11 @@ struct DevLayout {
   const double *xy = nullptr;       // [n_local][2]
   const int *color_idx = nullptr;   // rows of each colour (see mesh.h LocalLayout)
   const uint8_t *rowcolor = nullptr;
+  // Spatial block order for the whole-matrix kernels (assembly, SpMV): logical block (XCD-major,
+  // see xcd_block) -> 256-row block.  Blocks are sorted by their Morton position inside their
+  // colour, so each XCD takes one spatial slice of the domain in every colour and the neighbour
+  // gathers of its rows share its L2 (colour-major rows otherwise spread a region over all XCDs).
+  const int *blkmap = nullptr;
   // triangular split of the owned-column pattern, SELL-64 each (same row order and chunks):
   // L = strictly lower slots (columns of earlier colours), U = slot 0 diagonal + upper slots.
   // Padding slots point at the row itself with zero values.  The sweeps read only the half

@@ -61,27 +61,28 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
                                                  const double *__restrict__ w,
                                                  double *__restrict__ partials) {
   constexpr int NV = popc9(PAT);
-  const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * kBlock + threadIdx.x;
+  const int row = row_block(L, blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
   double d[2] = {0, 0};
   if (row < L.n_owned) {
     const int chunk = row / kRows, lane = row % kRows;
     const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
     const int *__restrict__ cix = L.colidx + off + lane;
-    const double *__restrict__ vb = vals + size_t(off) * NV + lane;
+    const double *__restrict__ vc = vals + size_t(off) * NV;  // chunk base, see vin()
     double acc[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) acc[f] = 0;
     for (int s = 0; s < len; s++) {
       const int j = cix[s * kRows];
-      double xj[NF];
+      double xj[NF], a[NV];
 #pragma unroll
       for (int g = 0; g < NF; g++) xj[g] = x[size_t(j) * NF + g];
+      load_vals<NV>(vc + size_t(s) * NV * kRows, lane, a);
 #pragma unroll
       for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int g = 0; g < NF; g++) {
           const int v = pat_index(PAT, f, g);
-          if (v >= 0) acc[f] += vb[(size_t(s) * NV + v) * kRows] * xj[g];
+          if (v >= 0) acc[f] += a[v] * xj[g];
         }
     }
 #pragma unroll
@@ -115,10 +116,10 @@ __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__
   const int row = blockIdx.x * kBlock + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
-  const double *vb = vals + size_t(L.chunk_off[chunk]) * NV + lane;
+  double D[NV];
+  load_vals<NV>(vals + size_t(L.chunk_off[chunk]) * NV, lane, D);
 #pragma unroll
-  for (int f = 0; f < NF; f++)
-    v[size_t(row) * NF + f] = d[size_t(row) * NF + f] / vb[size_t(pat_index(PAT, f, f)) * kRows];
+  for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = d[size_t(row) * NF + f] / D[pat_index(PAT, f, f)];
 }
 
 // one colour of a Gauss-Seidel sweep: v_i += D_i^{-1} (d_i - sum_j A_ij v_j), rows of the
@@ -128,9 +129,9 @@ __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__
 // Row setup shared by the split sweeps: the row's slots in the L (FWD) or U (!FWD) storage.
 struct SplitRow {
   const int *cix;
-  const double *vb;  // values of slot s, entry q: vb[(s * NV + q) * kRows]
-  const double *dg;  // diagonal block (U slot 0): dg[q * kRows]
-  int len;
+  const double *vc;  // chunk base of the L or U values: slot s at vc + s * NV * kRows (vin())
+  const double *dg;  // U chunk base: slot 0 = diagonal block
+  int len, lane;
 };
 
 template <int NV, int FWD>
@@ -139,15 +140,16 @@ __device__ __forceinline__ SplitRow split_row(const DevLayout &L, const double *
   const int chunk = row / kRows, lane = row % kRows;
   const int uoff = L.uchunk_off[chunk];
   SplitRow r;
-  r.dg = uv + size_t(uoff) * NV + lane;
+  r.lane = lane;
+  r.dg = uv + size_t(uoff) * NV;
   if (FWD) {
     const int off = L.lchunk_off[chunk];
     r.cix = L.lcolidx + off + lane;
-    r.vb = lv + size_t(off) * NV + lane;
+    r.vc = lv + size_t(off) * NV;
     r.len = live ? L.lchunk_len[chunk] : 0;
   } else {
     r.cix = L.ucolidx + uoff + lane;
-    r.vb = r.dg;
+    r.vc = r.dg;
     r.len = live ? L.uchunk_len[chunk] : 0;
   }
   return r;
@@ -177,9 +179,12 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
       const bool use = j[b] != row;  // padding: zero values, v[row] may be stale
 #pragma unroll
       for (int g = 0; g < NF; g++) vj[b][g] = use ? v[size_t(j[b]) * NF + g] : 0.0;
+      if (use) {
+        load_vals<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
+      } else {
 #pragma unroll
-      for (int qq = 0; qq < NV; qq++)
-        a[b][qq] = use ? R.vb[(size_t(s) * NV + qq) * kRows] : 0.0;
+        for (int qq = 0; qq < NV; qq++) a[b][qq] = 0.0;
+      }
     }
 #pragma unroll
     for (int b = 0; b < B; b++)
@@ -230,8 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
       vi[f] = v[size_t(row) * NF + f];
     }
   }
-#pragma unroll
-  for (int qq = 0; qq < NV; qq++) Dg[qq] = R.dg[size_t(qq) * kRows];
+  load_vals<NV>(R.dg, R.lane, Dg);
 #pragma unroll
   for (int ff = 0; ff < NF; ff++) {
     const int f = FWD ? ff : NF - 1 - ff;
@@ -264,9 +268,9 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
   const int ci = row / kRows, li = row % kRows;
   const int offi = L.chunk_off[ci], leni = int(L.rowmeta[row] & 63);
   const int *__restrict__ cixi = L.colidx + offi + li;
-  double *__restrict__ vi = lu + size_t(offi) * NV + li;
+  double *__restrict__ vi = lu + size_t(offi) * NV;  // chunk base, see vin()
   auto A = [&](int t, int f, int g) -> double & {
-    return vi[(size_t(t) * NV + pat_index(PAT, f, g)) * kRows];
+    return vi[size_t(t) * NV * kRows + vin(NV, pat_index(PAT, f, g), li)];
   };
   // 1) eliminate by the lower neighbours j in increasing index order
   int prev = -1;
@@ -284,9 +288,9 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
     const int cj = j / kRows, lj = j % kRows;
     const int offj = L.chunk_off[cj], lenj = int(L.rowmeta[j] & 63);
     const int *__restrict__ cixj = L.colidx + offj + lj;
-    const double *__restrict__ vj = lu + size_t(offj) * NV + lj;
+    const double *__restrict__ vj = lu + size_t(offj) * NV;
     auto U = [&](int t, int g, int h) -> double {
-      return vj[(size_t(t) * NV + pat_index(PAT, g, h)) * kRows];
+      return vj[size_t(t) * NV * kRows + vin(NV, pat_index(PAT, g, h), lj)];
     };
 #pragma unroll
     for (int g = 0; g < NF; g++) {
@@ -360,8 +364,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] += FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
   double Dg[NV];
-#pragma unroll
-  for (int qq = 0; qq < NV; qq++) Dg[qq] = R.dg[size_t(qq) * kRows];
+  load_vals<NV>(R.dg, R.lane, Dg);
   if (FWD) {
 #pragma unroll
     for (int f = 0; f < NF; f++)
@@ -401,14 +404,14 @@ __global__ __launch_bounds__(kBlock) void k_split(int nv, const double *__restri
     ps = usrc;
     dst = uv;
   }
-  const long long lane = p & (kRows - 1);
-  const long long base = (p - lane) * nv + lane;
+  const int lane = int(p & (kRows - 1));
+  const long long base = (p - lane) * nv;  // slot base (position p - lane is lane 0 of the slot)
   const int sp = ps[p];
   if (sp < 0) {
-    for (int q = 0; q < nv; q++) dst[base + q * kRows] = 0.0;
+    for (int q = 0; q < nv; q++) dst[base + vin(nv, q, lane)] = 0.0;
   } else {
-    const long long sb = (sp - lane) * nv + lane;
-    for (int q = 0; q < nv; q++) dst[base + q * kRows] = src[sb + q * kRows];
+    const long long sb = (sp - lane) * nv;
+    for (int q = 0; q < nv; q++) dst[base + vin(nv, q, lane)] = src[sb + vin(nv, q, lane)];
   }
 }
 

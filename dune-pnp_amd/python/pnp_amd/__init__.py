@@ -25,7 +25,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(HERE))          # dune-pnp_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "libpnp_amd.so")
+LIB_PATH = os.environ.get("PNP_AMD_LIB") or os.path.join(PKG_ROOT, "libpnp_amd.so")
 HEADER = os.path.join(REPO_ROOT, "include", "pnp_capi.h")
 
 OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = \

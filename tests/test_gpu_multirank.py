@@ -58,20 +58,20 @@ def test_residual_and_jacobian_partitioned(nranks):
                                          (4, P.PREC_JACOBI), (2, P.PREC_ILU0), (4, P.PREC_ILU0)])
 def test_linear_solve_partitioned(nranks, prec):
     z, mesh, par, orc = golden("pore_small_k0")
-    x = z["newton_pnp_u"]
+    x = z["newton_pnp_x0"]  # the first Newton system (see test_gpu.test_linear_solve_...)
 
     def fn(ctx, r):
         ctx.set_operator(P.OP_PNP)
         J = ctx.jacobian(x)
         rhs = ctx.sync_vector(ctx.residual(x))
-        sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-10, maxit=5000)
+        sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-8, maxit=20000)
         return ctx.sync_vector(sol), res, J, rhs
     outs = run_ranks(nranks, mesh, par, fn)
     J = sum(o[2] for o in outs)
     rhs = outs[0][3]
     for sol, res, _, _ in outs:
         assert res["converged"] == 1, res
-        assert np.linalg.norm(J @ sol - rhs) <= 1.001e-10 * np.linalg.norm(rhs)
+        assert np.linalg.norm(J @ sol - rhs) <= 1.001e-8 * np.linalg.norm(rhs)
     # every rank sees the same global scalars
     assert len({o[1]["iterations"] for o in outs}) == 1
     np.testing.assert_array_equal(outs[0][0], outs[-1][0])

@@ -3,7 +3,7 @@
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_fanr.log"
 for i in 1 2 3; do
-  for v in 1 0; do
+  for v in ${MODES:-1 0}; do
     PNP_ASM_FANR=$v timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab_fanr.log" 2>&1 || exit $?
   done
 done

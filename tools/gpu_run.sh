@@ -17,8 +17,8 @@ for step in "$@"; do
     benchq) timeout -k 10 600 python bench.py --no-cpu --steps 10 > "$OUT/bench.log" 2>&1; rc=$? ;;
     trace)  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --no-cpu --no-solve --steps 3 --warmup 1 > "$OUT/trace.log" 2>&1; rc=$? ;;
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-solve --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
-    pmcf)   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 tools/prof_target.py 4 10 10 > "$OUT/pmcf.log" 2>&1; rc=$? ;;
-    pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
+    pmcf)   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcf.log" 2>&1; rc=$? ;;
+    pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
     ab)     : > "$OUT/ab.log"; rc=0
             for i in 1 2 3; do
               timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
