@@ -92,9 +92,8 @@ struct OpTraits {
   // independent coefficients of one block (i, j) while it accumulates over the fan:
   //   PNP: k0 = sum G_ij W, k1 = sum kappa M_ij, k2 = sum G_ij S+, k3 = sum G_ij S-,
   //        k4 = sum (grad phi . grad psi_i) m_j, (PNP_IE) k5 = sum tau M2_ij, scaled by dt;
-  //   stored values: (0,0) k0, (0,1) k1, (0,2) -k1, (1,0) -k2, (1,1) k0 - k4 (+k5),
-  //   (1,2) k5, (2,0) k3, (2,2) k0 + k4   (expand_block)
-  static constexpr int NK = OP == OP_PNP ? 5 : (OP == OP_PNP_IE ? 6 : 1);
+  //   these are what the matrix stores (k-form, kernels.h expand_k)
+  static constexpr int NK = nks_of(PAT);
 };
 
 // Contributions of element (i, b, c) to row i: residual res[NF], blocks (i,i), (i,b), (i,c).
@@ -214,44 +213,13 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
 }
 
 
-// block coefficients (OpTraits::NK) -> the NV stored values of the block pattern
-template <int OP>
-__device__ __forceinline__ void expand_block(const double *K, double *B) {
-  using T = OpTraits<OP>;
-  constexpr int PAT = T::PAT;
-  if constexpr (OP == OP_PNP || OP == OP_PNP_IE) {
-    B[pat_index(PAT, 0, 0)] = K[0];
-    B[pat_index(PAT, 0, 1)] = K[1];
-    B[pat_index(PAT, 0, 2)] = -K[1];
-    B[pat_index(PAT, 1, 0)] = -K[2];
-    B[pat_index(PAT, 1, 1)] = K[0] - K[4];
-    B[pat_index(PAT, 2, 0)] = K[3];
-    B[pat_index(PAT, 2, 2)] = K[0] + K[4];
-    if constexpr (OP == OP_PNP_IE) {
-      B[pat_index(PAT, 1, 1)] += K[5];
-      B[pat_index(PAT, 1, 2)] = K[5];
-    }
-  } else {
-    B[0] = K[0];
-  }
-}
-
+// store one block's coefficients (k-form, OpTraits::NK values, unmasked: the Dirichlet rows are
+// applied by the consumers, see kernels.h expand_k / mask_rows)
 template <int OP>
 __device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, int s,
-                                            const double *Kc, unsigned dm, bool diag) {
-  using T = OpTraits<OP>;
-  constexpr int PAT = T::PAT, NV = T::NV, NF = T::NF;
-  double B[NV];
-  expand_block<OP>(Kc, B);
-#pragma unroll
-  for (int f = 0; f < NF; f++)
-#pragma unroll
-    for (int g = 0; g < NF; g++) {
-      const int v = pat_index(PAT, f, g);
-      if (v < 0) continue;
-      if ((dm >> f) & 1) B[v] = (diag && f == g) ? 1.0 : 0.0;  // constrained row -> identity
-    }
-  store_vals<NV>(vc + size_t(s) * NV * kRows, lane, B);
+                                            const double *Kc) {
+  constexpr int NK = OpTraits<OP>::NK;
+  store_vals<NK>(vc + size_t(s) * NK * kRows, lane, Kc);
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
@@ -263,7 +231,7 @@ __device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, i
 template <int OP, int JAC, int MINW, int FANR>
 __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
-  constexpr int NF = T::NF, NV = T::NV, NK = T::NK;
+  constexpr int NF = T::NF, NK = T::NK;
   const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * blockDim.x + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
@@ -272,7 +240,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   const int len = int(meta & 63);
   const bool closed = (meta >> 6) & 1;
   const int *__restrict__ cix = L.colidx + off + lane;
-  double *__restrict__ vc = a.vals + size_t(off) * NV;  // chunk base, see vin()
+  double *__restrict__ vc = a.vals + size_t(off) * NK;  // chunk base (k-form), see vin()
 
   const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
   double ui[NF];
@@ -359,13 +327,13 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 #pragma unroll
           for (int v = 0; v < NK; v++) F[v] = P[v];
         } else {
-          store_block<OP>(vc, lane, s, P, dm, false);
+          store_block<OP>(vc, lane, s, P);
         }
 #pragma unroll
         for (int v = 0; v < NK; v++) P[v] = Ct[v];
       }
     } else if constexpr (JAC) {
-      store_block<OP>(vc, lane, s, P, dm, false);
+      store_block<OP>(vc, lane, s, P);
 #pragma unroll
       for (int v = 0; v < NK; v++) P[v] = 0;
     }
@@ -387,9 +355,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
     if (closed) {
 #pragma unroll
       for (int v = 0; v < NK; v++) F[v] += P[v];
-      store_block<OP>(vc, lane, 1, F, dm, false);
+      store_block<OP>(vc, lane, 1, F);
     }
-    store_block<OP>(vc, lane, 0, D, dm, true);
+    store_block<OP>(vc, lane, 0, D);
   }
 #pragma unroll
   for (int f = 0; f < NF; f++) {

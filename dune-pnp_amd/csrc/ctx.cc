@@ -103,7 +103,8 @@ struct pnp_ctx {
   DBuf<double> d_xy;
 
   // operator
-  int kind = -1, nf = 0, pat = 0, nvb = 0;
+  int kind = -1, nf = 0, pat = 0, nvb = 0, nks = 0;  // nvb: block pattern size, nks: stored
+  std::vector<uint8_t> hmask;  // Dirichlet mask of the current operator, owned rows x nf
   pnp::AsmArgs aa{};
   DBuf<double> vals, lu;  // matrix and its ILU(0) factors
   bool lu_valid = false;
@@ -367,8 +368,7 @@ struct pnp_ctx {
   int ilu_factor() {
     if (lu_valid) return PNP_OK;
     hipEvent_t t0 = tb(T_FACT);
-    hipError_t e = hipMemcpyAsync(lu.p, vals.p, sizeof(double) * size_t(L.nslots) * nvb,
-                                  hipMemcpyDeviceToDevice, stream);
+    hipError_t e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
     if (e == hipSuccess) e = pnp::launch_ilu0_factor(dl, L.color_ptr.data(), nf, pat, lu.p, stream);
     if (e != hipSuccess) return hipfail(e, "ilu0 factorisation");
     te(T_FACT, t0);
@@ -381,8 +381,9 @@ struct pnp_ctx {
   int split(int which) {
     if (split_of == which) return PNP_OK;
     hipEvent_t t0 = tb(T_FACT);
-    hipError_t e = pnp::launch_split(nvb, which == 2 ? lu.p : vals.p, d_lsrc.p, (long long)d_lsrc.n,
-                                     d_usrc.p, (long long)d_usrc.n, lvals.p, uvals.p, stream);
+    hipError_t e = pnp::launch_split(dl, nf, pat, which == 1 ? 1 : 0, which == 2 ? lu.p : vals.p,
+                                     d_lsrc.p, (long long)d_lsrc.n, d_usrc.p, (long long)d_usrc.n,
+                                     lvals.p, uvals.p, stream);
     if (e != hipSuccess) return hipfail(e, "split");
     te(T_FACT, t0);
     split_of = which;
@@ -525,6 +526,20 @@ struct pnp_ctx {
 };
 
 using pnp_ctx_t = pnp_ctx;
+
+// host copy of kernels.h expand_k + mask_rows for the CSR export
+static void expand_host(int pat, const double *K, unsigned dm, bool diag, double *B) {
+  if (pat == pnp::kPatPnp) {
+    pnp::expand_k<pnp::kPatPnp>(K, B);
+    pnp::mask_rows<3, pnp::kPatPnp>(B, dm, diag);
+  } else if (pat == pnp::kPatPnpIE) {
+    pnp::expand_k<pnp::kPatPnpIE>(K, B);
+    pnp::mask_rows<3, pnp::kPatPnpIE>(B, dm, diag);
+  } else {
+    pnp::expand_k<pnp::kPatScalar>(K, B);
+    pnp::mask_rows<1, pnp::kPatScalar>(B, dm, diag);
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // mesh / comm
@@ -740,18 +755,18 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       for (int sl = 0; sl < ucl[ch]; sl++) ucol[size_t(uco[ch]) + 64 * sl + ln] = row;
       if (row >= L.n_owned) continue;
       int len = int(L.rowmeta[row] & 63), kl = 0, ku = 1;
-      usrc[size_t(uco[ch]) + ln] = L.chunk_off[ch] + ln;  // slot 0: the diagonal block
+      usrc[size_t(uco[ch]) + ln] = row << 6;  // slot 0: the diagonal block
       for (int sl = 1; sl < len; sl++) {
         int pos = L.chunk_off[ch] + 64 * sl + ln;
         int j = L.colidx[pos];
         if (j >= L.n_owned || j == row) continue;
         if (j < row) {
           lcol[size_t(lco[ch]) + 64 * kl + ln] = j;
-          lsrc[size_t(lco[ch]) + 64 * kl + ln] = pos;
+          lsrc[size_t(lco[ch]) + 64 * kl + ln] = row << 6 | sl;
           kl++;
         } else {
           ucol[size_t(uco[ch]) + 64 * ku + ln] = j;
-          usrc[size_t(uco[ch]) + 64 * ku + ln] = pos;
+          usrc[size_t(uco[ch]) + 64 * ku + ln] = row << 6 | sl;
           ku++;
         }
       }
@@ -928,12 +943,13 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   c->pat = kind == PNP_OP_PNP ? pnp::kPatPnp
                               : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE : pnp::kPatScalar);
   c->nvb = pnp::popc9(c->pat);
+  c->nks = pnp::nks_of(c->pat);
   c->assembled = false;
   c->lu_valid = false;
   c->split_of = 0;
   // SELL padding slots point at the row itself and are never written by the assembly, so they
-  // must hold zeros in the block layout of THIS operator (the SpMV multiplies them)
-  CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nvb, c->stream),
+  // must hold zeros in the k-form layout of THIS operator (the SpMV multiplies them)
+  CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nks, c->stream),
      "clear matrix");
   const pnp::Mesh &m = c->mesh;
   const pnp::LocalLayout &L = c->L;
@@ -957,6 +973,8 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
       lload[size_t(i) * nf + f] = load[size_t(L.l2g[i]) * nf + f];
     }
   CK(hipMemcpy(c->dmask.p, lmask.data(), lmask.size(), hipMemcpyHostToDevice), "dmask");
+  c->dl.dmask = c->dmask.p;
+  c->hmask = lmask;
   CK(hipMemcpy(c->cvec.p, lload.data(), sizeof(double) * lload.size(), hipMemcpyHostToDevice),
      "cvec");
   int nloc = L.n_owned + L.n_ghost;
@@ -1029,7 +1047,8 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
   total *= NV;
   *nnz = total;
   if (!rowptr || !col || !val) return PNP_OK;
-  std::vector<double> hv(size_t(L.nslots) * NV);
+  const int NKS = c->nks;
+  std::vector<double> hv(size_t(L.nslots) * NKS);
   CK(hipMemcpy(hv.data(), c->vals.p, sizeof(double) * hv.size(), hipMemcpyDeviceToHost), "export");
   // rows of the external layout: f*nv + g ; count per row
   int n = nf * nv;
@@ -1051,14 +1070,19 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
     for (int f = 0; f < nf; f++) {
       int R = f * nv + L.l2g[i];
       tmp.clear();
+      unsigned dm = 0;
+      for (int g = 0; g < nf; g++) dm |= unsigned(c->hmask[size_t(i) * nf + g] != 0) << g;
       for (int s = 0; s < len; s++) {
         int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows + lane];
+        double K[8], B[9];
+        for (int q = 0; q < NKS; q++)
+          K[q] = hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NKS +
+                    pnp::vin(NKS, q, lane)];
+        expand_host(c->pat, K, dm, s == 0, B);
         for (int g = 0; g < nf; g++) {
           int v = pnp::pat_index(c->pat, f, g);
           if (v < 0) continue;
-          double value =
-              hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NV + pnp::vin(NV, v, lane)];
-          tmp.push_back({g * nv + L.l2g[j], value});
+          tmp.push_back({g * nv + L.l2g[j], B[v]});
         }
       }
       std::sort(tmp.begin(), tmp.end());

@@ -94,6 +94,48 @@ __host__ __device__ constexpr int pat_index(int mask, int f, int g) {
   return c;
 }
 
+// ---- stored (K-form) block values -----------------------------------------------------------
+// The assembled Jacobian stores, per block (row i, column j), only the independent coefficients
+// of the operator's block (k-form), unmasked.  PnpOperator (kPatPnp), 5 values:
+//   k0 = sum G_ij W, k1 = sum kappa M_ij, k2 = sum G_ij S+, k3 = sum G_ij S-, k4 = sum gp m_j
+// PnpOperator + PnpTOperator (kPatPnpIE) add k5 = sum tau M2_ij; scalar operators store the
+// value itself.  expand_k gives the block pattern's values exactly (each is one coefficient, its
+// negation, or k0 -+ k4 (+ k5)); Dirichlet rows (mask_rows) become identity rows.
+__host__ __device__ constexpr int nks_of(int pat) {
+  return pat == kPatPnp ? 5 : (pat == kPatPnpIE ? 6 : 1);
+}
+
+template <int PAT>
+__host__ __device__ __forceinline__ void expand_k(const double *K, double *B) {
+  if constexpr (PAT == kPatPnp || PAT == kPatPnpIE) {
+    B[pat_index(PAT, 0, 0)] = K[0];
+    B[pat_index(PAT, 0, 1)] = K[1];
+    B[pat_index(PAT, 0, 2)] = -K[1];
+    B[pat_index(PAT, 1, 0)] = -K[2];
+    B[pat_index(PAT, 1, 1)] = K[0] - K[4];
+    B[pat_index(PAT, 2, 0)] = K[3];
+    B[pat_index(PAT, 2, 2)] = K[0] + K[4];
+    if constexpr (PAT == kPatPnpIE) {
+      B[pat_index(PAT, 1, 1)] += K[5];
+      B[pat_index(PAT, 1, 2)] = K[5];
+    }
+  } else {
+    B[0] = K[0];
+  }
+}
+
+// constrained rows f (bit f of dm): identity row (1 on the diagonal block's (f,f), else 0)
+template <int NF, int PAT>
+__host__ __device__ __forceinline__ void mask_rows(double *B, unsigned dm, bool diag) {
+#pragma unroll
+  for (int f = 0; f < NF; f++)
+#pragma unroll
+    for (int g = 0; g < NF; g++) {
+      const int v = pat_index(PAT, f, g);
+      if (v >= 0 && ((dm >> f) & 1)) B[v] = (diag && f == g) ? 1.0 : 0.0;
+    }
+}
+
 // ---- device views ----------------------------------------------------------------------------
 struct DevLayout {
   int n_owned = 0, n_local = 0, nchunks = 0, ncolors = 0;
@@ -117,7 +159,17 @@ struct DevLayout {
   // they need (in the full SELL the lanes of a cache line disagree on lower/upper).
   const int *lchunk_len = nullptr, *lchunk_off = nullptr, *lcolidx = nullptr;
   const int *uchunk_len = nullptr, *uchunk_off = nullptr, *ucolidx = nullptr;
+  // Dirichlet mask of the current operator, [n_owned * nf] (see mask_rows)
+  const uint8_t *dmask = nullptr;
 };
+
+template <int NF>
+__device__ __forceinline__ unsigned row_mask(const DevLayout &L, int row) {
+  unsigned dm = 0;
+#pragma unroll
+  for (int f = 0; f < NF; f++) dm |= unsigned(L.dmask[size_t(row) * NF + f] != 0) << f;
+  return dm;
+}
 
 struct AsmArgs {
   int kind;
@@ -163,9 +215,15 @@ hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals
 hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int pat,  // NOLINT
                       const double *lv, const double *uv, const double *d, double *v, double *t,
                       hipStream_t s);
-// copy a full-SELL matrix (vals or ILU factors) into the L / U split storage
-hipError_t launch_split(int nv, const double *src, const int *lsrc, long long ln, const int *usrc,
-                        long long un, double *lv, double *uv, hipStream_t s);
+// fill the L / U split storage (NV values per block) from the k-form matrix (from_k = 1: expand
+// and mask) or from the ILU factors (from_k = 0: copy).  lsrc/usrc: (row << 6 | slot) of the
+// source block in the full SELL, -1 for padding
+hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,
+                        const int *lsrc, long long ln, const int *usrc, long long un, double *lv,
+                        double *uv, hipStream_t s);
+// lu = the k-form matrix expanded and masked to NV values per block (ILU input)
+hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals, double *lu,
+                         hipStream_t s);
 // ILU(0) of the local (owned x owned) matrix on the stored block pattern, scalar elimination in
 // colour-major vertex order (fields ascending inside a vertex); lu = copy of vals on entry,
 // factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)

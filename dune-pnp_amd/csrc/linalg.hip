@@ -60,23 +60,24 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
                                                  double *__restrict__ y,
                                                  const double *__restrict__ w,
                                                  double *__restrict__ partials) {
-  constexpr int NV = popc9(PAT);
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
   const int row = row_block(L, blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
   double d[2] = {0, 0};
   if (row < L.n_owned) {
     const int chunk = row / kRows, lane = row % kRows;
     const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
     const int *__restrict__ cix = L.colidx + off + lane;
-    const double *__restrict__ vc = vals + size_t(off) * NV;  // chunk base, see vin()
+    const double *__restrict__ vc = vals + size_t(off) * NK;  // chunk base (k-form), see vin()
     double acc[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) acc[f] = 0;
     for (int s = 0; s < len; s++) {
       const int j = cix[s * kRows];
-      double xj[NF], a[NV];
+      double xj[NF], k[NK], a[NV];
 #pragma unroll
       for (int g = 0; g < NF; g++) xj[g] = x[size_t(j) * NF + g];
-      load_vals<NV>(vc + size_t(s) * NV * kRows, lane, a);
+      load_vals<NK>(vc + size_t(s) * NK * kRows, lane, k);
+      expand_k<PAT>(k, a);
 #pragma unroll
       for (int f = 0; f < NF; f++)
 #pragma unroll
@@ -85,8 +86,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
           if (v >= 0) acc[f] += a[v] * xj[g];
         }
     }
+    const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
 #pragma unroll
-    for (int f = 0; f < NF; f++) y[size_t(row) * NF + f] = acc[f];
+    for (int f = 0; f < NF; f++) {
+      if ((dm >> f) & 1) acc[f] = x[size_t(row) * NF + f];
+      y[size_t(row) * NF + f] = acc[f];
+    }
     if constexpr (MODE >= 1) {
 #pragma unroll
       for (int f = 0; f < NF; f++) d[0] += acc[f] * w[size_t(row) * NF + f];
@@ -112,12 +117,14 @@ template <int NF, int PAT>
 __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__restrict__ vals,
                                                    const double *__restrict__ d,
                                                    double *__restrict__ v) {
-  constexpr int NV = popc9(PAT);
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
   const int row = blockIdx.x * kBlock + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
-  double D[NV];
-  load_vals<NV>(vals + size_t(L.chunk_off[chunk]) * NV, lane, D);
+  double K[NK], D[NV];
+  load_vals<NK>(vals + size_t(L.chunk_off[chunk]) * NK, lane, K);
+  expand_k<PAT>(K, D);
+  mask_rows<NF, PAT>(D, row_mask<NF>(L, row), true);
 #pragma unroll
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = d[size_t(row) * NF + f] / D[pat_index(PAT, f, f)];
 }
@@ -388,13 +395,16 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = acc[f];
 }
 
-// full SELL -> split storage; position p of the split layout takes the NV values of source
-// position src[p] (same row, so the same lane), or zeros for padding (src < 0)
-__global__ __launch_bounds__(kBlock) void k_split(int nv, const double *__restrict__ src,
+// split storage position p takes the block (row, slot) = (src >> 6, src & 63) of the full SELL:
+// FROMK: expanded and masked from the k-form matrix, else copied from the NV-form ILU factors;
+// padding (src < 0) gets zeros
+template <int NF, int PAT, int FROMK>
+__global__ __launch_bounds__(kBlock) void k_split(DevLayout L, const double *__restrict__ src,
                                                   const int *__restrict__ lsrc, long long ln,
                                                   const int *__restrict__ usrc, long long un,
                                                   double *__restrict__ lv,
                                                   double *__restrict__ uv) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
   long long p = blockIdx.x * (long long)kBlock + threadIdx.x;
   const int *ps = lsrc;
   double *dst = lv;
@@ -405,13 +415,45 @@ __global__ __launch_bounds__(kBlock) void k_split(int nv, const double *__restri
     dst = uv;
   }
   const int lane = int(p & (kRows - 1));
-  const long long base = (p - lane) * nv;  // slot base (position p - lane is lane 0 of the slot)
-  const int sp = ps[p];
-  if (sp < 0) {
-    for (int q = 0; q < nv; q++) dst[base + vin(nv, q, lane)] = 0.0;
+  double *sb = dst + (p - lane) * NV;  // slot base (position p - lane is lane 0 of the slot)
+  const int code = ps[p];
+  double B[NV];
+  if (code < 0) {
+#pragma unroll
+    for (int q = 0; q < NV; q++) B[q] = 0.0;
   } else {
-    const long long sb = (sp - lane) * nv;
-    for (int q = 0; q < nv; q++) dst[base + vin(nv, q, lane)] = src[sb + vin(nv, q, lane)];
+    const int row = code >> 6, slot = code & 63;
+    const int chunk = row / kRows, rl = row % kRows;
+    if constexpr (FROMK) {
+      double K[NK];
+      load_vals<NK>(src + (size_t(L.chunk_off[chunk]) + size_t(slot) * kRows) * NK, rl, K);
+      expand_k<PAT>(K, B);
+      mask_rows<NF, PAT>(B, row_mask<NF>(L, row), slot == 0);
+    } else {
+      load_vals<NV>(src + (size_t(L.chunk_off[chunk]) + size_t(slot) * kRows) * NV, rl, B);
+    }
+  }
+  // the split position's lane equals the row's lane (same row)
+#pragma unroll
+  for (int q = 0; q < NV; q++) sb[vin(NV, q, lane)] = B[q];
+}
+
+// lu = expand_k + mask_rows of every block of the k-form matrix (NV values per block)
+template <int NF, int PAT>
+__global__ __launch_bounds__(kBlock) void k_expand(DevLayout L, const double *__restrict__ vals,
+                                                   double *__restrict__ lu) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
+  const int row = blockIdx.x * kBlock + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
+  const unsigned dm = row_mask<NF>(L, row);
+  for (int s = 0; s < len; s++) {
+    double K[NK], B[NV];
+    load_vals<NK>(vals + (size_t(off) + size_t(s) * kRows) * NK, lane, K);
+    expand_k<PAT>(K, B);
+    mask_rows<NF, PAT>(B, dm, s == 0);
+    store_vals<NV>(lu + (size_t(off) + size_t(s) * kRows) * NV, lane, B);
   }
 }
 
@@ -749,12 +791,30 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
   return hipGetLastError();
 }
 
-hipError_t launch_split(int nv, const double *src, const int *lsrc, long long ln, const int *usrc,
-                        long long un, double *lv, double *uv, hipStream_t s) {
+hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,
+                        const int *lsrc, long long ln, const int *usrc, long long un, double *lv,
+                        double *uv, hipStream_t s) {
   const long long n = ln + un;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_split, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, nv,
-                     src, lsrc, ln, usrc, un, lv, uv);
+  const dim3 g(unsigned((n + kBlock - 1) / kBlock));
+  PNP_PAT_DISPATCH(nf, pat, {
+    if (from_k)
+      hipLaunchKernelGGL((k_split<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, src, lsrc, ln, usrc,
+                         un, lv, uv);
+    else
+      hipLaunchKernelGGL((k_split<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, src, lsrc, ln, usrc,
+                         un, lv, uv);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals, double *lu,
+                         hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    hipLaunchKernelGGL((k_expand<NFc, PATc>), rows_grid(L.n_owned), dim3(kBlock), 0, s, L, vals,
+                       lu);
+  });
   return hipGetLastError();
 }
 
