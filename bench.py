@@ -9,9 +9,11 @@ and R(x0) are the linear system (SURVEY.md §8(d) "Synthetic inputs").
 
 One step = one full residual + Jacobian assembly of the device-resident state (the headline
 `value`, assembled DOFs/s), timed over K steps bracketed by barrier + device sync.  A second
-timed region runs K x --bicg-iters BiCGSTAB iterations (SSOR = multicolour symmetric GS) on
+timed region runs K x --bicg-iters BiCGSTAB iterations (ILU0 = multicolour ILU(0) by default) on
 the assembled system and reports BiCGSTAB iterations/s.  Roofline numbers come from HIP events
-recorded on the library's own stream around every assembly launch.
+recorded on the library's own stream around every assembly launch; `roofline.traffic` is the
+HBM-side byte count per launch of the same kernel from rocprofv3 PMC passes (FETCH_SIZE x2 +
+WRITE_SIZE, tools/pmc_summary.py), read from the committed profiles/<round>/pmc_summary.json.
 
 Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling -- the mesh is N mirrored
 copies of the pore glued at their outflow/inflow planes, partitioned by RCB (one copy per GPU),
@@ -31,6 +33,20 @@ sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
 import pnp_amd as P  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6290
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+
+
+def pmc_traffic(kernel_prefix):
+    """Per-launch HBM-side bytes of a kernel from the committed rocprofv3 PMC summary, or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, v in ks.items():
+        if kernel_prefix in name:
+            return v["traffic_bytes"]
+    return None
 
 
 def tile_mesh(mesh, n):
@@ -268,7 +284,10 @@ def main():
             "bicgstab_iters_per_s": iters_per_s,
             "bicgstab_ms_per_iter": 1e3 * t_bicg / (args.steps * args.bicg_iters),
             "roofline": {"bound": "hbm", "achieved": achieved_asm, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_asm / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved_asm / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("k_assemble<0, 1, 3, 12>"),
+                         "traffic_source": "profiles/r01/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
+                                           "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble<OP_PNP,1>",
                          "bytes_per_launch": B_asm, "avg_launch_us": asm_avg_s * 1e6},
             "roofline_bicgstab": {"bound": "hbm", "bytes_per_iter": B_it,
