@@ -267,8 +267,9 @@ struct pnp_ctx {
       if (e == hipSuccess) e = hipStreamSynchronize(stream);
       return e == hipSuccess ? PNP_OK : hipfail(e, "allreduce");
     }
-    if (ncclAllReduce(d, d, k, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
-      return fail(PNP_E_RCCL, "ncclAllReduce");
+    ncclResult_t nr = ncclAllReduce(d, d, k, ncclDouble, ncclSum, comm, stream);
+    if (nr != ncclSuccess)
+      return fail(PNP_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
     return PNP_OK;
   }
 
@@ -704,8 +705,10 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   if (c->nranks > 1 && comm->rccl_unique_id) {
     ncclUniqueId id;
     std::memcpy(&id, comm->rccl_unique_id, sizeof id);
-    if (ncclCommInitRank(&c->comm, c->nranks, id, c->rank) != ncclSuccess) {
-      g_err = "ncclCommInitRank failed";
+    ncclResult_t nr = ncclCommInitRank(&c->comm, c->nranks, id, c->rank);
+    if (nr != ncclSuccess) {
+      g_err = std::string("ncclCommInitRank failed: ") + ncclGetErrorString(nr) + " (" +
+              ncclGetLastError(nullptr) + ")";
       return PNP_E_RCCL;
     }
   }

@@ -137,3 +137,40 @@ def test_pb_then_pnp_partitioned_on_refined_pore_ilu0():
     for u, res, rpb in outs:
         assert rpb["converged"] == 1 and res["converged"] == 1, (rpb, res)
         assert np.max(np.abs(u - u1)) <= 1e-5 * np.max(np.abs(u1))
+
+
+def test_tiled_mesh_parity_single_and_partitioned():
+    """bench.py's weak-scaling mesh (mirrored copies, so half the triangles are clockwise):
+    residual and Jacobian vs the oracle on one rank, and the same on 2 ranks."""
+    import importlib.util
+    import meshio
+    import oracle_py as O
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(DATA), "bench.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = B.tile_mesh(P.Mesh.read_gmsh(cfg.meshfile), 2)
+    par = P.Params.from_config(cfg)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    rng = np.random.default_rng(11)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    ro = orc.residual(op, x)
+    Jo = orc.jacobian(op, x)  # analytic
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    r1, J1 = ctx.residual(x), ctx.jacobian(x)
+    assert np.max(np.abs(r1 - ro)) <= 1e-12 * np.max(np.abs(ro))
+    assert abs(J1 - Jo).max() <= 1e-12 * abs(Jo).max()
+
+    def fn(c, r):
+        c.set_operator(P.OP_PNP)
+        return c.residual(x), c.jacobian(x)
+    outs = run_ranks(2, mesh, par, fn)
+    assert np.max(np.abs(sum(o[0] for o in outs) - r1)) <= 1e-13 * np.max(np.abs(r1))
+    assert abs(sum(o[1] for o in outs) - J1).max() <= 1e-13 * abs(J1).max()
