@@ -105,6 +105,16 @@ def barrier_sync(dist, world):
         dist.barrier()
 
 
+def max_over_ranks(dist, world, v):
+    """The job's time: the slowest rank's (gloo all-reduce MAX on the host)."""
+    if world == 1:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(cfg, refine, seconds):
     """The oracle (C restatement of the reference algorithm: FD Jacobian with PDELab eps,
     BCRS-style CSR scatter, ISTL BiCGSTAB) single-threaded on the host, bounded sample."""
@@ -224,15 +234,7 @@ def main():
                   "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                   "reduction": 1e-8, "preconditioner": args.prec}
 
-    def maxall(v):
-        if world == 1:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    t_asm, t_bicg = maxall(t_asm), maxall(t_bicg)
+    t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
     asm_avg_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
     V, T = info["nv_owned"], None
     # algorithmic bytes: B_asm = 8 nnz_red + 16 N + 12 T + 16 V, per rank
