@@ -55,7 +55,7 @@ def test_residual_and_jacobian_partitioned(nranks):
 
 
 @pytest.mark.parametrize("nranks,prec", [(2, P.PREC_NONE), (2, P.PREC_SSOR), (4, P.PREC_SSOR),
-                                         (4, P.PREC_JACOBI), (2, P.PREC_ILU0), (4, P.PREC_ILU0)])
+                                         (2, P.PREC_ILU0), (4, P.PREC_ILU0)])
 def test_linear_solve_partitioned(nranks, prec):
     z, mesh, par, orc = golden("pore_small_k0")
     x = z["newton_pnp_x0"]  # the first Newton system (see test_gpu.test_linear_solve_...)
@@ -79,6 +79,7 @@ def test_linear_solve_partitioned(nranks, prec):
 
 @pytest.mark.parametrize("nranks,prec", [(2, P.PREC_SSOR), (4, P.PREC_SSOR), (4, P.PREC_ILU0)])
 def test_newton_partitioned_matches_single_rank(nranks, prec):
+    """(Jacobi is covered on the scalar PB system in test_pb_jacobi_partitioned.)"""
     z, mesh, par, orc = golden("pore_small_k0")
 
     def fn(ctx, r):
@@ -174,3 +175,23 @@ def test_tiled_mesh_parity_single_and_partitioned():
     outs = run_ranks(2, mesh, par, fn)
     assert np.max(np.abs(sum(o[0] for o in outs) - r1)) <= 1e-13 * np.max(np.abs(r1))
     assert abs(sum(o[1] for o in outs) - J1).max() <= 1e-13 * abs(J1).max()
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_pb_jacobi_partitioned(nranks):
+    """Jacobi BiCGSTAB on the PB system (first Newton step) on 2 and 4 ranks."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = np.zeros(mesh.nv)
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PB)
+        J = ctx.jacobian(x)
+        rhs = ctx.sync_vector(ctx.residual(x), 1)
+        sol, res = ctx.linear_solve(rhs, prec=P.PREC_JACOBI, reduction=1e-8, maxit=20000)
+        return ctx.sync_vector(sol, 1), res, J, rhs
+    outs = run_ranks(nranks, mesh, par, fn)
+    J = sum(o[2] for o in outs)
+    rhs = outs[0][3]
+    for sol, res, _, _ in outs:
+        assert res["converged"] == 1, res
+        assert np.linalg.norm(J @ sol - rhs) <= 1.001e-8 * np.linalg.norm(rhs)
