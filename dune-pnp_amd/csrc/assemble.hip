@@ -407,7 +407,57 @@ __global__ __launch_bounds__(256) void k_mass_apply(DevLayout L, double tau, dou
     cvec[row] -= acc;
 }
 
+// Ion-current observable (calcIonFlux, src/ionFlux.hh:8-96): one thread per boundary segment
+// handled by this rank; seg = {a, c, o, group} local vertices (segment a-c, opposite vertex o of
+// its element).  out[2k] = ip contribution, out[2k+1] = im contribution (summed on the host in
+// segment order, so the result does not depend on the launch).
+__global__ __launch_bounds__(256) void k_ion_flux(int ns, const int4 *__restrict__ seg,
+                                                  const double *__restrict__ xy,
+                                                  const double *__restrict__ x, int cyl,
+                                                  double pi, double *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ns) return;
+  const int4 q = seg[k];
+  const double2 pa = reinterpret_cast<const double2 *>(xy)[q.x];
+  const double2 pc = reinterpret_cast<const double2 *>(xy)[q.y];
+  const double2 po = reinterpret_cast<const double2 *>(xy)[q.z];
+  Geo G;  // vertex order (a, c, o): gi = grad psi_a, gb = grad psi_c, gc = grad psi_o
+  geometry(pa.x, pa.y, pc.x, pc.y, po.x, po.y, G);
+  double gf[3][2];
+#pragma unroll
+  for (int f = 0; f < 3; f++) {
+    const double ua = x[size_t(q.x) * 3 + f], uc = x[size_t(q.y) * 3 + f],
+                 uo = x[size_t(q.z) * 3 + f];
+    gf[f][0] = ua * G.gi0 + uc * G.gb0 + uo * G.gc0;
+    gf[f][1] = ua * G.gi1 + uc * G.gb1 + uo * G.gc1;
+  }
+  const double cp = 0.5 * (x[size_t(q.x) * 3 + 1] + x[size_t(q.y) * 3 + 1]);
+  const double cm = 0.5 * (x[size_t(q.x) * 3 + 2] + x[size_t(q.y) * 3 + 2]);
+  const double tx = pc.x - pa.x, ty = pc.y - pa.y;
+  const double len = sqrt(tx * tx + ty * ty);
+  double factor = len;
+  if (cyl) factor *= 2 * pi * (0.5 * (pa.y + pc.y));
+  double nx = ty / len, ny = -tx / len;
+  if (nx * (po.x - pa.x) + ny * (po.y - pa.y) > 0) {
+    nx = -nx;
+    ny = -ny;
+  }
+  const double gp0 = factor * gf[0][0] * cp, gp1 = factor * gf[0][1] * cp;
+  out[2 * size_t(k)] = (-factor * gf[1][0] + gp0) * nx + (-factor * gf[1][1] + gp1) * ny;
+  const double r = cm / cp;
+  out[2 * size_t(k) + 1] =
+      (-factor * gf[2][0] - gp0 * r) * nx + (-factor * gf[2][1] - gp1 * r) * ny;
+}
+
 }  // namespace
+
+hipError_t launch_ion_flux(int ns, const int4 *seg, const double *xy, const double *x, int cyl,
+                           double pi, double *out, hipStream_t s) {
+  if (ns == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ion_flux, dim3((ns + 255) / 256), dim3(256), 0, s, ns, seg, xy, x, cyl, pi,
+                     out);
+  return hipGetLastError();
+}
 
 hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <cmath>
 #include <cstdio>
@@ -115,6 +116,12 @@ struct pnp_ctx {
   DBuf<double> lvals, uvals, tsgs;
   int split_of = 0;
   DBuf<int> d_blkmap;
+  // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
+  // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
+  // global segment order
+  DBuf<int4> d_fseg;
+  std::vector<int> fseg_group;
+  DBuf<double> fluxout, fluxx, fluxred;
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
@@ -802,6 +809,38 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       c->dl.blkmap = c->d_blkmap.p;
     }
   }
+  {  // boundary segments for the ion-flux observable
+    const pnp::Mesh &mg = c->mesh;
+    auto ekey = [](int a, int b) {
+      if (a > b) std::swap(a, b);
+      return (long long)a << 32 | (unsigned)b;
+    };
+    std::unordered_map<long long, int> opp;
+    opp.reserve(size_t(mg.nb) * 2);
+    for (int b = 0; b < mg.nb; b++) opp[ekey(mg.bseg[2 * b], mg.bseg[2 * b + 1])] = -1;
+    for (int e = 0; e < mg.nt; e++)
+      for (int k = 0; k < 3; k++) {
+        auto it = opp.find(ekey(mg.tri[3 * e + k], mg.tri[3 * e + (k + 1) % 3]));
+        if (it != opp.end() && it->second < 0) it->second = mg.tri[3 * e + (k + 2) % 3];
+      }
+    std::vector<int4> segs;
+    for (int b = 0; b < mg.nb; b++) {
+      const int a = mg.bseg[2 * b], cc = mg.bseg[2 * b + 1], lo = L.g2l[std::min(a, cc)];
+      if (lo < 0 || lo >= L.n_owned) continue;  // another rank's segment
+      const int o = opp[ekey(a, cc)];
+      const int la = L.g2l[a], lc = L.g2l[cc], lop = o >= 0 ? L.g2l[o] : -1;
+      if (la < 0 || lc < 0 || lop < 0) {
+        g_err = "ion flux: the element of a boundary segment is not local";
+        return PNP_E_MESH;
+      }
+      segs.push_back(make_int4(la, lc, lop, mg.bgroup[b]));
+      c->fseg_group.push_back(mg.bgroup[b]);
+    }
+    if ((rc = up(c->d_fseg, segs, "flux segments"))) {
+      g_err = c->err;
+      return rc;
+    }
+  }
   c->dl.lchunk_len = c->d_lchunk_len.p;
   c->dl.lchunk_off = c->d_lchunk_off.p;
   c->dl.lcolidx = c->d_lcolidx.p;
@@ -845,7 +884,9 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   if ((rc = al(c->vals, size_t(L.nslots) * 8, "vals")) ||
       (rc = al(c->lu, size_t(L.nslots) * 8, "lu")) ||
       (rc = al(c->lvals, c->d_lsrc.n * 8, "lvals")) || (rc = al(c->uvals, c->d_usrc.n * 8, "uvals")) ||
-      (rc = al(c->tsgs, nv3, "sgs scratch")) || (rc = al(c->x, nv3, "x")) ||
+      (rc = al(c->tsgs, nv3, "sgs scratch")) || (rc = al(c->fluxx, nv3, "flux state")) ||
+      (rc = al(c->fluxout, 2 * c->fseg_group.size() + 2, "flux out")) ||
+      (rc = al(c->fluxred, 2 * 256, "flux reduce")) || (rc = al(c->x, nv3, "x")) ||
       (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
       (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
       (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
@@ -1125,6 +1166,49 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
   if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
   if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
   return c->download_ext(c->z.p, c->nf, v);
+}
+
+extern "C" int pnp_ion_flux(pnp_ctx *c, const double *x, int32_t nsurf, double *ip, double *im) {
+  if (!c || !ip || !im || nsurf < 0 || nsurf > 256) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  const double *xd = c->x.p;
+  int rc;
+  if (x) {
+    if ((rc = c->upload_ext(x, 3, c->fluxx.p, true))) return rc;
+    xd = c->fluxx.p;
+  } else if (c->nf != 3) {
+    return c->fail(PNP_E_STATE, "ion flux of the context state needs a 3-field (PNP) operator");
+  }
+  const int ns = int(c->fseg_group.size());
+  CK(pnp::launch_ion_flux(ns, c->d_fseg.p, c->d_xy.p, xd, c->params.cylindrical, c->params.pi,
+                          c->fluxout.p, c->stream),
+     "ion flux");
+  std::vector<double> out(2 * size_t(ns)), acc(2 * size_t(nsurf), 0.0);
+  if (ns) {
+    CK(hipMemcpyAsync(out.data(), c->fluxout.p, sizeof(double) * out.size(),
+                      hipMemcpyDeviceToHost, c->stream),
+       "ion flux");
+  }
+  CK(hipStreamSynchronize(c->stream), "ion flux");
+  for (int k = 0; k < ns; k++) {  // global segment order: independent of the launch
+    const int g = c->fseg_group[k];
+    if (g < 0 || g >= nsurf) return c->fail(PNP_E_ARG, "boundary group outside [0, nsurf)");
+    acc[2 * size_t(g)] += out[2 * size_t(k)];
+    acc[2 * size_t(g) + 1] += out[2 * size_t(k) + 1];
+  }
+  if (c->nranks > 1 && nsurf > 0) {
+    CK(hipMemcpy(c->fluxred.p, acc.data(), sizeof(double) * acc.size(), hipMemcpyHostToDevice),
+       "ion flux");
+    if ((rc = c->allreduce_dev(c->fluxred.p, 2 * nsurf))) return rc;
+    CK(hipStreamSynchronize(c->stream), "ion flux");
+    CK(hipMemcpy(acc.data(), c->fluxred.p, sizeof(double) * acc.size(), hipMemcpyDeviceToHost),
+       "ion flux");
+  }
+  for (int g = 0; g < nsurf; g++) {
+    ip[g] = acc[2 * size_t(g)];
+    im[g] = acc[2 * size_t(g) + 1];
+  }
+  return PNP_OK;
 }
 
 extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_newton_result *res) {

@@ -199,6 +199,8 @@ struct Scalars {
 // ---- launchers (return hipError_t of the launch) ----------------------------------------------
 hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s);
 // old-time mass M(x_old) (PnpTOperator / DiffusionTOperator) subtracted into cvec
+hipError_t launch_ion_flux(int ns, const int4 *seg, const double *xy, const double *x, int cyl,
+                           double pi, double *out, hipStream_t s);
 hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi, int cylindrical,
                              const double *x_old, double *cvec, hipStream_t s);
 

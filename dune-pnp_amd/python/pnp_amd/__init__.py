@@ -447,6 +447,18 @@ class Context:
         self._ck(lib().pnp_prec_apply(self.h, int(prec), _ptr(d), _ptr(v)))
         return v
 
+    def ion_flux(self, x=None, nsurf=None):
+        """calcIonFlux (src/ionFlux.hh:8-96): per-surface (ip, im) of x = [phi|c+|c-] (or of
+        the context's state when x is None)."""
+        n = int(nsurf if nsurf is not None else len(self.params.surfaces))
+        ip = np.zeros(n)
+        im = np.zeros(n)
+        xv = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+        if xv is not None and xv.size != 3 * self.mesh.nv:
+            raise PnpError(E_ARG, "ion_flux needs a 3-field state")
+        self._ck(lib().pnp_ion_flux(self.h, _ptr(xv), n, _ptr(ip), _ptr(im)))
+        return ip, im
+
     def newton(self, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
                line_search_maxit=500, prec=PREC_NONE, linear_maxit=20000, check_every=8):
         u = self._vec(u).copy()

@@ -223,6 +223,14 @@ int pnp_sync_vector(pnp_ctx *ctx, double *v, int32_t nfields);
 /* BCExtension interpolation: x0 (3*nv, external layout) from the PB potential phi_pb (nv). */
 int pnp_initial_state(pnp_ctx *ctx, const double *phi_pb, double *x0);
 
+/* Ion-current observable, calcIonFlux (src/ionFlux.hh:8-96, written to current.dat by
+ * src/instationary_pnp_from_pb_md.hh:443-450): per boundary group g < nsurf,
+ *   ip[g] = sum over its segments of len (x 2 PI y) (-grad c+ + c+ grad phi) . n,
+ *   im[g] = ... (-grad c- - c- grad phi) . n,
+ * fields at the segment midpoint, n the unit outer normal.  x: [phi | c+ | c-] (host, external
+ * layout) or NULL for the context's current 3-field state.  Collective on multi-GPU. */
+int pnp_ion_flux(pnp_ctx *ctx, const double *x, int32_t nsurf, double *ip, double *im);
+
 /* ---- device-resident hot path (benchmarks: inputs already in HBM) --------------------------- */
 /* upload x (external layout) into the context's state vector */
 int pnp_state_set(pnp_ctx *ctx, const double *x);

@@ -1062,3 +1062,67 @@ void orc_newton(const orc_mesh *m, const orc_params *p, const orc_operator *op, 
   free(z);
   free(prevu);
 }
+
+/* calcIonFlux, src/ionFlux.hh:8-96.  Elements in tri order, intersections in DUNE's triangle
+ * facet order (0: vertices 0-1, 1: 0-2, 2: 1-2).  At the facet centre (local coordinates in the
+ * element) the P1 fields are evaluated (:60-66), with the element's constant gradients; factor
+ * = facet length (:69), x 2*PI*y(centre) when cylindrical (:70-71, PI = 3.1415 at :4).
+ *   gradCp *= -factor; gradCm *= -factor; gradphi *= factor; gradphi *= cp        (:72-76)
+ *   ip[g] += (gradCp + gradphi) . n                                               (:80)
+ *   gradphi *= cm / cp; im[g] += (gradCm - gradphi) . n                           (:84-85)
+ * for boundary intersections only, g = pg[boundarySegmentIndex] (:79), n = unit outer normal. */
+void orc_ion_flux(const orc_mesh *m, const orc_params *p, const double *x, double *ip,
+                  double *im) {
+  static const int fv[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+  static const double centre[3][2] = {{0.5, 0.0}, {0.0, 0.5}, {0.5, 0.5}};
+  const int nv = m->nv;
+  ehash h;
+  eh_init(&h, m->nb);
+  for (int b = 0; b < m->nb; b++) eh_put(&h, ekey(m->bseg[2 * b], m->bseg[2 * b + 1]), b);
+  for (int g = 0; g < p->nsurf; g++) ip[g] = im[g] = 0.0;
+  for (int e = 0; e < m->nt; e++) {
+    const int *t = m->tri + 3 * e;
+    elgeo G;
+    element_geometry(m, e, &G);
+    double gphi[2] = {0, 0}, gcp[2] = {0, 0}, gcm[2] = {0, 0};
+    for (int i = 0; i < 3; i++)
+      for (int d = 0; d < 2; d++) {
+        gphi[d] += x[t[i]] * G.g[i][d];
+        gcp[d] += x[nv + t[i]] * G.g[i][d];
+        gcm[d] += x[2 * nv + t[i]] * G.g[i][d];
+      }
+    for (int k = 0; k < 3; k++) {
+      const int ia = fv[k][0], ic = fv[k][1], io = 3 - ia - ic;
+      const int b = eh_get(&h, ekey(t[ia], t[ic]));
+      if (b < 0) continue;
+      double psi[3];
+      p1_values(centre[k][0], centre[k][1], psi);
+      double cp = 0, cm = 0;
+      for (int i = 0; i < 3; i++) {
+        cp += psi[i] * x[nv + t[i]];
+        cm += psi[i] * x[2 * nv + t[i]];
+      }
+      const double *pa = m->xy + 2 * t[ia], *pc = m->xy + 2 * t[ic], *po = m->xy + 2 * t[io];
+      const double tx = pc[0] - pa[0], ty = pc[1] - pa[1];
+      const double len = sqrt(tx * tx + ty * ty);
+      double factor = len;
+      if (p->cylindrical) factor *= 2 * p->pi * global_y(&G, centre[k][0], centre[k][1]);
+      double nx = ty / len, ny = -tx / len;
+      if (nx * (po[0] - pa[0]) + ny * (po[1] - pa[1]) > 0) {
+        nx = -nx;
+        ny = -ny;
+      }
+      double gCp[2], gCm[2], gPh[2];
+      for (int d = 0; d < 2; d++) {
+        gCp[d] = -factor * gcp[d];
+        gCm[d] = -factor * gcm[d];
+        gPh[d] = factor * gphi[d] * cp;
+      }
+      const int g = m->bgroup[b];
+      ip[g] += (gCp[0] + gPh[0]) * nx + (gCp[1] + gPh[1]) * ny;
+      for (int d = 0; d < 2; d++) gPh[d] *= cm / cp;
+      im[g] += (gCm[0] - gPh[0]) * nx + (gCm[1] - gPh[1]) * ny;
+    }
+  }
+  eh_free(&h);
+}

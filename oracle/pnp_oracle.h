@@ -163,6 +163,12 @@ typedef struct {
 void orc_newton(const orc_mesh *m, const orc_params *p, const orc_operator *op, double *u,
                 const orc_newton_opts *o, orc_newton_result *res);
 
+/* ---- f3: ion-current observable ---------------------------------------------------------
+ * calcIonFlux, src/ionFlux.hh:8-96 (called from src/instationary_pnp_from_pb_md.hh:443):
+ * x = [phi | c+ | c-] (lexicographic, 3*nv).  ip, im: [nsurf], indexed by bgroup. */
+void orc_ion_flux(const orc_mesh *m, const orc_params *p, const double *x, double *ip,
+                  double *im);
+
 #ifdef __cplusplus
 }
 #endif

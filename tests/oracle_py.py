@@ -116,6 +116,15 @@ class Problem:
         lib().orc_initial_state(C.byref(self.m), C.byref(self.p), _p(phi), _p(out))
         return out
 
+    def ion_flux(self, x):
+        """calcIonFlux (src/ionFlux.hh:8-96): per-surface (ip, im) of the state x."""
+        n = self.p.nsurf
+        ip = np.zeros(n, dtype=np.float64)
+        im = np.zeros(n, dtype=np.float64)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        lib().orc_ion_flux(C.byref(self.m), C.byref(self.p), _p(x), _p(ip), _p(im))
+        return ip, im
+
     # operators ---------------------------------------------------------------------------
     def operator(self, kind, flux=None, mask=None, dt=0.0, z=0.0, phi=None, cp=None, cm=None,
                  x_old=None):

@@ -402,3 +402,23 @@ def test_operator_switch_leaves_no_stale_matrix_entries():
     assert ra["converged"] == rb["converged"] == 1
     assert ra["it_half"] == rb["it_half"]
     np.testing.assert_array_equal(za, zb)
+
+
+# ---- f3: ion-current observable ----------------------------------------------------------------
+@pytest.mark.parametrize("name", ["cylinder_k0", "pore_small_k0", "one_wall_k1"])
+def test_ion_flux_matches_oracle(name):
+    """pnp_ion_flux (GPU, one thread per boundary segment) vs the oracle's calcIonFlux
+    (src/ionFlux.hh:8-96) on the golden converged state; host vector and context state."""
+    z, mesh, par, orc = golden(name)
+    x = z["newton_pnp_u"] if "newton_pnp_u" in z.files else z["pnp_x"]
+    ipo, imo = orc.ion_flux(x)
+    ctx = P.Context(mesh, par)
+    ip, im = ctx.ion_flux(x)
+    scale = max(np.max(np.abs(ipo)), np.max(np.abs(imo)))
+    assert np.max(np.abs(ip - ipo)) <= 1e-12 * scale
+    assert np.max(np.abs(im - imo)) <= 1e-12 * scale
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(x)
+    ip2, im2 = ctx.ion_flux()
+    np.testing.assert_array_equal(ip2, ip)
+    np.testing.assert_array_equal(im2, im)

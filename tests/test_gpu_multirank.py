@@ -195,3 +195,15 @@ def test_pb_jacobi_partitioned(nranks):
     for sol, res, _, _ in outs:
         assert res["converged"] == 1, res
         assert np.linalg.norm(J @ sol - rhs) <= 1.001e-8 * np.linalg.norm(rhs)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_ion_flux_partitioned(nranks):
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["newton_pnp_u"]
+    ipo, imo = orc.ion_flux(x)
+    outs = run_ranks(nranks, mesh, par, lambda ctx, r: ctx.ion_flux(x))
+    scale = max(np.max(np.abs(ipo)), np.max(np.abs(imo)))
+    for ip, im in outs:
+        assert np.max(np.abs(ip - ipo)) <= 1e-12 * scale
+        assert np.max(np.abs(im - imo)) <= 1e-12 * scale

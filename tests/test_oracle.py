@@ -201,3 +201,55 @@ def test_initial_state_dirichlet_values():
     free = mask[:m.nv] == 0
     np.testing.assert_allclose(x0[m.nv:2 * m.nv][free], 0.06 * np.exp(-phi[free]), rtol=1e-15)
     np.testing.assert_allclose(x0[2 * m.nv:][free], 0.06 * np.exp(phi[free]), rtol=1e-15)
+
+
+def _ion_flux_numpy(mesh, surfaces, x, cylindrical, pi=3.1415):
+    """Independent restatement of calcIonFlux (src/ionFlux.hh:8-96), per boundary segment:
+    the segment's element, fields at the segment midpoint, outward unit normal."""
+    nv = mesh.xy.shape[0]
+    tri = mesh.tri
+    owner = {}
+    for e, t in enumerate(tri):
+        for a, b in ((t[0], t[1]), (t[0], t[2]), (t[1], t[2])):
+            owner.setdefault((min(a, b), max(a, b)), []).append(e)
+    ip = np.zeros(len(surfaces))
+    im = np.zeros(len(surfaces))
+    for b, (a, c) in enumerate(mesh.bseg):
+        e = owner[(min(a, c), max(a, c))][0]
+        t = tri[e]
+        P = mesh.xy[t]
+        J = np.array([P[1] - P[0], P[2] - P[0]]).T
+        G = np.linalg.solve(J.T, np.array([[-1.0, 1.0, 0.0], [-1.0, 0.0, 1.0]]))  # 2 x 3
+        gphi, gcp, gcm = (G @ x[k * nv + t] for k in range(3))
+        o = [v for v in t if v != a and v != c][0]
+        pa, pc, po = mesh.xy[a], mesh.xy[c], mesh.xy[o]
+        mid = 0.5 * (pa + pc)
+        cp = 0.5 * (x[nv + a] + x[nv + c])
+        cm = 0.5 * (x[2 * nv + a] + x[2 * nv + c])
+        tvec = pc - pa
+        ln = np.hypot(*tvec)
+        fac = ln * (2 * pi * mid[1] if cylindrical else 1.0)
+        n = np.array([tvec[1], -tvec[0]]) / ln
+        if n @ (po - pa) > 0:
+            n = -n
+        g = mesh.bgroup[b]
+        ip[g] += fac * (-gcp + cp * gphi) @ n
+        im[g] += fac * (-gcm - cm * gphi) @ n
+    return ip, im
+
+
+@pytest.mark.parametrize("name", ["cylinder_k0", "pore_small_k0", "one_wall_k1"])
+def test_ion_flux_matches_numpy_restatement(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    mesh = meshio.Mesh(z["xy"], z["tri"], z["bseg"], z["bgroup"])
+    surfs = [meshio.Surface(int(s[0]), s[1], s[2], int(s[3]), s[4], s[5], int(s[6]), s[7], s[8])
+             for s in z["surfaces"]]
+    l_b, c0, tau, cyl, pi = z["params"]
+    orc = O.Problem(mesh, surfs, l_b=l_b, c0=c0, tau=tau, cylindrical=int(cyl), pi=pi)
+    x = z["newton_pnp_u"] if "newton_pnp_u" in z.files else z["pnp_x"]
+    ip, im = orc.ion_flux(x)
+    ipn, imn = _ion_flux_numpy(mesh, surfs, x, int(cyl), pi)
+    scale = max(np.max(np.abs(ipn)), np.max(np.abs(imn)))
+    assert scale > 0
+    np.testing.assert_allclose(ip, ipn, rtol=0, atol=1e-12 * scale)
+    np.testing.assert_allclose(im, imn, rtol=0, atol=1e-12 * scale)
