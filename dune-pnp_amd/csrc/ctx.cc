@@ -1016,6 +1016,7 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
     for (int f = 0; f < nf; f++) {
       lmask[size_t(i) * nf + f] = mask[size_t(L.l2g[i]) * nf + f];
       lload[size_t(i) * nf + f] = load[size_t(L.l2g[i]) * nf + f];
+      if (a->c_extra) lload[size_t(i) * nf + f] += a->c_extra[size_t(f) * m.nv + L.l2g[i]];
     }
   CK(hipMemcpy(c->dmask.p, lmask.data(), lmask.size(), hipMemcpyHostToDevice), "dmask");
   c->dl.dmask = c->dmask.p;

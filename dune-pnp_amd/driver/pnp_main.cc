@@ -3,12 +3,17 @@
 //   src/pnp_solver_main.cc:70-116  (config, gmsh read, grid, scenario)
 //   src/stationary_pnp_from_pb.hh:93-369  (PB Newton -> BCExtension -> PNP Newton)
 //   src/instationary_pnp_from_pb.hh:320-431  (time loop; implicit Euler here)
+//   src/instationary_pnp_from_pb_md.hh:295-454  (operator split: Poisson + Alexander2 diffusion,
+//                                                 ion current to current.dat)
 //
-// usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|pb] [--steps n]
-//                 [--prec none|ssor|jacobi] [--pb-prec ...] [--device d] [--out prefix]
+// usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb] [--steps n]
+//                 [--prec none|ssor|jacobi|ilu0] [--pb-prec ...] [--device d] [--out prefix]
+//                 [--md-reduction r]
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,9 +36,9 @@ static int prec_of(const std::string &s) {
 
 static void usage() {
   std::printf(
-      "usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|pb]\n"
-      "                [--steps n] [--prec none|ssor|jacobi] [--pb-prec p] [--device d]\n"
-      "                [--out prefix]\n");
+      "usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb]\n"
+      "                [--steps n] [--prec none|ssor|jacobi|ilu0] [--pb-prec p] [--device d]\n"
+      "                [--out prefix] [--md-reduction r]\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -46,6 +51,109 @@ static void write_vector(const std::string &path, const V &v, int nv) {
   }
 }
 
+// StationaryLinearProblemSolver::apply (PDELab; used at src/instationary_pnp_from_pb_md.hh:
+// 349-350, 383-386): r = R(x), A = J(x), solve A z = r to `reduction`, x -= z.
+static void linear_problem(pnp_gpu::Context &ctx, pnp_gpu::GridOperator<V> &go,
+                           pnp_gpu::BiCGStabBackend<V> &ls, V &x, int nfields, double reduction) {
+  V r(x.size(), 0.0), z(x.size(), 0.0);
+  pnp_gpu::Matrix m;
+  go.residual(x, r);
+  go.jacobian(x, m);
+  ctx.sync(r, nfields);
+  ls.apply(m, z, r, reduction);
+  ctx.sync(z, nfields);
+  for (size_t i = 0; i < x.size(); i++) x[i] -= z[i];
+}
+
+// Operator-split time loop of src/instationary_pnp_from_pb_md.hh:411-454.
+//   c+ and c- each take one OneStepMethod<Alexander2> step (a = 1 - sqrt(2)/2):
+//     stage 1: M(u1) - M(u0) + a dt R(u1) = 0                      (DIFF_IMPLICIT_EULER, a dt)
+//     stage 2: M(u2) - M(u0) + (1-a) dt R(u1) + a dt R(u2) = 0      (same + c_extra)
+//   with R = DiffusionOperator (frozen phi, z = +-1) and M = DiffusionTOperator, each stage one
+//   linear solve (StationaryLinearProblemSolver, reduction 1e-5, :380-384); every
+//   potentialUpdateFreq steps the PoissonOperator problem with the new c+- (reduction 1e-10,
+//   :349-350, :421-423); every outputFreq steps the ion current (calcIonFlux) to current.dat
+//   (:424-451) as "time ip_0 im_0 ip_1 im_1 ..." with each ip/im a 2-vector (component 1 = 0).
+static void md_loop(pnp_gpu::Context &ctx, const pnp_gpu::Sysparams &s, V &u, int nv, int rank,
+                    int steps, double md_reduction, int prec, const std::string &out) {
+  V phi(u.begin(), u.begin() + nv), cp(u.begin() + nv, u.begin() + 2 * size_t(nv)),
+      cm(u.begin() + 2 * size_t(nv), u.end());
+  const double a = 1.0 - 0.5 * std::sqrt(2.0), dt = s.cfg.tau;
+  const double red_diff = md_reduction > 0 ? md_reduction : 1e-5;
+  const double red_pois = md_reduction > 0 ? md_reduction : 1e-10;
+  const int nsteps = steps > 0 ? steps : s.cfg.n_steps;
+  const int upd = std::max(1, s.cfg.potential_update_freq), outf = std::max(1, s.cfg.output_freq);
+  const int nsurf = s.cfg.n_surfaces;
+  pnp_gpu::BiCGStabBackend<V> ls(ctx, s.cfg.linear_solver_iterations, prec, 0);
+  std::ofstream current;
+  if (rank == 0) current.open(out.empty() ? std::string("current.dat") : out + "_current.dat");
+  current.precision(17);
+  auto poisson = [&]() {
+    pnp_gpu::Operator op(PNP_OP_POISSON);
+    op.args.cp = cp.data();
+    op.args.cm = cm.data();
+    pnp_gpu::GridOperator<V> go(ctx, op);
+    linear_problem(ctx, go, ls, phi, 1, red_pois);
+  };
+  auto alexander2 = [&](V &c, double z, int field) {
+    const V u0 = c;
+    pnp_gpu::Operator s1(PNP_OP_DIFF_IMPLICIT_EULER);
+    s1.args.dt = a * dt;
+    s1.args.z = z;
+    s1.args.field = field;
+    s1.args.phi = phi.data();
+    s1.args.x_old = u0.data();
+    V u1 = u0;
+    {
+      pnp_gpu::GridOperator<V> go(ctx, s1);
+      linear_problem(ctx, go, ls, u1, 1, red_diff);
+    }
+    pnp_gpu::Operator sp(PNP_OP_DIFF);
+    sp.args.z = z;
+    sp.args.field = field;
+    sp.args.phi = phi.data();
+    V r1(nv, 0.0);
+    {
+      pnp_gpu::GridOperator<V> go(ctx, sp);
+      go.residual(u1, r1);
+      ctx.sync(r1, 1);
+    }
+    for (auto &v : r1) v *= (1.0 - a) * dt;
+    pnp_gpu::Operator s2 = s1;
+    s2.args.c_extra = r1.data();
+    V u2 = u1;
+    {
+      pnp_gpu::GridOperator<V> go(ctx, s2);
+      linear_problem(ctx, go, ls, u2, 1, red_diff);
+    }
+    c = u2;
+  };
+  double time = 0;
+  std::vector<double> ip(nsurf), im(nsurf);
+  V x(3 * size_t(nv));
+  for (int i = 0; i < nsteps; i++) {
+    alexander2(cp, +1.0, 1);
+    alexander2(cm, -1.0, 2);
+    time += dt;
+    if (i % upd == 0) poisson();
+    if (i % outf == 0) {
+      std::copy(phi.begin(), phi.end(), x.begin());
+      std::copy(cp.begin(), cp.end(), x.begin() + nv);
+      std::copy(cm.begin(), cm.end(), x.begin() + 2 * size_t(nv));
+      pnp_gpu::check(pnp_ion_flux(ctx.get(), x.data(), nsurf, ip.data(), im.data()), ctx.get());
+      if (rank == 0) {
+        current << time;
+        for (int g = 0; g < nsurf; g++) current << " " << ip[g] << " 0 " << im[g] << " 0";
+        current << std::endl;
+      }
+    }
+  }
+  poisson();
+  std::copy(phi.begin(), phi.end(), u.begin());
+  std::copy(cp.begin(), cp.end(), u.begin() + nv);
+  std::copy(cm.begin(), cm.end(), u.begin() + 2 * size_t(nv));
+}
+
 int main(int argc, char **argv) {
   if (argc < 2 || !std::strcmp(argv[1], "--help") || !std::strcmp(argv[1], "-h")) {
     usage();
@@ -53,6 +161,7 @@ int main(int argc, char **argv) {
   }
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
   int refine = 0, steps = -1, device = -1;
+  double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
   for (int i = 2; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -66,6 +175,7 @@ int main(int argc, char **argv) {
     else if (a == "--pb-prec") pb_prec = next();
     else if (a == "--device") device = std::atoi(next().c_str());
     else if (a == "--out") out = next();
+    else if (a == "--md-reduction") md_reduction = std::atof(next().c_str());
     else {
       usage();
       return 1;
@@ -173,6 +283,9 @@ int main(int argc, char **argv) {
                       newton.result().iterations, newton.result().linear_iterations,
                       newton.result().defect);
       }
+    } else if (mode == "md") {  // src/instationary_pnp_from_pb_md.hh:295-454
+      if (!out.empty() && rank == 0) write_vector(out + "_x0.dat", u, nv);
+      md_loop(ctx, s, u, nv, rank, steps, md_reduction, prec_of(prec), out);
     } else {
       usage();
       return 1;

@@ -92,7 +92,7 @@ class _Info(C.Structure):
 class _OpArgs(C.Structure):
     _fields_ = [("kind", C.c_int32), ("dt", C.c_double), ("z", C.c_double),
                 ("field", C.c_int32), ("phi", C.c_void_p), ("cp", C.c_void_p),
-                ("cm", C.c_void_p), ("x_old", C.c_void_p)]
+                ("cm", C.c_void_p), ("x_old", C.c_void_p), ("c_extra", C.c_void_p)]
 
 
 class _SolveOpts(C.Structure):
@@ -395,9 +395,10 @@ class Context:
         self._ck(lib().pnp_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in _Info._fields_}
 
-    def set_operator(self, kind, dt=0.0, z=0.0, field=0, phi=None, cp=None, cm=None, x_old=None):
+    def set_operator(self, kind, dt=0.0, z=0.0, field=0, phi=None, cp=None, cm=None, x_old=None,
+                     c_extra=None):
         keep = [np.ascontiguousarray(a, dtype=np.float64) if a is not None else None
-                for a in (phi, cp, cm, x_old)]
+                for a in (phi, cp, cm, x_old, c_extra)]
         a = _OpArgs(kind, dt, z, field, *[None if k is None else k.ctypes.data for k in keep])
         self._ck(lib().pnp_set_operator(self.h, C.byref(a)))
         self.nf = 3 if kind in (OP_PNP, OP_PNP_IMPLICIT_EULER) else 1

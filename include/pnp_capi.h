@@ -159,6 +159,10 @@ typedef struct {
   const double *phi;  /* DIFF*: frozen potential [nv] */
   const double *cp, *cm; /* POISSON: frozen concentrations [nv] */
   const double *x_old;   /* *_IMPLICIT_EULER: previous time level, external layout */
+  /* optional constant added to the residual (external layout, nfields x nv; constrained rows
+   * stay 0): the explicit part of a multi-stage step, e.g. (1-a) dt R(u_1) in the second
+   * stage of Alexander2 (PDELab OneStepMethod, src/instationary_pnp_from_pb_md.hh:387-391) */
+  const double *c_extra;
 } pnp_op_args;
 
 int pnp_set_operator(pnp_ctx *ctx, const pnp_op_args *args);

@@ -422,3 +422,82 @@ def test_ion_flux_matches_oracle(name):
     ip2, im2 = ctx.ion_flux()
     np.testing.assert_array_equal(ip2, ip)
     np.testing.assert_array_equal(im2, im)
+
+
+# ---- f1: operator-split driver (src/instationary_pnp_from_pb_md.hh) -----------------------------
+def _md_oracle(orc, cfg, x0, nsteps):
+    """The _md time loop on the oracle's operators with exact sparse solves: Alexander2 for c+
+    and c- (DiffusionOperator + DiffusionTOperator), PoissonOperator problem every
+    potentialUpdateFreq steps, calcIonFlux every outputFreq steps, a final Poisson solve."""
+    import scipy.sparse.linalg as spla
+    s = cfg.system
+    nv = orc.nv
+    phi, cp, cm = x0[:nv].copy(), x0[nv:2 * nv].copy(), x0[2 * nv:].copy()
+    a, dt = 1.0 - 0.5 * np.sqrt(2.0), s["tau"]
+    upd, outf = max(1, int(s["potentialUpdateFreq"])), max(1, int(s["outputFreq"]))
+    m3 = orc.mask(3)
+
+    def solve(op, x, extra=None):
+        r = orc.residual(op, x) + (0 if extra is None else extra)
+        return x - spla.spsolve(orc.jacobian(op, x).tocsc(), r)
+
+    def poisson(phi, cp, cm):
+        op = orc.operator(O.OP_POISSON, flux=orc.flux(), mask=orc.mask(1),
+                          cp=np.ascontiguousarray(cp), cm=np.ascontiguousarray(cm))
+        return solve(op, phi)
+
+    def alexander2(c, z, field, phi):
+        mask = np.ascontiguousarray(m3[field * nv:(field + 1) * nv])
+        u0 = np.ascontiguousarray(c)
+        op1 = orc.operator(O.OP_DIFF_IE, mask=mask, dt=a * dt, z=z, phi=np.ascontiguousarray(phi),
+                           x_old=u0)
+        u1 = solve(op1, u0.copy())
+        opr = orc.operator(O.OP_DIFF, mask=mask, z=z, phi=np.ascontiguousarray(phi))
+        r1 = (1.0 - a) * dt * orc.residual(opr, u1)
+        return solve(op1, u1, r1)
+
+    t, fluxes = 0.0, []
+    for i in range(nsteps):
+        cp = alexander2(cp, +1.0, 1, phi)
+        cm = alexander2(cm, -1.0, 2, phi)
+        t += dt
+        if i % upd == 0:
+            phi = poisson(phi, cp, cm)
+        if i % outf == 0:
+            fluxes.append((t, orc.ion_flux(np.concatenate([phi, cp, cm]))))
+    phi = poisson(phi, cp, cm)
+    return np.concatenate([phi, cp, cm]), fluxes
+
+
+def test_md_driver_matches_oracle_loop(tmp_path):
+    """The C++ driver's operator-split mode (pnp_main --mode md, 11 steps, linear reductions
+    1e-12) against the same loop on the oracle with exact solves, from the driver's own
+    Boltzmann initial state: final phi/c+/c- and the current.dat lines."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    pre = str(tmp_path / "md")
+    out = subprocess.run([exe, cfgp, "--mode", "md", "--steps", "11", "--md-reduction", "1e-12",
+                          "--out", pre], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    x0 = np.loadtxt(pre + "_x0.dat").T.ravel()
+    u_drv = np.loadtxt(pre + "_pnp.dat").T.ravel()
+    cur = np.atleast_2d(np.loadtxt(pre + "_current.dat"))
+    cfg = P.read_config(cfgp)
+    mesh = P.Mesh.read_gmsh(cfg.meshfile)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    u_orc, fluxes = _md_oracle(orc, cfg, x0, 11)
+    nv = mesh.nv
+    for f in range(3):
+        ref = u_orc[f * nv:(f + 1) * nv]
+        assert np.max(np.abs(u_drv[f * nv:(f + 1) * nv] - ref)) <= 1e-8 * max(np.max(np.abs(ref)), 1e-30)
+    assert cur.shape[0] == len(fluxes)
+    for row, (t, (ip, im)) in zip(cur, fluxes):
+        assert row[0] == pytest.approx(t)
+        got = row[1:].reshape(-1, 4)
+        scale = max(np.max(np.abs(ip)), np.max(np.abs(im)), 1e-30)
+        assert np.max(np.abs(got[:, 0] - ip)) <= 1e-8 * scale
+        assert np.max(np.abs(got[:, 2] - im)) <= 1e-8 * scale
+        assert np.all(got[:, 1] == 0) and np.all(got[:, 3] == 0)
