@@ -1,0 +1,128 @@
+"""Rates for the other SURVEY.md §8(d) configurations on one MI355X (the bench line is config 3;
+these are reported in DESIGN.md).  Each config: mesh, state, timed assembly / BiCGSTAB, and the
+driver-level solve it stands for.  Prints one JSON object per config.
+  config 1: PB on test/sphere_pb refined k=6 (733k vertices), Newton from 0
+  config 2: PNP on test/cylinder refined k=6 (3.3M DOF), PB -> BCExtension -> PNP Newton
+  config 4: instationary PNP (PnpOperator + PnpTOperator, implicit Euler, dt = tau) on
+            test/pore_pnp refined k=3 (556k DOF), 100 steps
+  config 5 (fallback): PNP on test/pore_pnp refined k=5 (8.8M DOF), assembly + BiCGSTAB rates
+usage: python tools/bench_configs.py [1 2 4 5]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
+import pnp_amd as P  # noqa: E402
+
+DATA = os.path.join(ROOT, "data")
+
+
+def rates(ctx, nasm=10, nit=20, prec=P.PREC_ILU0):
+    ctx.assemble_state(2)
+    ctx.bicgstab_iterations(2, prec)
+    ctx.timers(enable=True, reset=True)
+    t0 = time.perf_counter()
+    ctx.assemble_state(nasm)
+    ctx.bicgstab_iterations(1, prec)  # sync
+    ta = time.perf_counter() - t0
+    tm = ctx.timers(enable=False)
+    t0 = time.perf_counter()
+    ctx.bicgstab_iterations(nit, prec)
+    tb = time.perf_counter() - t0
+    return {"assemble_us": tm["assemble_ms"] / tm["assemble_launches"] * 1e3,
+            "assemble_wall_us": ta / nasm * 1e6, "bicgstab_ms_per_iter": tb / nit * 1e3}
+
+
+def pb_then(ctx, mesh, prec=P.PREC_SSOR):
+    ctx.set_operator(P.OP_PB)
+    t0 = time.perf_counter()
+    phi, res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=prec)
+    return phi, res, time.perf_counter() - t0
+
+
+def config1():
+    cfg = P.read_config(os.path.join(DATA, "sphere_pb", "sphere.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(6)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    phi, res, t = pb_then(ctx, mesh)
+    ctx.state_set(np.zeros(mesh.nv))
+    r = rates(ctx, prec=P.PREC_SSOR)
+    return {"config": 1, "mesh": "sphere_pb k=6", "dofs": mesh.nv,
+            "pb_newton": {k: res[k] for k in ("converged", "iterations", "linear_iterations")},
+            "pb_newton_s": t, "assembled_dofs_per_s": mesh.nv / (r["assemble_us"] * 1e-6), **r}
+
+
+def config2():
+    cfg = P.read_config(os.path.join(DATA, "cylinder_config.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(6)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    phi, pbres, tpb = pb_then(ctx, mesh)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    t0 = time.perf_counter()
+    u, res = ctx.newton(x0, reduction=1e-8, prec=P.PREC_ILU0)
+    tn = time.perf_counter() - t0
+    ctx.state_set(x0)
+    r = rates(ctx)
+    n = 3 * mesh.nv
+    return {"config": 2, "mesh": "cylinder k=6", "dofs": n, "pb_newton_s": tpb,
+            "pnp_newton": {k: res[k] for k in ("converged", "status", "iterations",
+                                                "linear_iterations")},
+            "pnp_newton_s": tn, "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6), **r}
+
+
+def config4(nsteps=100):
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(3)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    phi, pbres, tpb = pb_then(ctx, mesh)
+    u = ctx.initial_state(phi)
+    dt = cfg.system["tau"]
+    lin, newt, t_asm, t_sol = 0, 0, 0.0, 0.0
+    t0 = time.perf_counter()
+    for i in range(nsteps):
+        ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=dt, x_old=u)
+        # abs_limit 1e-9: from step 1 on the first defect is ~1e-2 and the residual's rounding
+        # floor ~2e-10, so reduction 1e-8 alone (with PDELab's 1e-12 absolute limit) stalls
+        u, res = ctx.newton(u, reduction=1e-8, abs_limit=1e-9, prec=P.PREC_ILU0)
+        if not res["converged"]:
+            return {"config": 4, "failed_step": i, "result": res}
+        lin += res["linear_iterations"]
+        newt += res["iterations"]
+        t_asm += res["assemble_seconds"]
+        t_sol += res["solve_seconds"]
+    tt = time.perf_counter() - t0
+    ctx.state_set(u)
+    r = rates(ctx)
+    n = 3 * mesh.nv
+    return {"config": 4, "mesh": "pore_pnp k=3", "dofs": n, "steps": nsteps, "seconds": tt,
+            "newton_tolerances": "reduction 1e-8, abs_limit 1e-9",
+            "ms_per_step": tt / nsteps * 1e3, "newton_iterations": newt,
+            "bicgstab_iterations": lin, "assemble_s": t_asm, "solve_s": t_sol,
+            "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6), **r}
+
+
+def config5():
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(5)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    phi, pbres, tpb = pb_then(ctx, mesh)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(x0)
+    r = rates(ctx)
+    n = 3 * mesh.nv
+    return {"config": "5 (fallback: pore_pnp k=5, one GPU)", "dofs": n, "pb_newton_s": tpb,
+            "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6),
+            "bicgstab_iters_per_s": 1e3 / r["bicgstab_ms_per_iter"], **r}
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["1", "2", "4", "5"]
+    for w in which:
+        out = {"1": config1, "2": config2, "4": config4, "5": config5}[w]()
+        print(json.dumps(out), flush=True)
