@@ -531,6 +531,79 @@ struct pnp_ctx {
     res.elapsed = now_s() - t_start;
     return PNP_OK;
   }
+
+  // ISTL CGSolver on J zout = bdev (owned rows), zout zero start; device-resident scalars
+  // (derive stages 10-14).  iterations = matrix-vector products.
+  int cg(const double *bdev, double *zout, const pnp_solve_opts &o, pnp_solve_result &res) {
+    if (!assembled) return fail(PNP_E_STATE, "no Jacobian assembled");
+    double t_start = now_s();
+    long long n = nown();
+    int np = pnp::blas_nparts(n);
+    int prec = o.prec, nsp = 0, rc;
+    hipError_t e = hipMemsetAsync(zout, 0, sizeof(double) * n, stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(rs.p, bdev, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return hipfail(e, "cg init");
+    pnp::Scalars &init = hS[2];
+    std::memset(&init, 0, sizeof init);
+    init.reduction = o.reduction;
+    e = hipMemcpyAsync(S.p, &init, sizeof init, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return hipfail(e, "cg scalars");
+    if ((e = pnp::launch_dot(n, rs.p, rs.p, 0, partials.p, stream)) != hipSuccess)
+      return hipfail(e, "cg norm0");
+    if ((rc = reduce_derive(np, 1, 10))) return rc;
+    if ((rc = precond(prec, rs.p, p.p))) return rc;  // p = M^{-1} r
+    if ((e = pnp::launch_dot(n, p.p, rs.p, 0, partials.p, stream)) != hipSuccess)
+      return hipfail(e, "cg rho");
+    if ((rc = reduce_derive(np, 1, 11))) return rc;
+    int check = o.check_every > 0 ? o.check_every : 8;
+    for (int k = 0; k < o.maxit; k++) {
+      if ((rc = halo(p.p, nf))) return rc;
+      hipEvent_t t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, p.p, v.p, 1, p.p, partials.p, &nsp, stream);
+      if (e != hipSuccess) return hipfail(e, "cg spmv");
+      te(T_SPMV, t0);
+      if ((rc = reduce_derive(nsp, 1, 12))) return rc;
+      t0 = tb(T_BLAS);
+      e = pnp::launch_update_xr(n, S.p, 0, zout, p.p, rs.p, v.p, nullptr, partials.p, stream);
+      if (e != hipSuccess) return hipfail(e, "cg update");
+      if ((rc = reduce_derive(np, 1, 13))) return rc;
+      te(T_BLAS, t0);
+      if ((k + 1) % check == 0 || k + 1 == o.maxit) {
+        e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hipfail(e, "cg poll");
+        if (hS->done) break;
+      }
+      if ((rc = precond(prec, rs.p, y.p))) return rc;  // q = M^{-1} r
+      t0 = tb(T_BLAS);
+      if ((e = pnp::launch_dot(n, y.p, rs.p, 0, partials.p, stream)) != hipSuccess)
+        return hipfail(e, "cg rho'");
+      if ((rc = reduce_derive(np, 1, 14))) return rc;
+      if ((e = pnp::launch_cg_update_p(n, S.p, y.p, p.p, stream)) != hipSuccess)
+        return hipfail(e, "cg p");
+      te(T_BLAS, t0);
+    }
+    e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "cg result");
+    res.converged = hS->done == 1 ? 1 : 0;
+    res.breakdown = 0;
+    res.iterations = hS->iter;
+    res.it_half = hS->iter;
+    res.defect0 = hS->norm0;
+    res.defect = hS->norm;
+    res.reduction = hS->norm0 > 0 ? hS->norm / hS->norm0 : 0.0;
+    res.elapsed = now_s() - t_start;
+    return PNP_OK;
+  }
+
+  // the linear solver selected by o.method
+  int krylov(const double *bdev, double *zout, const pnp_solve_opts &o, pnp_solve_result &res) {
+    if (o.method == PNP_METHOD_CG) return cg(bdev, zout, o, res);
+    if (o.method != PNP_METHOD_BICGSTAB) return fail(PNP_E_ARG, "unknown solver method");
+    return bicgstab(bdev, zout, o, res, 0);
+  }
 };
 
 using pnp_ctx_t = pnp_ctx;
@@ -1153,7 +1226,7 @@ extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const 
   std::memset(res, 0, sizeof *res);
   int rc;
   if ((rc = c->upload_ext(rhs, c->nf, c->b.p, false))) return rc;
-  if ((rc = c->bicgstab(c->b.p, c->z.p, *o, *res, 0))) return rc;
+  if ((rc = c->krylov(c->b.p, c->z.p, *o, *res))) return rc;
   if ((rc = c->download_ext(c->z.p, c->nf, z))) return rc;
   return res->breakdown ? PNP_E_BREAKDOWN : PNP_OK;
 }
@@ -1254,7 +1327,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
     lo.reduction = lin_red;
     pnp_solve_result sr{};
     double ts = now_s();
-    if ((rc = c->bicgstab(c->b.p, c->z.p, lo, sr, 0))) return rc;
+    if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
     res->solve_seconds += now_s() - ts;
     res->linear_iterations += sr.iterations;
     if (sr.breakdown) {

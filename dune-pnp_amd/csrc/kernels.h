@@ -240,6 +240,9 @@ int blas_nparts(long long n);
 // p = (it<1) ? r : beta*(p - omega*v) + r, with beta from Scalars
 hipError_t launch_update_p(long long n, const Scalars *S, const double *r, const double *v,
                            double *p, int first, hipStream_t s);
+// CG: p = q + beta p, beta = S->omega
+hipError_t launch_cg_update_p(long long n, const Scalars *S, const double *q, double *p,
+                              hipStream_t s);
 // x += a*y; r -= a*v; partials <r,r> [, <rt, r>];  a = S->alpha (which=0) or S->omega (which=1)
 hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x, const double *y,
                             double *r, const double *v, const double *rt, double *partials,

@@ -472,6 +472,17 @@ __global__ __launch_bounds__(kBlock) void k_update_p(long long n, const Scalars 
     p[i] = first ? r[i] : beta * (p[i] - om * v[i]) + r[i];
 }
 
+// CG: p = q + beta p (beta kept in S->omega, derive stage 14)
+__global__ __launch_bounds__(kBlock) void k_cg_update_p(long long n, const Scalars *__restrict__ S,
+                                                        const double *__restrict__ q,
+                                                        double *__restrict__ p) {
+  if (S->done) return;
+  const double beta = S->omega;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock)
+    p[i] = q[i] + beta * p[i];
+}
+
 template <int TWO>
 __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars *__restrict__ S,
                                                       int which, double *__restrict__ x,
@@ -521,7 +532,7 @@ __device__ void derive(Scalars *S, int stage);
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const double *__restrict__ partials, int np,
                                                    int k, Scalars *__restrict__ S, int stage) {
-  if (S->done && stage != 0) return;
+  if (S->done && stage != 0 && stage != 10) return;
   double acc[4] = {0, 0, 0, 0};
   for (int i = threadIdx.x; i < np; i += kBlock)
     for (int j = 0; j < k; j++) acc[j] += partials[size_t(i) * k + j];
@@ -548,7 +559,36 @@ __device__ void derive(Scalars *S, int stage) {
     S->done = (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) ? 1 : 0;
     return;
   }
+  if (stage == 10) {  // CG start: red = <r, r>
+    S->norm0 = S->norm = sqrt(S->red[0]);
+    S->it_half = 0;
+    S->iter = 0;
+    S->breakdown = 0;
+    S->done = S->norm0 < 1e-30 ? 1 : 0;
+    return;
+  }
   if (S->done) return;
+  if (stage == 11) {  // CG: rho = <M^{-1} r, r>
+    S->rho = S->red[0];
+    return;
+  }
+  if (stage == 12) {  // CG: lambda = rho / <p, A p>
+    S->h = S->red[0];
+    S->alpha = S->rho / S->h;
+    return;
+  }
+  if (stage == 13) {  // CG: ||r|| after x += lambda p, r -= lambda A p
+    S->norm = sqrt(S->red[0]);
+    S->iter += 1;
+    S->it_half = S->iter;
+    if (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) S->done = 1;
+    return;
+  }
+  if (stage == 14) {  // CG: beta = <q, r> / rho (kept in omega), rho = <q, r>
+    S->omega = S->red[0] / S->rho;
+    S->rho = S->red[0];
+    return;
+  }
   if (stage == 1) {  // h = <rt, v>
     S->h = S->red[0];
     if (fabs(S->h) < kEps) {
@@ -821,6 +861,12 @@ hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals
 hipError_t launch_update_p(long long n, const Scalars *S, const double *r, const double *v,
                            double *p, int first, hipStream_t s) {
   hipLaunchKernelGGL(k_update_p, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, r, v, p, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_cg_update_p(long long n, const Scalars *S, const double *q, double *p,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_cg_update_p, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, q, p);
   return hipGetLastError();
 }
 

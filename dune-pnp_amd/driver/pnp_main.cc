@@ -8,7 +8,7 @@
 //
 // usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb] [--steps n]
 //                 [--prec none|ssor|jacobi|ilu0] [--pb-prec ...] [--device d] [--out prefix]
-//                 [--md-reduction r]
+//                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi]
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
 #include <algorithm>
@@ -38,7 +38,8 @@ static void usage() {
   std::printf(
       "usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb]\n"
       "                [--steps n] [--prec none|ssor|jacobi|ilu0] [--pb-prec p] [--device d]\n"
-      "                [--out prefix] [--md-reduction r]\n");
+      "                [--out prefix] [--md-reduction r]\n"
+      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi]\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -75,7 +76,8 @@ static void linear_problem(pnp_gpu::Context &ctx, pnp_gpu::GridOperator<V> &go,
 //   :349-350, :421-423); every outputFreq steps the ion current (calcIonFlux) to current.dat
 //   (:424-451) as "time ip_0 im_0 ip_1 im_1 ..." with each ip/im a 2-vector (component 1 = 0).
 static void md_loop(pnp_gpu::Context &ctx, const pnp_gpu::Sysparams &s, V &u, int nv, int rank,
-                    int steps, double md_reduction, int prec, const std::string &out) {
+                    int steps, double md_reduction, int prec, int method,
+                    const std::string &out) {
   V phi(u.begin(), u.begin() + nv), cp(u.begin() + nv, u.begin() + 2 * size_t(nv)),
       cm(u.begin() + 2 * size_t(nv), u.end());
   const double a = 1.0 - 0.5 * std::sqrt(2.0), dt = s.cfg.tau;
@@ -84,7 +86,7 @@ static void md_loop(pnp_gpu::Context &ctx, const pnp_gpu::Sysparams &s, V &u, in
   const int nsteps = steps > 0 ? steps : s.cfg.n_steps;
   const int upd = std::max(1, s.cfg.potential_update_freq), outf = std::max(1, s.cfg.output_freq);
   const int nsurf = s.cfg.n_surfaces;
-  pnp_gpu::BiCGStabBackend<V> ls(ctx, s.cfg.linear_solver_iterations, prec, 0);
+  pnp_gpu::BiCGStabBackend<V> ls(ctx, s.cfg.linear_solver_iterations, prec, 0, method);
   std::ofstream current;
   if (rank == 0) current.open(out.empty() ? std::string("current.dat") : out + "_current.dat");
   current.precision(17);
@@ -162,6 +164,8 @@ int main(int argc, char **argv) {
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
   int refine = 0, steps = -1, device = -1;
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
+  // md mode: PbLS, the compile-time LINEARSOLVER of src/instationary_pnp_from_pb_md.hh:20-32,188-211
+  std::string linsolver = "bcgs_ssork";
   for (int i = 2; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -176,6 +180,7 @@ int main(int argc, char **argv) {
     else if (a == "--device") device = std::atoi(next().c_str());
     else if (a == "--out") out = next();
     else if (a == "--md-reduction") md_reduction = std::atof(next().c_str());
+    else if (a == "--linear-solver") linsolver = next();
     else {
       usage();
       return 1;
@@ -285,7 +290,13 @@ int main(int argc, char **argv) {
       }
     } else if (mode == "md") {  // src/instationary_pnp_from_pb_md.hh:295-454
       if (!out.empty() && rank == 0) write_vector(out + "_x0.dat", u, nv);
-      md_loop(ctx, s, u, nv, rank, steps, md_reduction, prec_of(prec), out);
+      int lmethod = PNP_METHOD_BICGSTAB, lprec = PNP_PREC_SSOR;
+      if (linsolver == "bcgs_noprec") lprec = PNP_PREC_NONE;
+      else if (linsolver == "cg_noprec") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_NONE;
+      else if (linsolver == "cg_jacobi") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_JACOBI;
+      else if (linsolver != "bcgs_ssork")
+        throw pnp_gpu::Error(PNP_E_ARG, "unknown --linear-solver " + linsolver);
+      md_loop(ctx, s, u, nv, rank, steps, md_reduction, lprec, lmethod, out);
     } else {
       usage();
       return 1;

@@ -32,6 +32,7 @@ OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = 
     0, -1, -2, -3, -4, -5, -6, -7, -8
 OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI = range(4)
+METHOD_BICGSTAB, METHOD_CG = 0, 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
                 "jacobi": PREC_JACOBI}
 MAX_SURFACES = 64
@@ -97,7 +98,7 @@ class _OpArgs(C.Structure):
 
 class _SolveOpts(C.Structure):
     _fields_ = [("prec", C.c_int32), ("reduction", C.c_double), ("maxit", C.c_int32),
-                ("check_every", C.c_int32)]
+                ("check_every", C.c_int32), ("method", C.c_int32)]
 
 
 class _SolveResult(C.Structure):
@@ -431,10 +432,12 @@ class Context:
         self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), _ptr(rp), _ptr(col), _ptr(val)))
         return sp.csr_matrix((val, col, rp), shape=(n, n))
 
-    def linear_solve(self, rhs, prec=PREC_NONE, reduction=1e-8, maxit=20000, check_every=8):
+    def linear_solve(self, rhs, prec=PREC_NONE, reduction=1e-8, maxit=20000, check_every=8,
+                     method=0):
+        """method 0: ISTL BiCGSTABSolver, 1: ISTL CGSolver (METHOD_CG)."""
         rhs = self._vec(rhs)
         z = np.zeros_like(rhs)
-        o = _SolveOpts(prec, reduction, maxit, check_every)
+        o = _SolveOpts(prec, reduction, maxit, check_every, method)
         r = _SolveResult()
         rc = lib().pnp_linear_solve(self.h, _ptr(rhs), _ptr(z), C.byref(o), C.byref(r))
         if rc not in (OK, E_BREAKDOWN):
@@ -461,10 +464,11 @@ class Context:
         return ip, im
 
     def newton(self, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
-               line_search_maxit=500, prec=PREC_NONE, linear_maxit=20000, check_every=8):
+               line_search_maxit=500, prec=PREC_NONE, linear_maxit=20000, check_every=8,
+               method=0):
         u = self._vec(u).copy()
         o = _NewtonOpts(reduction, abs_limit, min_linear_reduction, maxit, line_search_maxit,
-                        _SolveOpts(prec, 0.0, linear_maxit, check_every))
+                        _SolveOpts(prec, 0.0, linear_maxit, check_every, method))
         r = _NewtonResult()
         self._ck(lib().pnp_newton(self.h, _ptr(u), C.byref(o), C.byref(r)))
         return u, {k: getattr(r, k) for k, _ in _NewtonResult._fields_}

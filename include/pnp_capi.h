@@ -183,11 +183,15 @@ int pnp_jacobian_export(pnp_ctx *ctx, int64_t *nnz, int32_t *rowptr, int32_t *co
 
 /* ---- linear solve (ISTL BiCGSTABSolver semantics) ----------------------------------------- */
 enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3 };
+enum { PNP_METHOD_BICGSTAB = 0, PNP_METHOD_CG = 1 };
 typedef struct {
   int32_t prec;       /* SSOR = one multicolour symmetric Gauss-Seidel sweep (k=1, w=1) */
   double reduction;   /* stop when ||r|| < reduction * ||r0|| (checked every half step) */
   int32_t maxit;
   int32_t check_every; /* host convergence poll period in iterations (0: default 8) */
+  int32_t method;     /* PNP_METHOD_BICGSTAB (ISTL BiCGSTABSolver, the default) or
+                         PNP_METHOD_CG (ISTL CGSolver: LINEARSOLVER CG_NOPREC / CG_Jacobi,
+                         src/instationary_pnp_from_pb_md.hh:198-206) */
 } pnp_solve_opts;
 typedef struct {
   int32_t converged, iterations, breakdown; /* iterations = ceil(half-step counter) */

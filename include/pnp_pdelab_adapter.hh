@@ -171,12 +171,14 @@ struct InverseOperatorResult {  // Dune::InverseOperatorResult
 template <class V>
 class BiCGStabBackend {
  public:
-  BiCGStabBackend(Context &ctx, int maxit, int prec = PNP_PREC_NONE, int verbose = 0)
-      : ctx_(ctx), maxit_(maxit), prec_(prec), verbose_(verbose) {}
+  // method PNP_METHOD_CG gives the ISTLBackend_NOVLP_CG_* backends (ISTL CGSolver)
+  BiCGStabBackend(Context &ctx, int maxit, int prec = PNP_PREC_NONE, int verbose = 0,
+                  int method = PNP_METHOD_BICGSTAB)
+      : ctx_(ctx), maxit_(maxit), prec_(prec), verbose_(verbose), method_(method) {}
   // z = A^{-1} r (A = last assembled Jacobian), ISTL BiCGSTABSolver semantics
   void apply(Matrix &A, V &z, V &r, double reduction) {
     if (!A.assembled) throw Error(PNP_E_STATE, "pnp: matrix not assembled");
-    pnp_solve_opts o{prec_, reduction, maxit_, 8};
+    pnp_solve_opts o{prec_, reduction, maxit_, 8, method_};
     pnp_solve_result res{};
     int rc = pnp_linear_solve(ctx_.get(), data(r), data(z), &o, &res);
     if (rc != PNP_OK && rc != PNP_E_BREAKDOWN) check(rc, ctx_.get());
@@ -199,10 +201,11 @@ class BiCGStabBackend {
   const InverseOperatorResult &result() const { return res_; }
   int prec() const { return prec_; }
   int maxit() const { return maxit_; }
+  int method() const { return method_; }
 
  private:
   Context &ctx_;
-  int maxit_, prec_, verbose_;
+  int maxit_, prec_, verbose_, method_;
   InverseOperatorResult res_;
 };
 
@@ -228,6 +231,7 @@ class Newton {
     go_.bind();
     o_.linear.prec = ls_.prec();
     o_.linear.maxit = ls_.maxit();
+    o_.linear.method = ls_.method();
     o_.linear.check_every = 8;
     pnp_newton_result r{};
     check(pnp_newton(go_.context().get(), data(u_), &o_, &r), go_.context().get());
@@ -249,7 +253,7 @@ class Newton {
   GridOperator<V> &go_;
   V &u_;
   BiCGStabBackend<V> &ls_;
-  pnp_newton_opts o_{1e-8, 1e-12, 1e-3, 40, 10, {PNP_PREC_NONE, 0.0, 20000, 8}};
+  pnp_newton_opts o_{1e-8, 1e-12, 1e-3, 40, 10, {PNP_PREC_NONE, 0.0, 20000, 8, PNP_METHOD_BICGSTAB}};
   Result res_;
   int verbose_ = 0;
 };

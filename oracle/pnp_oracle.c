@@ -989,6 +989,60 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
   free(p); free(v); free(t); free(y); free(rt);
 }
 
+/* ISTL CGSolver::apply (dune-istl 2.2 solvers.hh; the ISTLBackend_NOVLP_CG_NOPREC / _CG_Jacobi
+ * backends selected by LINEARSOLVER 3 / 4, src/instationary_pnp_from_pb_md.hh:198-206):
+ *   r = b - A x; def0 = ||r||; done if def0 < 1e-30;  p = M^{-1} r; rho = <p, r>
+ *   for i = 1 .. maxit:  q = A p; lambda = rho / <p, q>; x += lambda p; r -= lambda q;
+ *                        def = ||r||; converged if def < reduction def0 or def < 1e-30;
+ *                        q = M^{-1} r; rho' = <q, r>; p = q + (rho'/rho) p; rho = rho'
+ * iterations = i (matrix-vector products).  b is overwritten with the residual. */
+void orc_cg(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
+            orc_solve_result *res) {
+  int n = A->n;
+  double *r = b;
+  double *p = (double *)calloc(n, sizeof(double));
+  double *q = (double *)calloc(n, sizeof(double));
+  prec_t P;
+  prec_init(&P, A, prec);
+  memset(res, 0, sizeof *res);
+  orc_spmv(A, x, q);
+  for (int i = 0; i < n; i++) r[i] -= q[i];
+  double def0 = sqrt(dot(n, r, r)), def = def0;
+  res->defect0 = def0;
+  int it = 0;
+  if (def0 < 1e-30) {
+    res->converged = 1;
+  } else {
+    prec_apply(&P, p, r);
+    double rho = dot(n, p, r);
+    for (it = 1; it <= maxit; it++) {
+      orc_spmv(A, p, q);
+      const double lambda = rho / dot(n, p, q);
+      for (int i = 0; i < n; i++) x[i] += lambda * p[i];
+      for (int i = 0; i < n; i++) r[i] -= lambda * q[i];
+      def = sqrt(dot(n, r, r));
+      if (def < reduction * def0 || def < 1e-30) {
+        res->converged = 1;
+        break;
+      }
+      memset(q, 0, sizeof(double) * n);
+      prec_apply(&P, q, r);
+      const double rho_new = dot(n, q, r);
+      const double beta = rho_new / rho;
+      for (int i = 0; i < n; i++) p[i] = q[i] + beta * p[i];
+      rho = rho_new;
+    }
+    if (it > maxit) it = maxit;
+  }
+  res->it_half = it;
+  res->iterations = it;
+  res->defect = def;
+  res->reduction = def0 > 0 ? def / def0 : 0.0;
+  prec_free(&P);
+  free(p);
+  free(q);
+}
+
 /* ----------------------------------------------------------------------------------------
  * Newton (a12), PDELab newton.hh semantics
  * ---------------------------------------------------------------------------------------- */

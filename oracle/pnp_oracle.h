@@ -147,6 +147,9 @@ void orc_spmv(const orc_csr *A, const double *x, double *y);
 /* ISTL BiCGSTABSolver::apply(x, b, res): x overwritten (start value = x), b overwritten. */
 void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
                   orc_solve_result *res);
+/* ISTL CGSolver (LINEARSOLVER CG_NOPREC / CG_Jacobi), see pnp_oracle.c */
+void orc_cg(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
+            orc_solve_result *res);
 
 /* ---- nonlinear / time (a12, a13) ------------------------------------------------------ */
 typedef struct {

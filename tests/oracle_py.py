@@ -199,6 +199,15 @@ class Problem:
 
 def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
     """ISTL-semantics BiCGStab on a scipy CSR matrix (sorted indices)."""
+    return _krylov("orc_bicgstab", A, b, prec, reduction, maxit, x0)
+
+
+def cg(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
+    """ISTL-semantics CG (CGSolver) on a scipy CSR matrix."""
+    return _krylov("orc_cg", A, b, prec, reduction, maxit, x0)
+
+
+def _krylov(fn, A, b, prec, reduction, maxit, x0):
     A = A.tocsr()
     A.sort_indices()
     rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
@@ -209,6 +218,6 @@ def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
     x = np.zeros(A.shape[0]) if x0 is None else np.array(x0, dtype=np.float64)
     bb = np.array(b, dtype=np.float64)
     res = OrcSolveResult()
-    lib().orc_bicgstab(C.byref(M), prec, C.c_double(reduction), maxit, _p(x), _p(bb),
+    getattr(lib(), fn)(C.byref(M), prec, C.c_double(reduction), maxit, _p(x), _p(bb),
                        C.byref(res))
     return x, res

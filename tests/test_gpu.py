@@ -501,3 +501,25 @@ def test_md_driver_matches_oracle_loop(tmp_path):
         assert np.max(np.abs(got[:, 0] - ip)) <= 1e-8 * scale
         assert np.max(np.abs(got[:, 2] - im)) <= 1e-8 * scale
         assert np.all(got[:, 1] == 0) and np.all(got[:, 3] == 0)
+
+
+# ---- f4: ISTL CGSolver (LINEARSOLVER CG_NOPREC / CG_Jacobi) ---------------------------------------
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI])
+def test_cg_matches_oracle_cg(prec):
+    """Device-resident CG vs the oracle's ISTL CGSolver on the PB system (phi = 0): same solution,
+    iteration counts equal up to one (the stop test compares a norm with summation-order
+    rounding)."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    ctx = P.Context(mesh, par)
+    op = set_ops(z, ctx, orc, "pb")
+    x = np.zeros(mesh.nv)
+    J = ctx.jacobian(x)
+    rhs = ctx.residual(x)
+    sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-10, maxit=5000, method=P.METHOD_CG)
+    assert res["converged"] == 1, res
+    assert np.linalg.norm(J @ sol - rhs) <= 1.001e-10 * np.linalg.norm(rhs)
+    xo, ro = O.cg(orc.jacobian(op, x), rhs, prec=O.PREC_JACOBI if prec == P.PREC_JACOBI
+                  else O.PREC_NONE, reduction=1e-10, maxit=5000)
+    assert ro.converged
+    assert abs(res["iterations"] - ro.iterations) <= 1
+    assert np.max(np.abs(sol - xo)) <= 1e-8 * np.max(np.abs(xo))

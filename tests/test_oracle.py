@@ -253,3 +253,39 @@ def test_ion_flux_matches_numpy_restatement(name):
     assert scale > 0
     np.testing.assert_allclose(ip, ipn, rtol=0, atol=1e-12 * scale)
     np.testing.assert_allclose(im, imn, rtol=0, atol=1e-12 * scale)
+
+
+def test_cg_oracle_solves_pb_system_and_counts_matvecs():
+    """orc_cg (ISTL CGSolver semantics) on the PB Jacobian at phi = 0: converges, the solution
+    satisfies the system, and CG_NOPREC / CG_Jacobi agree with a numpy CG restatement on the
+    iteration count (matrix-vector products)."""
+    z = np.load(os.path.join(GOLD, "pore_small_k0.npz"))
+    mesh = meshio.Mesh(z["xy"], z["tri"], z["bseg"], z["bgroup"])
+    surfs = [meshio.Surface(int(s[0]), s[1], s[2], int(s[3]), s[4], s[5], int(s[6]), s[7], s[8])
+             for s in z["surfaces"]]
+    l_b, c0, tau, cyl, pi = z["params"]
+    orc = O.Problem(mesh, surfs, l_b=l_b, c0=c0, tau=tau, cylindrical=int(cyl), pi=pi)
+    op = orc.operator(O.OP_PB, flux=orc.flux(), mask=orc.mask(1))
+    x = np.zeros(mesh.xy.shape[0])
+    J = orc.jacobian(op, x).tocsr()
+    b = orc.residual(op, x)
+    for prec in (O.PREC_NONE, O.PREC_JACOBI):
+        sol, res = O.cg(J, b, prec=prec, reduction=1e-10, maxit=5000)
+        assert res.converged
+        assert np.linalg.norm(J @ sol - b) <= 1.001e-10 * np.linalg.norm(b)
+        Dinv = 1 / J.diagonal() if prec == O.PREC_JACOBI else np.ones_like(b)
+        r = b.copy()
+        p = Dinv * r
+        rho = p @ r
+        d0 = np.linalg.norm(r)
+        for it in range(1, 5001):
+            q = J @ p
+            lam = rho / (p @ q)
+            r -= lam * q
+            if np.linalg.norm(r) < 1e-10 * d0:
+                break
+            q = Dinv * r
+            rho_new = q @ r
+            p = q + rho_new / rho * p
+            rho = rho_new
+        assert res.iterations == it
