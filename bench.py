@@ -251,7 +251,7 @@ def main():
     iters_per_s = args.steps * args.bicg_iters / t_bicg
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # the contract: rank 0 at N=1 only
         cb = cpu_baseline(cfg, args.cpu_refine, args.cpu_seconds)
         cpu = {"value": cb["dofs_per_s"], "unit": "assembled DOFs/s", "cores": 1, "kind": "port",
                "sample": (f"oracle/pnp_oracle.c (C restatement of the reference: PnpOperator "
