@@ -299,17 +299,14 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
     auto U = [&](int t, int g, int h) -> double {
       return vj[size_t(t) * NV * kRows + vin(NV, pat_index(PAT, g, h), lj)];
     };
-#pragma unroll
     for (int g = 0; g < NF; g++) {
       const double dinv = U(0, g, g);  // stored inverted
-#pragma unroll
       for (int f = 0; f < NF; f++) {
         if (pat_index(PAT, f, g) < 0) continue;
         const double l = A(s, f, g) * dinv;
         A(s, f, g) = l;
         if (l == 0.0) continue;
         // q = (j, h > g): block (i, j), slot s of row i, diagonal block of row j
-#pragma unroll
         for (int h = g + 1; h < NF; h++)
           if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
             A(s, f, h) -= l * U(0, g, h);
@@ -319,7 +316,6 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
           if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;  // padding -> m == row
           for (int u = 1; u < lenj; u++) {
             if (cixj[u * kRows] != m) continue;
-#pragma unroll
             for (int h = 0; h < NF; h++)
               if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(t, f, h) -= l * U(u, g, h);
             break;
@@ -329,20 +325,16 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
     }
   }
   // 2) inside the vertex: rows (i,f) eliminated by (i,g<f); invert the pivots
-#pragma unroll
   for (int f = 0; f < NF; f++) {
-#pragma unroll
     for (int g = 0; g < f; g++) {
       if (pat_index(PAT, f, g) < 0) continue;
       const double l = A(0, f, g) * A(0, g, g);  // A(0,g,g) already inverted
       A(0, f, g) = l;
-#pragma unroll
       for (int h = g + 1; h < NF; h++)
         if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(0, f, h) -= l * A(0, g, h);
       for (int t = 1; t < leni; t++) {
         const int m = cixi[t * kRows];
         if (m <= row || m >= L.n_owned) continue;
-#pragma unroll
         for (int h = 0; h < NF; h++)
           if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0) A(t, f, h) -= l * A(t, g, h);
       }
