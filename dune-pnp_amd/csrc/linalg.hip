@@ -54,7 +54,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double *out) {
 // ------------------------------------------------------------------------------------------
 // SpMV (+ fused dots)
 // ------------------------------------------------------------------------------------------
-template <int NF, int PAT, int MODE>
+template <int NF, int PAT, int MODE, int SB>
 __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__restrict__ vals,
                                                  const double *__restrict__ x,
                                                  double *__restrict__ y,
@@ -71,20 +71,36 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
     double acc[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) acc[f] = 0;
-    for (int s = 0; s < len; s++) {
-      const int j = cix[s * kRows];
-      double xj[NF], k[NK], a[NV];
+    // slots in batches of SB: their column indices, then their gathers and values, are
+    // issued together (memory-level parallelism inside the thread)
+    for (int s0 = 0; s0 < len; s0 += SB) {
+      int j[SB];
 #pragma unroll
-      for (int g = 0; g < NF; g++) xj[g] = x[size_t(j) * NF + g];
-      load_vals<NK>(vc + size_t(s) * NK * kRows, lane, k);
-      expand_k<PAT>(k, a);
+      for (int b = 0; b < SB; b++) j[b] = s0 + b < len ? cix[(s0 + b) * kRows] : row;
+      double xj[SB][NF], k[SB][NK];
 #pragma unroll
-      for (int f = 0; f < NF; f++)
+      for (int b = 0; b < SB; b++) {
 #pragma unroll
-        for (int g = 0; g < NF; g++) {
-          const int v = pat_index(PAT, f, g);
-          if (v >= 0) acc[f] += a[v] * xj[g];
+        for (int g = 0; g < NF; g++) xj[b][g] = x[size_t(j[b]) * NF + g];
+        if (s0 + b < len) {
+          load_vals<NK>(vc + size_t(s0 + b) * NK * kRows, lane, k[b]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < NK; q++) k[b][q] = 0.0;
         }
+      }
+#pragma unroll
+      for (int b = 0; b < SB; b++) {
+        double a[NV];
+        expand_k<PAT>(k[b], a);
+#pragma unroll
+        for (int f = 0; f < NF; f++)
+#pragma unroll
+          for (int g = 0; g < NF; g++) {
+            const int v = pat_index(PAT, f, g);
+            if (v >= 0) acc[f] += a[v] * xj[b][g];
+          }
+      }
     }
     const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
 #pragma unroll
@@ -677,6 +693,34 @@ int blas_nparts(long long n) {
     }                                                                     \
   } while (0)
 
+// SpMV slot batch (PNP_SPMV_BATCH = 1, 2 or 4; A/B knob)
+static int spmv_batch() {
+  static const int v = [] {
+    const char *e = std::getenv("PNP_SPMV_BATCH");
+    const int b = e ? std::atoi(e) : 4;
+    return (b == 1 || b == 2 || b == 4) ? b : 4;
+  }();
+  return v;
+}
+
+template <int NF, int PAT, int MODE>
+static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double *vals,
+                        const double *x, double *y, const double *w, double *partials) {
+  switch (spmv_batch()) {
+    case 1:
+      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 1>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 2>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+      break;
+    default:
+      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 4>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
+                         partials);
+  }
+}
+
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
                        hipStream_t s) {
@@ -685,14 +729,11 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
-      hipLaunchKernelGGL((k_spmv<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
+      (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials);
     else if (mode == 1)
-      hipLaunchKernelGGL((k_spmv<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
+      (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials);
     else
-      hipLaunchKernelGGL((k_spmv<NFc, PATc, 2>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
+      (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials);
   });
   return hipGetLastError();
 }
