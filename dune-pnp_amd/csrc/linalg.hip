@@ -15,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace pnp {
@@ -229,7 +231,9 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
 // colour in parallel (never adjacent), the NF fields of a row in sequence (ascending forward,
 // descending backward).  Forward: t_i = d_i - sum_{j lower} A_ij v_j, then the block-lower
 // solve; backward: v_i += D_i^{-1}(t_i - sum_{j upper} A_ij v_j - D_i v_i), field by field.
-template <int NF, int PAT, int FWD, int LPR, int B>
+// KIND 1 forward, 0 backward, 2 both for the last colour (no upper neighbours: its backward
+// step is pointwise, t stays in registers).
+template <int NF, int PAT, int KIND, int LPR, int B>
 __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int nk,
                                                       const double *__restrict__ lv,
                                                       const double *__restrict__ uv,
@@ -237,6 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
                                                       double *__restrict__ v,
                                                       double *__restrict__ t) {
   constexpr int NV = popc9(PAT);
+  constexpr bool FWD = KIND != 0;
   // XCD remap pays here (+5 % measured): a colour's rows are a contiguous range
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
   const int k = gt / LPR, q = gt % LPR;
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   for (int f = 0; f < NF; f++) {
     if (FWD) {
       rhs[f] = d[size_t(row) * NF + f] + acc[f];
-      t[size_t(row) * NF + f] = rhs[f];
+      if (KIND == 1) t[size_t(row) * NF + f] = rhs[f];
       vi[f] = 0.0;
     } else {
       rhs[f] = t[size_t(row) * NF + f] + acc[f];
@@ -260,16 +265,19 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   }
   load_vals<NV>(R.dg, R.lane, Dg);
 #pragma unroll
-  for (int ff = 0; ff < NF; ff++) {
-    const int f = FWD ? ff : NF - 1 - ff;
-    double r = rhs[f];
+  for (int pass = 0; pass < (KIND == 2 ? 2 : 1); pass++)
 #pragma unroll
-    for (int g = 0; g < NF; g++) {
-      const int qq = pat_index(PAT, f, g);
-      if (qq >= 0) r -= Dg[qq] * vi[g];
+    for (int ff = 0; ff < NF; ff++) {
+      const bool up = KIND == 0 || pass == 1;
+      const int f = up ? NF - 1 - ff : ff;
+      double r = rhs[f];
+#pragma unroll
+      for (int g = 0; g < NF; g++) {
+        const int qq = pat_index(PAT, f, g);
+        if (qq >= 0) r -= Dg[qq] * vi[g];
+      }
+      vi[f] += r / Dg[pat_index(PAT, f, f)];
     }
-    vi[f] += r / Dg[pat_index(PAT, f, f)];
-  }
 #pragma unroll
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = vi[f];
 }
@@ -359,15 +367,50 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
   }
 }
 
-// forward (unit lower, colours ascending) and backward (upper, colours descending) sweeps over
-// the split factors; LPR lanes per row as in k_sgs_color
-template <int NF, int PAT, int FWD, int LPR, int B>
+// y <- Ld^-1 y (unit lower part of the factored diagonal block, fields ascending)
+template <int NF, int PAT, int NV>
+__device__ __forceinline__ void diag_lower_solve(const double (&Dg)[NV], double (&y)[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; f++)
+#pragma unroll
+    for (int g = 0; g < f; g++) {
+      const int qq = pat_index(PAT, f, g);
+      if (qq >= 0) y[f] -= Dg[qq] * y[g];
+    }
+}
+
+// y <- U^-1 y (upper part, pivots stored inverted, fields descending)
+template <int NF, int PAT, int NV>
+__device__ __forceinline__ void diag_upper_solve(const double (&Dg)[NV], double (&y)[NF]) {
+#pragma unroll
+  for (int ff = NF - 1; ff >= 0; ff--) {
+#pragma unroll
+    for (int h = ff + 1; h < NF; h++) {
+      const int qq = pat_index(PAT, ff, h);
+      if (qq >= 0) y[ff] -= Dg[qq] * y[h];
+    }
+    y[ff] *= Dg[pat_index(PAT, ff, ff)];
+  }
+}
+
+// Sweeps over the split factors, one colour per launch, LPR lanes per row as in k_sgs_color.
+// KIND kIluFwd / kIluBwd: forward (unit lower, colours ascending) / backward (upper, colours
+// descending).  kIluLast: the last colour's forward and backward in one launch -- it has no upper
+// neighbours (every row after it in the colour-major order is of its own colour, hence not
+// adjacent), so its backward step is pointwise; the arithmetic is that of the two launches.
+// (Folding Ld into the coupling blocks, L'_ij = Lo_ij Ld_j^-1, would drop the colour-0 forward
+// launch too, but z = Ld y cancels on the strongly coupled drift blocks: +24 % iterations on the
+// 24 V pore case, measured -- DESIGN.md §4.)
+enum { kIluFwd = 0, kIluBwd = 1, kIluLast = 2 };
+
+template <int NF, int PAT, int KIND, int LPR, int B>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
                                                        const double *__restrict__ lv,
                                                        const double *__restrict__ uv,
                                                        const double *__restrict__ d,
                                                        double *__restrict__ v) {
   constexpr int NV = popc9(PAT);
+  constexpr bool FWD = KIND != kIluBwd;
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
   const int k = gt / LPR, q = gt % LPR;
   const bool live = r0 + k < r1;
@@ -380,25 +423,8 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   for (int f = 0; f < NF; f++) acc[f] += FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
   double Dg[NV];
   load_vals<NV>(R.dg, R.lane, Dg);
-  if (FWD) {
-#pragma unroll
-    for (int f = 0; f < NF; f++)
-#pragma unroll
-      for (int g = 0; g < f; g++) {
-        const int qq = pat_index(PAT, f, g);
-        if (qq >= 0) acc[f] -= Dg[qq] * acc[g];
-      }
-  } else {
-#pragma unroll
-    for (int ff = NF - 1; ff >= 0; ff--) {
-#pragma unroll
-      for (int h = ff + 1; h < NF; h++) {
-        const int qq = pat_index(PAT, ff, h);
-        if (qq >= 0) acc[ff] -= Dg[qq] * acc[h];
-      }
-      acc[ff] *= Dg[pat_index(PAT, ff, ff)];
-    }
-  }
+  if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
+  if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
 #pragma unroll
   for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = acc[f];
 }
@@ -811,21 +837,19 @@ static int sweep_cfg() {
 hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
                       const double *uv, const double *d, double *v, double *t, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
+  const int nc = L.ncolors;
   // the forward sweep writes every owned row exactly once and reads only rows of earlier
   // colours, so v needs no zeroing (ISTL starts the sweep from v = 0)
   PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
-    for (int c = 0; c < L.ncolors; c++) {
-      int n = cp[c + 1] - cp[c];
+    auto go = [&](auto kind, int c) {
+      const int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 1, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
-                           0, s, L, cp[c], n, lv, uv, d, v, t);
-    }
-    for (int c = L.ncolors - 1; c >= 0; c--) {
-      int n = cp[c + 1] - cp[c];
-      if (n > 0)
-        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, 0, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
-                           0, s, L, cp[c], n, lv, uv, d, v, t);
-    }
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, decltype(kind)::value, LPRc, Bc>),
+                           rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], n, lv, uv, d, v, t);
+    };
+    for (int c = 0; c < nc - 1; c++) go(std::integral_constant<int, 1>(), c);
+    go(std::integral_constant<int, 2>(), nc - 1);  // last colour: forward + backward
+    for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, 0>(), c);
   }));
   return hipGetLastError();
 }
@@ -847,19 +871,19 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
                              const double *uv, const double *d, double *v, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
+  const int nc = L.ncolors;
   PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
-    for (int c = 0; c < L.ncolors; c++) {
-      int n = cp[c + 1] - cp[c];
+    auto go = [&](auto kind, int c) {
+      const int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 1, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
-                           0, s, L, cp[c], cp[c + 1], lv, uv, d, v);
-    }
-    for (int c = L.ncolors - 1; c >= 0; c--) {
-      int n = cp[c + 1] - cp[c];
-      if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, 0, LPRc, Bc>), rows_grid(n * LPRc), dim3(kBlock),
-                           0, s, L, cp[c], cp[c + 1], lv, uv, d, v);
-    }
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc>),
+                           rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
+                           d, v);
+    };
+    // the last colour's backward step runs in its forward launch (kIluLast)
+    for (int c = 0; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
+    go(std::integral_constant<int, kIluLast>(), nc - 1);
+    for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
   }));
   return hipGetLastError();
 }

@@ -4,8 +4,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <numeric>
 #include <sstream>
 #include <unordered_map>
@@ -546,6 +548,75 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
     while ((usedc >> c) & 1) c++;
     color[v] = c;
     ncolors = std::max(ncolors, c + 1);
+  }
+  // Tail repair: greedy leaves a few thin top colours (config 3: 17 K and 51 of 738 K rows), each
+  // a latency-bound launch per sweep.  A top-colour vertex v takes a lower colour c when the
+  // neighbours of colour c can all move to other colours below the top, recursively (bounded
+  // Kempe-style chains, undone on failure); a top colour that empties is dropped.  Only thin top
+  // colours (<= 1/16 of the rows) are attacked.  PNP_RECOLOR=0 turns the repair off.
+  const char *rc_env = std::getenv("PNP_RECOLOR");
+  const bool recolor = !(rc_env && rc_env[0] == '0');
+  std::vector<std::pair<int, int>> undo;  // (vertex, previous colour)
+  auto setc = [&](int v, int c) {
+    undo.emplace_back(v, color[v]);
+    color[v] = c;
+  };
+  auto rollback = [&](size_t mark) {
+    while (undo.size() > mark) {
+      color[undo.back().first] = undo.back().second;
+      undo.pop_back();
+    }
+  };
+  auto owned_nbr = [&](int u) { return part[u] == rank && color[u] >= 0; };
+  // resolve every conflict of w (neighbours sharing its colour) by moving them below `top`
+  std::function<bool(int, int, int)> fix = [&](int w, int top, int depth) -> bool {
+    for (int k = f.ptr[w]; k < f.ptr[w + 1]; k++) {
+      const int x = f.nbr[k];
+      if (!owned_nbr(x) || color[x] != color[w]) continue;
+      bool done = false;
+      for (int pass = 0; pass < 2 && !done; pass++) {  // pass 0: conflict-free colours only
+        if (pass == 1 && depth == 0) break;
+        for (int c2 = 0; c2 < top && !done; c2++) {
+          if (c2 == color[x]) continue;
+          bool clash = false;
+          for (int kk = f.ptr[x]; kk < f.ptr[x + 1] && !clash; kk++)
+            clash = owned_nbr(f.nbr[kk]) && color[f.nbr[kk]] == c2;
+          if (clash != (pass == 1)) continue;
+          const size_t mark = undo.size();
+          setc(x, c2);
+          if (fix(x, top, depth - 1)) {
+            done = true;
+          } else {
+            rollback(mark);
+          }
+        }
+      }
+      if (!done) return false;
+    }
+    return true;
+  };
+  while (recolor && ncolors > 1) {
+    const int top = ncolors - 1;
+    int left = 0, ntop = 0;
+    for (int v : owned) ntop += color[v] == top;
+    if (ntop * 16 > int(owned.size())) break;
+    for (int v : owned) {
+      if (color[v] != top) continue;
+      bool moved = false;
+      for (int c = 0; c < top && !moved; c++) {
+        const size_t mark = undo.size();
+        setc(v, c);
+        if (fix(v, top, 2)) {
+          moved = true;
+        } else {
+          rollback(mark);
+        }
+      }
+      undo.clear();
+      if (!moved) left++;
+    }
+    if (left > 0) break;
+    ncolors--;
   }
   // colour-major order (rows of one colour contiguous, Morton order inside a colour), in
   // windows of kOrderBlock rows sorted by slot count (longest first) so that SELL chunks carry
