@@ -667,6 +667,38 @@ extern "C" int pnp_mesh_refine(const pnp_mesh *in, int32_t k, pnp_mesh_buf **out
   return PNP_OK;
 }
 
+extern "C" int pnp_mesh_from_geo(const char *path, double size_scale, pnp_mesh_buf **out) {
+  if (!path || !out || !(size_scale > 0)) return PNP_E_ARG;
+  pnp::GeoModel g;
+  std::string err;
+  if (!pnp::read_geo(path, g, err)) {
+    g_err = err;
+    return err.rfind("cannot open", 0) == 0 ? PNP_E_IO : PNP_E_MESH;
+  }
+  auto mb = std::make_unique<pnp_mesh_buf>();
+  if (!pnp::mesh_geo(g, size_scale, mb->m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  *out = mb.release();
+  return PNP_OK;
+}
+
+extern "C" int pnp_mesh_write_gmsh(const pnp_mesh *in, const char *path) {
+  if (!path) return PNP_E_ARG;
+  pnp::Mesh m;
+  std::string err;
+  if (!mesh_from_view(in, m, err)) {
+    g_err = err;
+    return PNP_E_MESH;
+  }
+  if (!pnp::write_gmsh(path, m, err)) {
+    g_err = err;
+    return PNP_E_IO;
+  }
+  return PNP_OK;
+}
+
 extern "C" int pnp_mesh_view(const pnp_mesh_buf *mb, pnp_mesh *view) {
   if (!mb || !view) return PNP_E_ARG;
   view->nv = mb->m.nv;

@@ -556,6 +556,8 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
   // colours (<= 1/16 of the rows) are attacked.  PNP_RECOLOR=0 turns the repair off.
   const char *rc_env = std::getenv("PNP_RECOLOR");
   const bool recolor = !(rc_env && rc_env[0] == '0');
+  const char *rd_env = std::getenv("PNP_RECOLOR_DEPTH");
+  const int recolor_depth = rd_env ? std::atoi(rd_env) : 2;
   std::vector<std::pair<int, int>> undo;  // (vertex, previous colour)
   auto setc = [&](int v, int c) {
     undo.emplace_back(v, color[v]);
@@ -606,7 +608,7 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
       for (int c = 0; c < top && !moved; c++) {
         const size_t mark = undo.size();
         setc(v, c);
-        if (fix(v, top, 2)) {
+        if (fix(v, top, recolor_depth)) {
           moved = true;
         } else {
           rollback(mark);

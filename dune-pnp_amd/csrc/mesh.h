@@ -9,7 +9,9 @@
 //   RCB partition, colouring, Morton order and the SELL-64 block layout of the local problem.
 #pragma once
 
+#include <array>
 #include <cstdint>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -24,8 +26,25 @@ struct Mesh {
 };
 
 bool read_gmsh(const std::string &path, Mesh &m, std::string &err);
+bool write_gmsh(const std::string &path, const Mesh &m, std::string &err);
 Mesh refine(const Mesh &m, int k);
 bool validate(const Mesh &m, std::string &err);
+
+// .geo subset and the native mesher standing in for gmsh (geo_mesh.cc)
+struct GeoModel {
+  std::map<int, std::array<double, 3>> pts;  // id -> x, y, lc (0: none given)
+  struct Curve {
+    bool circle = false;
+    int a = -1, b = -1, c = -1;  // start, end, centre (circle)
+  };
+  std::map<int, Curve> curves;
+  std::map<int, std::vector<int>> loops;     // signed curve ids
+  std::map<int, std::vector<int>> surfaces;  // loop ids, outer first
+  std::map<int, int> curve_group;            // Physical Line
+};
+bool read_geo(const std::string &path, GeoModel &g, std::string &err);
+// size_scale multiplies every characteristic length (gmsh -clscale)
+bool mesh_geo(const GeoModel &g, double size_scale, Mesh &m, std::string &err);
 
 // Vertex fan: for vertex v, neighbours nbr[ptr[v] .. ptr[v+1]) in CCW order around v.
 // meta bits: [0,6) L = 1 + #neighbours (slots incl. diagonal), bit 6 closed (an element joins

@@ -36,7 +36,7 @@ static int prec_of(const std::string &s) {
 
 static void usage() {
   std::printf(
-      "usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb]\n"
+      "usage: pnp_main <config.cfg> [--refine k] [--mesh-scale s] [--mode stationary|instationary|md|pb]\n"
       "                [--steps n] [--prec none|ssor|jacobi|ilu0] [--pb-prec p] [--device d]\n"
       "                [--out prefix] [--md-reduction r]\n"
       "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi]\n");
@@ -163,6 +163,7 @@ int main(int argc, char **argv) {
   }
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
   int refine = 0, steps = -1, device = -1;
+  double mesh_scale = 1.0;  // size scale when the mesh comes from a .geo (gmsh -clscale)
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
   // md mode: PbLS, the compile-time LINEARSOLVER of src/instationary_pnp_from_pb_md.hh:20-32,188-211
   std::string linsolver = "bcgs_ssork";
@@ -173,6 +174,7 @@ int main(int argc, char **argv) {
       return argv[++i];
     };
     if (a == "--refine") refine = std::atoi(next().c_str());
+    else if (a == "--mesh-scale") mesh_scale = std::atof(next().c_str());
     else if (a == "--mode") mode = next();
     else if (a == "--steps") steps = std::atoi(next().c_str());
     else if (a == "--prec") prec = next();
@@ -191,7 +193,7 @@ int main(int argc, char **argv) {
     int world = std::getenv("WORLD_SIZE") ? std::atoi(std::getenv("WORLD_SIZE")) : 1;
     if (device < 0) device = std::getenv("LOCAL_RANK") ? std::atoi(std::getenv("LOCAL_RANK")) : 0;
     pnp_gpu::Sysparams s(cfgfile);
-    pnp_gpu::Mesh mesh(s.cfg.meshfile, refine);
+    pnp_gpu::Mesh mesh(s.cfg.meshfile, refine, mesh_scale);
     pnp_params params = s.params();
     std::vector<char> uid(128, 0);
     pnp_comm comm{rank, world, nullptr, nullptr};

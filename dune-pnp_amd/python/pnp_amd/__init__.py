@@ -213,6 +213,29 @@ class Mesh:
         _check(lib().pnp_mesh_read_gmsh(path.encode(), C.byref(buf)))
         return Mesh._from_buf(buf)
 
+    @staticmethod
+    def from_geo(path, size_scale=1.0):
+        """gmsh's preprocessing of a .geo geometry, natively (pnp_mesh_from_geo)."""
+        buf = C.c_void_p()
+        _check(lib().pnp_mesh_from_geo(path.encode(), C.c_double(size_scale), C.byref(buf)))
+        return Mesh._from_buf(buf)
+
+    @staticmethod
+    def load(meshfile, size_scale=1.0):
+        """The mesh a config names: the .msh if it exists, else the .geo of the same name meshed
+        here (the reference's workflow runs gmsh on the .geo first, e.g.
+        test/pore_without_dna/pore.cfg:21 names a .msh that only exists as a .geo)."""
+        if os.path.exists(meshfile):
+            return Mesh.read_gmsh(meshfile)
+        geo = os.path.splitext(meshfile)[0] + ".geo"
+        if os.path.exists(geo):
+            return Mesh.from_geo(geo, size_scale)
+        return Mesh.read_gmsh(meshfile)  # raises the reader's error
+
+    def write_gmsh(self, path):
+        m = self.c()
+        _check(lib().pnp_mesh_write_gmsh(C.byref(m), path.encode()))
+
     def refine(self, k):
         if k == 0:
             return self

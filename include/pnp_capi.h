@@ -74,6 +74,16 @@ typedef struct pnp_mesh_buf pnp_mesh_buf; /* library-owned mesh */
 int pnp_mesh_read_gmsh(const char *path, pnp_mesh_buf **out);
 /* k levels of uniform red refinement (midpoints; boundary segments split, groups kept) */
 int pnp_mesh_refine(const pnp_mesh *in, int32_t k, pnp_mesh_buf **out);
+/* gmsh's preprocessing step for a .geo geometry (the reference runs gmsh on
+ * test/pore_without_dna/pore_without_dna.geo to get the .msh its pore.cfg:21 names): the .geo
+ * subset of the reference's geometries (variables, Point, Line, Circle, Line/Curve Loop, Plane
+ * Surface, Physical Line) meshed natively; size_scale multiplies every characteristic length
+ * (gmsh -clscale).  Deterministic. */
+int pnp_mesh_from_geo(const char *path, double size_scale, pnp_mesh_buf **out);
+/* write ASCII gmsh 2.2 (boundary segments with their physical group, then triangles);
+ * pnp_mesh_read_gmsh of the file gives the same mesh back when the vertices are numbered in
+ * order of first use by a triangle (as every mesh this library makes is) */
+int pnp_mesh_write_gmsh(const pnp_mesh *m, const char *path);
 /* view into a library-owned mesh (valid until pnp_mesh_free) */
 int pnp_mesh_view(const pnp_mesh_buf *m, pnp_mesh *view);
 void pnp_mesh_free(pnp_mesh_buf *m);

@@ -24,6 +24,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <fstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -53,9 +54,15 @@ inline size_t size(const std::vector<double> &v) { return v.size(); }
 // ---- mesh / config (GmshReader, Sysparams) ---------------------------------------------------
 class Mesh {
  public:
-  explicit Mesh(const std::string &gmsh_file, int refine = 0) {
+  // the .msh a config names; when it does not exist but the .geo of the same name does, the
+  // geometry is meshed here (the reference's workflow runs gmsh on the .geo first)
+  explicit Mesh(const std::string &gmsh_file, int refine = 0, double size_scale = 1.0) {
     pnp_mesh_buf *b = nullptr;
-    check(pnp_mesh_read_gmsh(gmsh_file.c_str(), &b));
+    const std::string geo = gmsh_file.substr(0, gmsh_file.rfind('.')) + ".geo";
+    if (!std::ifstream(gmsh_file) && std::ifstream(geo))
+      check(pnp_mesh_from_geo(geo.c_str(), size_scale, &b));
+    else
+      check(pnp_mesh_read_gmsh(gmsh_file.c_str(), &b));
     if (refine > 0) {
       pnp_mesh v;
       pnp_mesh_view(b, &v);

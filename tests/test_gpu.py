@@ -382,6 +382,32 @@ def test_pb_then_pnp_on_refined_pore_converges_with_ilu0():
     assert r1 <= 1e-8 * r0 * 1.01
 
 
+@pytest.mark.parametrize("prec", ["SSOR", "ILU0"])
+def test_pb_then_pnp_on_the_meshed_pore_without_dna(prec):
+    """Config 5's geometry: test/pore_without_dna's .geo meshed natively (tests/test_mesher.py),
+    refined once, PB Newton then PNP Newton (the reference's stationary driver sequence).  The
+    converged state is checked with the oracle's residual."""
+    cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
+    mesh = P.Mesh.load(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+    ctx = P.Context(mesh, par)
+    pr = getattr(P, "PREC_" + prec)
+    ctx.set_operator(P.OP_PB)
+    phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=pr)
+    assert rpb["converged"] == 1, rpb
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(x0, prec=pr, reduction=1e-8)
+    assert res["converged"] == 1 and res["status"] == 0, res
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    r0 = np.linalg.norm(orc.residual(op, x0))
+    r1 = np.linalg.norm(orc.residual(op, u))
+    assert r1 <= 1e-8 * r0 * 1.01
+
+
 def test_operator_switch_leaves_no_stale_matrix_entries():
     """PB Newton then PNP in one context (the driver sequence): the PNP solve must behave exactly
     as in a fresh context (SELL padding slots hold zeros for the new block layout)."""

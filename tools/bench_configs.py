@@ -5,8 +5,10 @@ driver-level solve it stands for.  Prints one JSON object per config.
   config 2: PNP on test/cylinder refined k=6 (3.3M DOF), PB -> BCExtension -> PNP Newton
   config 4: instationary PNP (PnpOperator + PnpTOperator, implicit Euler, dt = tau) on
             test/pore_pnp refined k=3 (556k DOF), 100 steps
-  config 5 (fallback): PNP on test/pore_pnp refined k=5 (8.8M DOF), assembly + BiCGSTAB rates
-usage: python tools/bench_configs.py [1 2 4 5]"""
+  config 5: PNP on test/pore_without_dna (the .geo meshed natively, size scale 0.85, refined
+            k=6: ~10M DOF), PB -> PNP Newton, assembly + BiCGSTAB rates
+  config 5f: the earlier fallback, test/pore_pnp refined k=5 (8.8M DOF)
+usage: python tools/bench_configs.py [1 2 4 5 5f]"""
 import json
 import os
 import sys
@@ -107,6 +109,33 @@ def config4(nsteps=100):
 
 
 def config5():
+    """test/pore_without_dna: the .geo meshed here (size scale 0.85), refined k=6 -> ~10 M DOF."""
+    cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
+    t0 = time.perf_counter()
+    base = P.Mesh.load(cfg.meshfile, size_scale=0.85)
+    tmesh = time.perf_counter() - t0
+    mesh = base.refine(6)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    phi, pbres, tpb = pb_then(ctx, mesh, prec=P.PREC_ILU0)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(x0)
+    r = rates(ctx)
+    n = 3 * mesh.nv
+    t0 = time.perf_counter()
+    u, res = ctx.newton(x0, prec=P.PREC_ILU0, reduction=cfg.system["newtonReduction"],
+                        min_linear_reduction=cfg.system["newtonMinLinearReduction"])
+    t_pnp = time.perf_counter() - t0
+    return {"config": "5 (pore_without_dna.geo meshed natively, scale 0.85, k=6, one GPU)",
+            "base_vertices": base.nv, "mesher_s": tmesh, "dofs": n, "pb_newton_s": tpb,
+            "pb_converged": pbres["converged"], "pnp_newton_s": t_pnp,
+            "pnp_newton_iterations": res["iterations"],
+            "pnp_linear_iterations": res["linear_iterations"], "pnp_converged": res["converged"],
+            "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6),
+            "bicgstab_iters_per_s": 1e3 / r["bicgstab_ms_per_iter"], **r}
+
+
+def config5_fallback():
     cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
     mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(5)
     ctx = P.Context(mesh, P.Params.from_config(cfg))
@@ -116,7 +145,7 @@ def config5():
     ctx.state_set(x0)
     r = rates(ctx)
     n = 3 * mesh.nv
-    return {"config": "5 (fallback: pore_pnp k=5, one GPU)", "dofs": n, "pb_newton_s": tpb,
+    return {"config": "5f (pore_pnp k=5, one GPU)", "dofs": n, "pb_newton_s": tpb,
             "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6),
             "bicgstab_iters_per_s": 1e3 / r["bicgstab_ms_per_iter"], **r}
 
@@ -124,5 +153,5 @@ def config5():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["1", "2", "4", "5"]
     for w in which:
-        out = {"1": config1, "2": config2, "4": config4, "5": config5}[w]()
+        out = {"1": config1, "2": config2, "4": config4, "5": config5, "5f": config5_fallback}[w]()
         print(json.dumps(out), flush=True)
