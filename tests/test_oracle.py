@@ -289,3 +289,34 @@ def test_cg_oracle_solves_pb_system_and_counts_matvecs():
             p = q + rho_new / rho * p
             rho = rho_new
         assert res.iterations == it
+
+
+def test_multicolour_ssor_diverges_where_natural_order_converges():
+    """Why the GPU test on config 5's geometry uses ILU(0): on the first PNP Newton system of
+    test/pore_without_dna (meshed natively, refined once) ISTL SSOR(k=1, w=1) in the file's
+    vertex order converges, but the same SSOR in the multicolour vertex-blocked order the GPU
+    sweeps use (pnp_layout: colour-major, fields inside a vertex) diverges -- Gauss-Seidel on a
+    drift-dominated non-symmetric system depends on the order.  ILU(0) in that order converges
+    with ~25 % more iterations than in the natural order.  All on the oracle (CPU)."""
+    import pnp_amd as P
+    cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
+    mesh = P.Mesh.load(cfg.meshfile).refine(1)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    x0 = orc.initial_state(np.zeros(mesh.nv))
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    r = orc.residual(op, x0)
+    J = orc.jacobian(op, x0).tocsr()
+    lay = P.Layout(mesh)
+    nv = mesh.nv
+    perm = np.array([f * nv + lay.l2g[q] for q in range(nv) for f in range(3)])
+    Jp = J[perm][:, perm]
+    _, nat = O.bicgstab(J, r, prec=O.PREC_SSOR, reduction=1e-8)
+    _, mc = O.bicgstab(Jp, r[perm], prec=O.PREC_SSOR, reduction=1e-8, maxit=2000)
+    _, ilu_nat = O.bicgstab(J, r, prec=O.PREC_ILU0, reduction=1e-8)
+    _, ilu_mc = O.bicgstab(Jp, r[perm], prec=O.PREC_ILU0, reduction=1e-8)
+    assert nat.converged == 1
+    assert mc.converged == 0 and mc.reduction > 1.0
+    assert ilu_nat.converged == 1 and ilu_mc.converged == 1
+    assert ilu_mc.iterations < 1.5 * ilu_nat.iterations
