@@ -277,7 +277,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   int cj[NC];
   if constexpr (FANR > 0) {
 #pragma unroll
-    for (int k = 1; k < FANR; k++) cj[k] = k < len ? cix[k * kRows] : row;
+    // branch-free: past the fan, slot 0 (the diagonal, column = row) is read instead, so all
+    // index loads issue back to back (guarded loads were serialised by the register allocator)
+    for (int k = 1; k < FANR; k++) cj[k] = cix[(k < len ? k : 0) * kRows];
   }
   // column of slot k (FANR path: k is the wave-uniform s + c, or 1 after a wrap)
   auto col = [&](int k) -> int {

@@ -19,6 +19,8 @@ for step in "$@"; do
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-solve --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
     pmcf)   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcf.log" 2>&1; rc=$? ;;
     pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
+    pmcsq)  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_sq" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcsq.log" 2>&1; rc=$? ;;
+    pmcsq2) timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INSTS_VALU --kernel-trace --output-format csv -d "$OUT/pmc_sq2" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcsq2.log" 2>&1; rc=$? ;;
     ab)     : > "$OUT/ab.log"; rc=0
             for i in 1 2 3; do
               timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
