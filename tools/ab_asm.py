@@ -30,7 +30,15 @@ for rep in range(10):
 ctx.timers(enable=True, reset=True)
 ctx.bicgstab_iterations(20, P.PREC_SSOR)
 t = ctx.timers(enable=False)
+ctx.bicgstab_iterations(2, P.PREC_ILU0)  # factorise
+ilu = []
+for rep in range(5):
+    ctx.timers(enable=True, reset=True)
+    ctx.bicgstab_iterations(10, P.PREC_ILU0)
+    ti = ctx.timers(enable=False)
+    ilu.append(ti['prec_ms'] / ti['prec_launches'] * 1e3)
 print(f"waves={os.environ.get('PNP_ASM_WAVES', '3')} fanr={os.environ.get('PNP_ASM_FANR', '1')} assemble_us median={np.median(res):.2f} "
       f"min={np.min(res):.2f}  spmv_us={t['spmv_ms'] / t['spmv_launches'] * 1e3:.2f} "
       f"sgs_apply_us={t['prec_ms'] / t['prec_launches'] * 1e3:.2f} "
+      f"ilu_apply_us={np.median(ilu):.2f} "
       f"blas_ms_per_it={t['blas_ms'] / 20:.4f}")
