@@ -263,10 +263,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   // fan wraps); consecutive elements share v_{s+1}, so each neighbour's data (coordinates, NF
   // dofs, frozen fields) is gathered once, one element ahead, and its column index two ahead.
   auto next_slot = [&](int s) { return (s + 1 < len) ? s + 1 : (closed ? 1 : -1); };
-  auto load_nb = [&](int j, double2 &p, double *u, double &a0, double &a1) {
+  auto load_nb = [&](int j, double2 &p, double (&u)[NF], double &a0, double &a1) {
     p = reinterpret_cast<const double2 *>(L.xy)[j];
-#pragma unroll
-    for (int f = 0; f < NF; f++) u[f] = a.x[size_t(j) * NF + f];
+    load_nf<NF>(a.x, size_t(j), u);
     if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) a0 = a.aux0[j];
     if constexpr (OP == OP_POISSON) a1 = a.aux1[j];
   };

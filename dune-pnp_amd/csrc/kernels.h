@@ -29,6 +29,38 @@ __device__ __forceinline__ int xcd_block(int b, int nwg, int on = 1) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
+// ---- per-vertex records of NF doubles -------------------------------------------------------
+// NF consecutive doubles at x + NF*j in the fewest memory instructions: 16-B loads/stores of
+// 8-B-aligned pairs (gfx950 global accesses need 4-B alignment only) plus the odd last value.
+// A gather of a 3-field record is 2 instructions instead of 3 (the sweeps and the SpMV are
+// VMEM-issue and L1-bound: TA busy ~70 %, TCP pending-stall ~55 % of cycles).
+typedef double double2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+template <int NF>
+__device__ __forceinline__ void load_nf(const double *__restrict__ x, size_t j, double (&o)[NF]) {
+  const double *b = x + size_t(NF) * j;
+  int f = 0;
+#pragma unroll
+  for (; f + 1 < NF; f += 2) {
+    const double2_a8 a = *reinterpret_cast<const double2_a8 *>(b + f);
+    o[f] = a.x;
+    o[f + 1] = a.y;
+  }
+  if (f < NF) o[f] = b[f];
+}
+template <int NF>
+__device__ __forceinline__ void store_nf(double *__restrict__ x, size_t j, const double (&v)[NF]) {
+  double *b = x + size_t(NF) * j;
+  int f = 0;
+#pragma unroll
+  for (; f + 1 < NF; f += 2) {
+    double2_a8 a;
+    a.x = v[f];
+    a.y = v[f + 1];
+    *reinterpret_cast<double2_a8 *>(b + f) = a;
+  }
+  if (f < NF) b[f] = v[f];
+}
+
 // ---- SELL value layout --------------------------------------------------------------------------
 // Slot s of chunk c holds NV values for each of the chunk's 64 rows, at doubles
 // [(chunk_off[c] + 64 s) * NV, +64 NV).  Inside a slot, value pairs (q, q+1) (q even, q+1 < NV)

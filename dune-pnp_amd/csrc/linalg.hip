@@ -82,8 +82,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
       double xj[SB][NF], k[SB][NK];
 #pragma unroll
       for (int b = 0; b < SB; b++) {
-#pragma unroll
-        for (int g = 0; g < NF; g++) xj[b][g] = x[size_t(j[b]) * NF + g];
+        load_nf<NF>(x, size_t(j[b]), xj[b]);
         if (s0 + b < len) {
           load_vals<NK>(vc + size_t(s0 + b) * NK * kRows, lane, k[b]);
         } else {
@@ -202,8 +201,11 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
     for (int b = 0; b < B; b++) {
       const int s = sb + b * LPR;
       const bool use = j[b] != row;  // padding: zero values, v[row] may be stale
+      load_nf<NF>(v, size_t(use ? j[b] : row), vj[b]);
+      if (!use) {
 #pragma unroll
-      for (int g = 0; g < NF; g++) vj[b][g] = use ? v[size_t(j[b]) * NF + g] : 0.0;
+        for (int g = 0; g < NF; g++) vj[b][g] = 0.0;
+      }
       if (use) {
         load_vals<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
       } else {

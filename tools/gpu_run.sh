@@ -21,6 +21,12 @@ for step in "$@"; do
     pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
     pmcsq)  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_sq" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcsq.log" 2>&1; rc=$? ;;
     pmcsq2) timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INSTS_VALU --kernel-trace --output-format csv -d "$OUT/pmc_sq2" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcsq2.log" 2>&1; rc=$? ;;
+    pmcmem) rc=0
+            for set in "TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES" "TCP_PENDING_STALL_CYCLES TCP_READ_TAGCONFLICT_STALL_CYCLES" "TCC_HIT TCC_MISS" "TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM"; do
+              tag=$(echo $set | cut -d' ' -f1)
+              timeout -k 10 600 rocprofv3 --pmc $set GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_$tag" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcmem.log" 2>&1; rc=$?
+              fatal $rc && break
+            done ;;
     ab)     : > "$OUT/ab.log"; rc=0
             for i in 1 2 3; do
               timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
