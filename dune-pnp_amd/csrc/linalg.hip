@@ -104,14 +104,19 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
       }
     }
     const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
+    if (dm) {
+      double xr[NF];
+      load_nf<NF>(x, size_t(row), xr);
 #pragma unroll
-    for (int f = 0; f < NF; f++) {
-      if ((dm >> f) & 1) acc[f] = x[size_t(row) * NF + f];
-      y[size_t(row) * NF + f] = acc[f];
+      for (int f = 0; f < NF; f++)
+        if ((dm >> f) & 1) acc[f] = xr[f];
     }
+    store_nf<NF>(y, size_t(row), acc);
     if constexpr (MODE >= 1) {
+      double wr[NF];
+      load_nf<NF>(w, size_t(row), wr);
 #pragma unroll
-      for (int f = 0; f < NF; f++) d[0] += acc[f] * w[size_t(row) * NF + f];
+      for (int f = 0; f < NF; f++) d[0] += acc[f] * wr[f];
     }
     if constexpr (MODE == 2) {
 #pragma unroll
@@ -254,16 +259,18 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
   double rhs[NF], vi[NF], Dg[NV];
+  load_nf<NF>(FWD ? d : t, size_t(row), rhs);
+  if (FWD) {
 #pragma unroll
-  for (int f = 0; f < NF; f++) {
-    if (FWD) {
-      rhs[f] = d[size_t(row) * NF + f] + acc[f];
-      if (KIND == 1) t[size_t(row) * NF + f] = rhs[f];
+    for (int f = 0; f < NF; f++) {
+      rhs[f] += acc[f];
       vi[f] = 0.0;
-    } else {
-      rhs[f] = t[size_t(row) * NF + f] + acc[f];
-      vi[f] = v[size_t(row) * NF + f];
     }
+    if (KIND == 1) store_nf<NF>(t, size_t(row), rhs);
+  } else {
+    load_nf<NF>(v, size_t(row), vi);
+#pragma unroll
+    for (int f = 0; f < NF; f++) rhs[f] += acc[f];
   }
   load_vals<NV>(R.dg, R.lane, Dg);
 #pragma unroll
@@ -280,8 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
       }
       vi[f] += r / Dg[pat_index(PAT, f, f)];
     }
-#pragma unroll
-  for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = vi[f];
+  store_nf<NF>(v, size_t(row), vi);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -421,14 +427,17 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
+  {
+    double own[NF];
+    load_nf<NF>(FWD ? d : v, size_t(row), own);
 #pragma unroll
-  for (int f = 0; f < NF; f++) acc[f] += FWD ? d[size_t(row) * NF + f] : v[size_t(row) * NF + f];
+    for (int f = 0; f < NF; f++) acc[f] += own[f];
+  }
   double Dg[NV];
   load_vals<NV>(R.dg, R.lane, Dg);
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
   if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
-#pragma unroll
-  for (int f = 0; f < NF; f++) v[size_t(row) * NF + f] = acc[f];
+  store_nf<NF>(v, size_t(row), acc);
 }
 
 // split storage position p takes the block (row, slot) = (src >> 6, src & 63) of the full SELL:
