@@ -255,11 +255,15 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   const bool live = k < nk;
   const int row = k0 + (live ? k : 0);  // colour-major order: the colour's rows are [k0, k0+nk)
   const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
+  // the row's own data and diagonal block do not depend on the neighbours: issued before the
+  // neighbour loop so that they share its memory round trips (after the loop they cost one more)
+  double rhs[NF], vi[NF], Dg[NV];
+  load_nf<NF>(FWD ? d : t, size_t(row), rhs);
+  if (!FWD) load_nf<NF>(v, size_t(row), vi);
+  load_vals<NV>(R.dg, R.lane, Dg);
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
-  double rhs[NF], vi[NF], Dg[NV];
-  load_nf<NF>(FWD ? d : t, size_t(row), rhs);
   if (FWD) {
 #pragma unroll
     for (int f = 0; f < NF; f++) {
@@ -268,11 +272,9 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
     }
     if (KIND == 1) store_nf<NF>(t, size_t(row), rhs);
   } else {
-    load_nf<NF>(v, size_t(row), vi);
 #pragma unroll
     for (int f = 0; f < NF; f++) rhs[f] += acc[f];
   }
-  load_vals<NV>(R.dg, R.lane, Dg);
 #pragma unroll
   for (int pass = 0; pass < (KIND == 2 ? 2 : 1); pass++)
 #pragma unroll
@@ -424,17 +426,15 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   const bool live = r0 + k < r1;
   const int row = live ? r0 + k : r0;
   const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
+  // own data and diagonal block first: they share the neighbour loop's round trips
+  double own[NF], Dg[NV];
+  load_nf<NF>(FWD ? d : v, size_t(row), own);
+  load_vals<NV>(R.dg, R.lane, Dg);
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
-  {
-    double own[NF];
-    load_nf<NF>(FWD ? d : v, size_t(row), own);
 #pragma unroll
-    for (int f = 0; f < NF; f++) acc[f] += own[f];
-  }
-  double Dg[NV];
-  load_vals<NV>(R.dg, R.lane, Dg);
+  for (int f = 0; f < NF; f++) acc[f] += own[f];
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
   if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
   store_nf<NF>(v, size_t(row), acc);
