@@ -127,7 +127,7 @@ struct pnp_ctx {
   bool assembled = false;
 
   // vectors (sized n_local * 3)
-  DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials;
+  DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials, partials2;
   DBuf<pnp::Scalars> S;
   pnp::Scalars *hS = nullptr;  // pinned host mirror
 
@@ -306,6 +306,21 @@ struct pnp_ctx {
     return e == hipSuccess ? PNP_OK : hipfail(e, "derive");
   }
 
+  // S->red[0..ka) = sum of partials (spmv), S->red[ka..) = sum of partials2, all ranks; derive
+  int reduce_derive2(int npa, int ka, int npb, int kb, int stage) {
+    hipError_t e;
+    if (nranks == 1) {
+      e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream, stage);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
+    }
+    e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream);
+    if (e != hipSuccess) return hipfail(e, "reduce");
+    int rc = allreduce_red(ka + kb);
+    if (rc) return rc;
+    e = pnp::launch_derive(S.p, stage, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "derive");
+  }
+
   // norm over owned rows of a vector, synchronous
   int norm(const double *vec, double &out) {
     hipEvent_t t0 = tb(T_BLAS);
@@ -477,11 +492,12 @@ struct pnp_ctx {
       if (e != hipSuccess) return hipfail(e, "spmv h");
       te(T_SPMV, t0);
       if ((rc = reduce_derive(nsp, 1, 1))) return rc;
-      // x += alpha y ; r -= alpha v ; ||r||
+      // x += alpha y ; r -= alpha v ; ||r|| (partials2: its half-step test is derived together
+      // with omega below -- one reduction and one allreduce fewer per iteration; the second
+      // half's kernels ignore a converged first half, update_xr skips on S->done)
       t0 = tb(T_BLAS);
-      e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials.p, stream);
+      e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials2.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (1)");
-      if ((rc = reduce_derive(np, 1, 2))) return rc;
       te(T_BLAS, t0);
       // y = M^{-1} r ; t = A y ; <t,r>, <t,t>
       const double *yin2 = rs.p;
@@ -494,7 +510,7 @@ struct pnp_ctx {
       e = pnp::launch_spmv(dl, nf, pat, vals.p, yin2, t.p, 2, rs.p, partials.p, &nsp, stream);
       if (e != hipSuccess) return hipfail(e, "spmv t");
       te(T_SPMV, t0);
-      if ((rc = reduce_derive(nsp, 2, 3))) return rc;
+      if ((rc = reduce_derive2(nsp, 2, np, 1, 23))) return rc;
       // x += omega y ; r -= omega t ; ||r||, <rt, r>
       t0 = tb(T_BLAS);
       e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
@@ -1000,7 +1016,9 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = al(c->partials,
                2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
                                     size_t((L.n_owned + 255) / 256)) + 64,
-               "partials")) || (rc = al(c->S, 2, "scalars")) ||
+               "partials")) ||
+      (rc = al(c->partials2, size_t(pnp::blas_nparts(3LL * nloc)) + 64, "partials2")) ||
+      (rc = al(c->S, 2, "scalars")) ||
       (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
       (rc = al(c->cvec, 3 * size_t(L.n_owned), "cvec")) || (rc = al(c->aux0, nloc, "aux0")) ||
       (rc = al(c->aux1, nloc, "aux1"))) {

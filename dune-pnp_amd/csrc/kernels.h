@@ -286,8 +286,12 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
 // the derive step in the same launch (single GPU: no allreduce in between)
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
                          int derive_stage = -1);
+// sum partials pa[npa][ka] -> S->red[0..ka) and pb[npb][kb] -> S->red[ka..ka+kb), ka+kb <= 4
+hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
+                          Scalars *S, hipStream_t s, int derive_stage = -1);
 // derive scalars after a reduction; stage: 0 init (red: <r,r>), 1 after h, 2 after first half
-// norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>)
+// norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>); 23 = 2 then 3 from one
+// reduction (red: <t,r>, <t,t>, ||s||^2), the first half step's test deferred to the second's
 hipError_t launch_derive(Scalars *S, int stage, hipStream_t s);
 
 // y = x - lambda*z (Newton line search), copy/scale helpers

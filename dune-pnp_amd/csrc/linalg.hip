@@ -589,6 +589,23 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const double *__restrict__ pa
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_reduce2(const double *__restrict__ pa, int npa, int ka,
+                                                    const double *__restrict__ pb, int npb, int kb,
+                                                    Scalars *__restrict__ S, int stage) {
+  if (S->done) return;
+  double acc[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < npa; i += kBlock)
+    for (int j = 0; j < ka; j++) acc[j] += pa[size_t(i) * ka + j];
+  for (int i = threadIdx.x; i < npb; i += kBlock)
+    for (int j = 0; j < kb; j++) acc[ka + j] += pb[size_t(i) * kb + j];
+  double out[4];
+  block_sum<4>(acc, out);
+  if (threadIdx.x == 0) {
+    for (int j = 0; j < ka + kb; j++) S->red[j] = out[j];
+    if (stage >= 0) derive(S, stage);
+  }
+}
+
 __global__ void k_derive(Scalars *S, int stage) {
   if (threadIdx.x == 0) derive(S, stage);
 }
@@ -647,6 +664,14 @@ __device__ void derive(Scalars *S, int stage) {
     S->it_half += 0.5;
     if (S->norm < S->reduction * S->norm0) S->done = 1;
   } else if (stage == 3) {  // omega = <t,r>/<t,t>
+    S->omega = S->red[0] / S->red[1];
+  } else if (stage == 23) {  // the first half step's test (red[2] = ||s||^2), then omega
+    S->norm = sqrt(S->red[2]);
+    S->it_half += 0.5;
+    if (S->norm < S->reduction * S->norm0) {
+      S->done = 1;
+      return;
+    }
     S->omega = S->red[0] / S->red[1];
   } else if (stage == 4) {  // second half step: red = <r,r>, <rt,r>
     S->norm = sqrt(S->red[0]);
@@ -962,6 +987,14 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
                          int derive_stage) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, nparts, k, S, derive_stage);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
+                          Scalars *S, hipStream_t s, int derive_stage) {
+  if (ka + kb > 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reduce2, dim3(1), dim3(kBlock), 0, s, pa, npa, ka, pb, npb, kb, S,
+                     derive_stage);
   return hipGetLastError();
 }
 
