@@ -1015,7 +1015,7 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
       (rc = al(c->partials,
                2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
-                                    size_t((L.n_owned + 255) / 256)) + 64,
+                                    size_t(pnp::spmv_parts(L.n_owned))) + 64,
                "partials")) ||
       (rc = al(c->partials2, size_t(pnp::blas_nparts(3LL * nloc)) + 64, "partials2")) ||
       (rc = al(c->S, 2, "scalars")) ||

@@ -82,6 +82,19 @@ __device__ __forceinline__ void load_vals(const double *__restrict__ sb, int lan
   if constexpr (NV & 1) B[NV - 1] = sb[(NV - 1) * kRows + lane];
 }
 
+// the same with a non-temporal hint (streamed once per launch: leaves L2 to the gathers)
+template <int NV>
+__device__ __forceinline__ void load_vals_nt(const double *__restrict__ sb, int lane, double *B) {
+#pragma unroll
+  for (int q = 0; q + 1 < NV; q += 2) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(sb + (q >> 1) * 2 * kRows) + lane);
+    B[q] = t.x;
+    B[q + 1] = t.y;
+  }
+  if constexpr (NV & 1) B[NV - 1] = __builtin_nontemporal_load(sb + (NV - 1) * kRows + lane);
+}
+
 template <int NV>
 __device__ __forceinline__ void store_vals(double *__restrict__ sb, int lane, const double *B) {
 #pragma unroll
@@ -286,6 +299,8 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
 // the derive step in the same launch (single GPU: no allreduce in between)
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
                          int derive_stage = -1);
+// partial-sum count of launch_spmv over nrows rows (allocation bound)
+int spmv_parts(int nrows);
 // sum partials pa[npa][ka] -> S->red[0..ka) and pb[npb][kb] -> S->red[ka..ka+kb), ka+kb <= 4
 hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
                           Scalars *S, hipStream_t s, int derive_stage = -1);

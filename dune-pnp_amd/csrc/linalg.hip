@@ -56,53 +56,75 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double *out) {
 // ------------------------------------------------------------------------------------------
 // SpMV (+ fused dots)
 // ------------------------------------------------------------------------------------------
-template <int NF, int PAT, int MODE, int SB>
+template <int NF, int PAT, int MODE, int SB, int LPR, int NT = 0>
 __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__restrict__ vals,
                                                  const double *__restrict__ x,
                                                  double *__restrict__ y,
                                                  const double *__restrict__ w,
                                                  double *__restrict__ partials) {
   constexpr int NV = popc9(PAT), NK = nks_of(PAT);
-  const int row = row_block(L, blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+  // LPR lanes per row (slots interleaved): block b covers part b % LPR of the 256-row group the
+  // spatial block map gives b / LPR
+  int row, q;
+  if constexpr (LPR == 1) {
+    row = row_block(L, blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    q = 0;
+  } else {
+    row = row_block(L, blockIdx.x / LPR, gridDim.x / LPR) * kBlock +
+          (blockIdx.x % LPR) * (kBlock / LPR) + threadIdx.x / LPR;
+    q = threadIdx.x % LPR;
+  }
+  const bool live = row < L.n_owned;
   double d[2] = {0, 0};
-  if (row < L.n_owned) {
-    const int chunk = row / kRows, lane = row % kRows;
-    const int off = L.chunk_off[chunk], len = L.chunk_len[chunk];
-    const int *__restrict__ cix = L.colidx + off + lane;
-    const double *__restrict__ vc = vals + size_t(off) * NK;  // chunk base (k-form), see vin()
-    double acc[NF];
+  double acc[NF];
 #pragma unroll
-    for (int f = 0; f < NF; f++) acc[f] = 0;
-    // slots in batches of SB: their column indices, then their gathers and values, are
-    // issued together (memory-level parallelism inside the thread)
-    for (int s0 = 0; s0 < len; s0 += SB) {
-      int j[SB];
+  for (int f = 0; f < NF; f++) acc[f] = 0;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = live ? L.chunk_off[chunk] : 0, len = live ? L.chunk_len[chunk] : 0;
+  const int *__restrict__ cix = L.colidx + off + lane;
+  const double *__restrict__ vc = vals + size_t(off) * NK;  // chunk base (k-form), see vin()
+  // slots in batches of SB: their column indices, then their gathers and values, are issued
+  // together (memory-level parallelism inside the thread); lane q takes slots q, q+LPR, ...
+  for (int s0 = q; s0 < len; s0 += SB * LPR) {
+    int j[SB];
 #pragma unroll
-      for (int b = 0; b < SB; b++) j[b] = s0 + b < len ? cix[(s0 + b) * kRows] : row;
-      double xj[SB][NF], k[SB][NK];
+    for (int b = 0; b < SB; b++) {
+      const int sl = s0 + b * LPR;
+      j[b] = sl < len ? cix[sl * kRows] : row;  // (non-temporal here: slower, reused)
+    }
+    double xj[SB][NF], k[SB][NK];
 #pragma unroll
-      for (int b = 0; b < SB; b++) {
-        load_nf<NF>(x, size_t(j[b]), xj[b]);
-        if (s0 + b < len) {
-          load_vals<NK>(vc + size_t(s0 + b) * NK * kRows, lane, k[b]);
-        } else {
+    for (int b = 0; b < SB; b++) {
+      const int sl = s0 + b * LPR;
+      load_nf<NF>(x, size_t(j[b]), xj[b]);
+      if (sl < len) {
+        if (NT)
+          load_vals_nt<NK>(vc + size_t(sl) * NK * kRows, lane, k[b]);
+        else
+          load_vals<NK>(vc + size_t(sl) * NK * kRows, lane, k[b]);
+      } else {
 #pragma unroll
-          for (int q = 0; q < NK; q++) k[b][q] = 0.0;
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < SB; b++) {
-        double a[NV];
-        expand_k<PAT>(k[b], a);
-#pragma unroll
-        for (int f = 0; f < NF; f++)
-#pragma unroll
-          for (int g = 0; g < NF; g++) {
-            const int v = pat_index(PAT, f, g);
-            if (v >= 0) acc[f] += a[v] * xj[b][g];
-          }
+        for (int qq = 0; qq < NK; qq++) k[b][qq] = 0.0;
       }
     }
+#pragma unroll
+    for (int b = 0; b < SB; b++) {
+      double a[NV];
+      expand_k<PAT>(k[b], a);
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int v = pat_index(PAT, f, g);
+          if (v >= 0) acc[f] += a[v] * xj[b][g];
+        }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1)
+#pragma unroll
+    for (int f = 0; f < NF; f++) acc[f] += __shfl_xor(acc[f], o, 64);
+  if (live && q == 0) {
     const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
     if (dm) {
       double xr[NF];
@@ -188,7 +210,7 @@ __device__ __forceinline__ SplitRow split_row(const DevLayout &L, const double *
 // lanes, slots interleaved), partial sums combined across the row's lanes.  A colour holds ~1/6
 // of the rows (~2 waves per SIMD at config 3), so latency is hidden inside the thread: the
 // column indices of B slots are loaded together, then their gathers and values together.
-template <int NF, int PAT, int LPR, int B>
+template <int NF, int PAT, int LPR, int B, int NT = 0>
 __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, int row,
                                               const double *__restrict__ v, double (&acc)[NF]) {
   constexpr int NV = popc9(PAT);
@@ -199,7 +221,7 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
 #pragma unroll
     for (int b = 0; b < B; b++) {
       const int s = sb + b * LPR;
-      j[b] = s < R.len ? R.cix[s * kRows] : row;
+      j[b] = s < R.len ? R.cix[s * kRows] : row;  // (non-temporal here: slower, reused)
     }
     double vj[B][NF], a[B][NV];
 #pragma unroll
@@ -212,7 +234,10 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
         for (int g = 0; g < NF; g++) vj[b][g] = 0.0;
       }
       if (use) {
-        load_vals<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
+        if (NT)
+          load_vals_nt<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
+        else
+          load_vals<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
       } else {
 #pragma unroll
         for (int qq = 0; qq < NV; qq++) a[b][qq] = 0.0;
@@ -240,7 +265,7 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
 // solve; backward: v_i += D_i^{-1}(t_i - sum_{j upper} A_ij v_j - D_i v_i), field by field.
 // KIND 1 forward, 0 backward, 2 both for the last colour (no upper neighbours: its backward
 // step is pointwise, t stays in registers).
-template <int NF, int PAT, int KIND, int LPR, int B>
+template <int NF, int PAT, int KIND, int LPR, int B, int NT>
 __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int nk,
                                                       const double *__restrict__ lv,
                                                       const double *__restrict__ uv,
@@ -262,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   if (!FWD) load_nf<NF>(v, size_t(row), vi);
   load_vals<NV>(R.dg, R.lane, Dg);
   double acc[NF];
-  split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
+  split_row_dot<NF, PAT, LPR, B, NT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
   if (FWD) {
 #pragma unroll
@@ -413,7 +438,7 @@ __device__ __forceinline__ void diag_upper_solve(const double (&Dg)[NV], double 
 // 24 V pore case, measured -- DESIGN.md §4.)
 enum { kIluFwd = 0, kIluBwd = 1, kIluLast = 2 };
 
-template <int NF, int PAT, int KIND, int LPR, int B>
+template <int NF, int PAT, int KIND, int LPR, int B, int NT>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
                                                        const double *__restrict__ lv,
                                                        const double *__restrict__ uv,
@@ -431,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   load_nf<NF>(FWD ? d : v, size_t(row), own);
   load_vals<NV>(R.dg, R.lane, Dg);
   double acc[NF];
-  split_row_dot<NF, PAT, LPR, B>(R, FWD ? 0 : 1, q, row, v, acc);
+  split_row_dot<NF, PAT, LPR, B, NT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] += own[f];
@@ -755,12 +780,31 @@ int blas_nparts(long long n) {
     }                                                                     \
   } while (0)
 
-// SpMV slot batch (PNP_SPMV_BATCH = 1, 2 or 4; A/B knob)
+// SpMV shape (A/B knobs): PNP_SPMV_BATCH = 1, 2, 4 or 8 slots per batch, PNP_SPMV_LPR = 1 or 2
+// lanes per row.  Default 2 lanes x 2-slot batches: ~2 % faster than 1 x 4
+// (profiles/r01/ab_spmv_shape.log); 8-slot batches do not help.
 static int spmv_batch() {
   static const int v = [] {
     const char *e = std::getenv("PNP_SPMV_BATCH");
-    const int b = e ? std::atoi(e) : 4;
-    return (b == 1 || b == 2 || b == 4) ? b : 4;
+    const int b = e ? std::atoi(e) : 2;
+    return (b == 1 || b == 2 || b == 4 || b == 8) ? b : 2;
+  }();
+  return v;
+}
+static int spmv_lpr() {
+  static const int v = [] {
+    const char *e = std::getenv("PNP_SPMV_LPR");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
+}
+// non-temporal loads of the matrix values (streamed once per launch; leaves L2 to the x
+// gathers): SpMV -2..3 %, and the following sweeps -1..2 % (profiles/r01/ab_spmv_nt.log);
+// PNP_SPMV_NT=0 turns it off (A/B)
+static bool spmv_nt() {
+  static const bool v = [] {
+    const char *e = std::getenv("PNP_SPMV_NT");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -768,26 +812,39 @@ static int spmv_batch() {
 template <int NF, int PAT, int MODE>
 static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double *vals,
                         const double *x, double *y, const double *w, double *partials) {
-  switch (spmv_batch()) {
-    case 1:
-      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 1>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
-      break;
-    case 2:
-      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 2>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
-      break;
-    default:
-      hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, 4>), g, dim3(kBlock), 0, s, L, vals, x, y, w,
-                         partials);
+#define PNP_SPMV_GO(SBc, LPRc)                                                                 \
+  hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc>), dim3(g.x * LPRc), dim3(kBlock), 0, s, \
+                     L, vals, x, y, w, partials)
+#define PNP_SPMV_GO2(SBc, LPRc, NTc)                                                        \
+  hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc, NTc>), dim3(g.x * LPRc), dim3(kBlock), \
+                     0, s, L, vals, x, y, w, partials)
+  const int b = spmv_batch(), l = spmv_lpr();
+  if (spmv_nt() && l == 2 && b == 2) {
+    PNP_SPMV_GO2(2, 2, 1);
+    return;
   }
+  if (l == 2) {
+    if (b == 8) PNP_SPMV_GO(8, 2);
+    else if (b == 2) PNP_SPMV_GO(2, 2);
+    else if (b == 1) PNP_SPMV_GO(1, 2);
+    else PNP_SPMV_GO(4, 2);
+  } else {
+    if (b == 8) PNP_SPMV_GO(8, 1);
+    else if (b == 2) PNP_SPMV_GO(2, 1);
+    else if (b == 1) PNP_SPMV_GO(1, 1);
+    else PNP_SPMV_GO(4, 1);
+  }
+#undef PNP_SPMV_GO
+#undef PNP_SPMV_GO2
 }
+
+int spmv_parts(int nrows) { return int(rows_grid(nrows).x) * spmv_lpr(); }
 
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
                        hipStream_t s) {
   dim3 g = rows_grid(L.n_owned);
-  if (nparts) *nparts = int(g.x);
+  if (nparts) *nparts = int(g.x) * spmv_lpr();
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
@@ -810,64 +867,52 @@ hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals
   return hipGetLastError();
 }
 
-// sweep kernel shape: lanes per row x slot batch (PNP_SWEEP = "LPRxB", e.g. 2x4; A/B knob)
+// sweep kernel shape: lanes per row x slot batch (PNP_SWEEP = "LPRxB": 1x2, 2x2, 2x4, default
+// 1x4; the other shapes measured in round 1 lost), and non-temporal loads of the
+// L/U values in the default shape (PNP_SWEEP_NT=0/1, A/B)
 static int sweep_cfg() {
   static const int v = [] {
     const char *e = std::getenv("PNP_SWEEP");
     int l = 1, b = 4;
     if (e && std::sscanf(e, "%dx%d", &l, &b) != 2) l = 1, b = 4;
-    int code = l * 16 + b;
-    switch (code) {
-      case 1 * 16 + 1: case 1 * 16 + 2: case 1 * 16 + 4: case 1 * 16 + 8:
-      case 2 * 16 + 1: case 2 * 16 + 2: case 2 * 16 + 4: case 4 * 16 + 1: case 4 * 16 + 2:
-        return code;
-      default:
-        return 1 * 16 + 4;
-    }
+    const int code = l * 16 + b;
+    return (code == 18 || code == 34 || code == 36) ? code : 20;
+  }();
+  return v;
+}
+static bool sweep_nt() {  // default on: ILU0 apply -7 %, SGS -7 % (profiles/r01/ab_sweep_nt.log)
+  static const bool v = [] {
+    const char *e = std::getenv("PNP_SWEEP_NT");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
 
-#define PNP_LPR_DISPATCH(CALL)           \
-  do {                                   \
-    switch (sweep_cfg()) {               \
-      case 17: {                         \
-        constexpr int LPRc = 1, Bc = 1;  \
-        CALL;                            \
-      } break;                           \
-      case 18: {                         \
-        constexpr int LPRc = 1, Bc = 2;  \
-        CALL;                            \
-      } break;                           \
-      case 24: {                         \
-        constexpr int LPRc = 1, Bc = 8;  \
-        CALL;                            \
-      } break;                           \
-      case 33: {                         \
-        constexpr int LPRc = 2, Bc = 1;  \
-        CALL;                            \
-      } break;                           \
-      case 34: {                         \
-        constexpr int LPRc = 2, Bc = 2;  \
-        CALL;                            \
-      } break;                           \
-      case 36: {                         \
-        constexpr int LPRc = 2, Bc = 4;  \
-        CALL;                            \
-      } break;                           \
-      case 65: {                         \
-        constexpr int LPRc = 4, Bc = 1;  \
-        CALL;                            \
-      } break;                           \
-      case 66: {                         \
-        constexpr int LPRc = 4, Bc = 2;  \
-        CALL;                            \
-      } break;                           \
-      default: {                         \
-        constexpr int LPRc = 1, Bc = 4;  \
-        CALL;                            \
-      } break;                           \
-    }                                    \
+#define PNP_LPR_DISPATCH(CALL)                     \
+  do {                                             \
+    switch (sweep_cfg()) {                         \
+      case 18: {                                   \
+        constexpr int LPRc = 1, Bc = 2, NTc = 0;   \
+        CALL;                                      \
+      } break;                                     \
+      case 34: {                                   \
+        constexpr int LPRc = 2, Bc = 2, NTc = 0;   \
+        CALL;                                      \
+      } break;                                     \
+      case 36: {                                   \
+        constexpr int LPRc = 2, Bc = 4, NTc = 0;   \
+        CALL;                                      \
+      } break;                                     \
+      default:                                     \
+        if (sweep_nt()) {                          \
+          constexpr int LPRc = 1, Bc = 4, NTc = 1; \
+          CALL;                                    \
+        } else {                                   \
+          constexpr int LPRc = 1, Bc = 4, NTc = 0; \
+          CALL;                                    \
+        }                                          \
+        break;                                     \
+    }                                              \
   } while (0)
 
 hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
@@ -880,7 +925,7 @@ hipError_t launch_sgs(const DevLayout &L, const int *cp, int nf, int pat, const 
     auto go = [&](auto kind, int c) {
       const int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, decltype(kind)::value, LPRc, Bc>),
+        hipLaunchKernelGGL((k_sgs_color<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc>),
                            rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], n, lv, uv, d, v, t);
     };
     for (int c = 0; c < nc - 1; c++) go(std::integral_constant<int, 1>(), c);
@@ -912,7 +957,7 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     auto go = [&](auto kind, int c) {
       const int n = cp[c + 1] - cp[c];
       if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc>),
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc>),
                            rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
                            d, v);
     };
