@@ -219,7 +219,10 @@ template <int OP>
 __device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, int s,
                                             const double *Kc) {
   constexpr int NK = OpTraits<OP>::NK;
-  store_vals<NK>(vc + size_t(s) * NK * kRows, lane, Kc);
+  // non-temporal: the blocks are read back only by later kernels (SpMV, split), which stream
+  // them non-temporally too; plain stores allocate the 207 MB in the caches and evict the
+  // gathered x / xy / column indices.  94 -> 77 us at config 3 (profiles/r01/ab_asm_nt_stores.log)
+  store_vals_nt<NK>(vc + size_t(s) * NK * kRows, lane, Kc);
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).

@@ -103,6 +103,19 @@ __device__ __forceinline__ void store_vals(double *__restrict__ sb, int lane, co
   if constexpr (NV & 1) sb[(NV - 1) * kRows + lane] = B[NV - 1];
 }
 
+template <int NV>
+__device__ __forceinline__ void store_vals_nt(double *__restrict__ sb, int lane, const double *B) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int q = 0; q + 1 < NV; q += 2) {
+    d2v t;
+    t.x = B[q];
+    t.y = B[q + 1];
+    __builtin_nontemporal_store(t, reinterpret_cast<d2v *>(sb + (q >> 1) * 2 * kRows) + lane);
+  }
+  if constexpr (NV & 1) __builtin_nontemporal_store(B[NV - 1], sb + (NV - 1) * kRows + lane);
+}
+
 // 256-row block processed by workgroup b of a whole-matrix launch of nwg workgroups
 template <class DL>
 __device__ __forceinline__ int row_block(const DL &L, int b, int nwg) {
