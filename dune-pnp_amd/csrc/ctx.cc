@@ -909,10 +909,11 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     g_err = c->err;
     return rc;
   }
-  {  // spatial block order (DevLayout::blkmap; SpMV -4 us at config 3, assembly neutral);
-     // A/B knob PNP_BLKMAP=0 disables it
+  {  // spatial block order (DevLayout::blkmap).  It paid 4 us of SpMV while the matrix streams
+     // went through the caches; with non-temporal matrix streams it costs ~1 us
+     // (profiles/r01/ab_blkmap_nt.log), so it is off unless PNP_BLKMAP=1
     const char *e = getenv("PNP_BLKMAP");
-    if (!(e && atoi(e) == 0) && L.n_owned > 0) {
+    if (e && atoi(e) == 1 && L.n_owned > 0) {
       int nblk = (L.n_owned + 255) / 256;
       std::vector<double> key(nblk);
       for (int b = 0; b < nblk; b++) {
