@@ -1,0 +1,63 @@
+// Aggregation AMG (PNP_PREC_AMG): host-side hierarchy (amg_setup.cc) and device launchers (amg.hip).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "mesh.h"
+
+namespace pnp {
+
+constexpr int kAmgMaxCoarse = 64;  // coarsest level: at most this many vertex blocks (dense solve)
+constexpr int kAmgMaxLevels = 16;
+
+// One coarse level l >= 1 (block-CSR, dense NF x NF blocks, columns sorted, diagonal present)
+// plus the maps to the level below it.
+struct AmgLevelHost {
+  int nb = 0;                        // rows (aggregates of the level below)
+  std::vector<int> rp, col, dpos;    // block-CSR pattern, diagonal block position per row
+  std::vector<long long> cptr;       // Galerkin contributors of each block: csrc[cptr[q]..cptr[q+1])
+  std::vector<int> csrc;             // level 1: (row << 6 | slot) of the SELL; else block index
+  std::vector<int> mptr, mem;        // rows of the level below in each aggregate (restriction)
+  std::vector<int> agg;              // rows of the level below -> this level's rows (prolongation)
+};
+
+// Greedy aggregation of the owned vertex rows over the matrix graph, recursively, until at most
+// coarse_target blocks remain (or max_levels).  Level 0 is the SELL layout of L (owned columns
+// only: the AMG is rank-local, i.e. block-Jacobi across ranks like the multicolour sweeps).
+bool amg_build(const LocalLayout &L, int coarse_target, int max_levels,
+               std::vector<AmgLevelHost> &levels, std::string &err);
+
+// aggregation of one graph (CSR adjacency without the diagonal): returns the number of aggregates
+int amg_aggregate(int n, const std::vector<int> &ap, const std::vector<int> &aj,
+                  std::vector<int> &agg);
+
+hipError_t launch_amg_galerkin0(const DevLayout &L, int nf, int pat, const double *kvals,
+                                long long nq, const long long *cptr, const int *csrc, double *cv,
+                                hipStream_t s);
+hipError_t launch_amg_galerkin(int nf, long long nq, const long long *cptr, const int *csrc,
+                               const double *fv, double *cv, hipStream_t s);
+hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, double *dinv,
+                           hipStream_t s);
+// work, ainv: (nb*nf)^2 doubles each
+hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
+                                     const double *v, double *work, double *ainv, hipStream_t s);
+// x1 == nullptr: no pre-smoothing (level 1 is the coarsest)
+hipError_t launch_amg_restrict0(int nf, int nb1, const int *mptr, const int *mem, const double *d,
+                                const double *t, double *b1, const double *dinv1, double omega,
+                                double *x1, hipStream_t s);
+hipError_t launch_amg_resid_restrict(int nf, int nbn, const int *mptr, const int *mem,
+                                     const int *rp, const int *col, const double *v,
+                                     const double *x, const double *b, double *bn,
+                                     const double *dinvn, double omega, double *xn, hipStream_t s);
+hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
+                                   hipStream_t s);
+hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
+                           const int *agg, const double *x, const double *e, const double *b,
+                           const double *dinv, double omega, double *out, hipStream_t s);
+hipError_t launch_amg_prolong0(int nf, int n, const int *agg, const double *x0, const double *e1,
+                               double *y, hipStream_t s);
+
+}  // namespace pnp

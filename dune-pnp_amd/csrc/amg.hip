@@ -1,0 +1,485 @@
+// Aggregation AMG preconditioner on gfx950 (PNP_PREC_AMG): the reference's CG_AMG_SSOR variant
+// (ISTLBackend_NOVLP_CG_AMG_SSOR, src/instationary_pnp_from_pb_md.hh:24,207-210; dune-istl
+// Amg::AMG with an SSOR smoother) restated for the GPU.
+//
+// Hierarchy (amg_setup.cc): level 0 is the assembled SELL matrix itself; level l+1 aggregates the
+// vertex rows of level l (greedy, on the matrix graph) with piecewise-constant prolongation, so
+// A_{l+1} = P^T A_l P is a plain sum of fine blocks.  Coarse levels are block-CSR with dense
+// NF x NF blocks.  The pattern and the per-coarse-block contributor lists are built once on the
+// host; the values are summed here after every assembly (deterministic: each coarse block is one
+// thread summing its contributors in a fixed order, no atomics).
+//
+// V-cycle (precond): level 0 pre/post-smoothing with the configured fine smoother (multicolour
+// SGS = SSOR(k=1, w=1) by default, or ILU(0) / Jacobi), damped block-Jacobi on the coarse
+// levels, an exact dense solve (Gauss-Jordan inverse, one workgroup) on the coarsest.
+// Restriction is fused with the residual and the next level's pre-smoothing; prolongation is
+// fused into the post-smoothing sweep.  Everything here is HBM/latency bound, fp64.
+#include "amg.h"
+
+namespace pnp {
+
+namespace {
+
+constexpr int kB = 256;
+
+// dense NF x NF block position of pattern value v
+template <int PAT>
+__device__ __forceinline__ int dense_of(int v) {
+  int c = 0;
+  for (int i = 0; i < 9; i++)
+    if ((PAT >> i) & 1) {
+      if (c == v) return (i / 3) * (PAT == kPatScalar ? 1 : 3) + (i % 3) * (PAT == kPatScalar ? 0 : 1);
+      c++;
+    }
+  return 0;
+}
+
+// ---- Galerkin products ----------------------------------------------------------------------
+// level 1 from the SELL k-form matrix: coarse block q = sum of the expanded, row-masked fine
+// blocks csrc[cptr[q] .. cptr[q+1]) (code row << 6 | slot)
+template <int NF, int PAT>
+__global__ __launch_bounds__(kB) void k_galerkin0(DevLayout L, const double *__restrict__ kv,
+                                                  long long nq, const long long *__restrict__ cptr,
+                                                  const int *__restrict__ csrc,
+                                                  double *__restrict__ cv) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT), NB = NF * NF;
+  const long long q = blockIdx.x * (long long)kB + threadIdx.x;
+  if (q >= nq) return;
+  double acc[NB];
+#pragma unroll
+  for (int v = 0; v < NB; v++) acc[v] = 0;
+  for (long long c = cptr[q]; c < cptr[q + 1]; c++) {
+    const int code = csrc[c], row = code >> 6, slot = code & 63;
+    const int chunk = row / kRows, lane = row % kRows;
+    double K[NK], B[NV];
+    load_vals<NK>(kv + (size_t(L.chunk_off[chunk]) + size_t(slot) * kRows) * NK, lane, K);
+    expand_k<PAT>(K, B);
+    mask_rows<NF, PAT>(B, row_mask<NF>(L, row), slot == 0);
+#pragma unroll
+    for (int v = 0; v < NV; v++) acc[dense_of<PAT>(v)] += B[v];
+  }
+#pragma unroll
+  for (int v = 0; v < NB; v++) cv[q * NB + v] = acc[v];
+}
+
+// level l+1 from level l (block-CSR): coarse block q = sum of fine blocks csrc[..]
+template <int NB>
+__global__ __launch_bounds__(kB) void k_galerkin(long long nq, const long long *__restrict__ cptr,
+                                                 const int *__restrict__ csrc,
+                                                 const double *__restrict__ fv,
+                                                 double *__restrict__ cv) {
+  const long long q = blockIdx.x * (long long)kB + threadIdx.x;
+  if (q >= nq) return;
+  double acc[NB];
+#pragma unroll
+  for (int v = 0; v < NB; v++) acc[v] = 0;
+  for (long long c = cptr[q]; c < cptr[q + 1]; c++) {
+    const double *s = fv + size_t(csrc[c]) * NB;
+#pragma unroll
+    for (int v = 0; v < NB; v++) acc[v] += s[v];
+  }
+#pragma unroll
+  for (int v = 0; v < NB; v++) cv[q * NB + v] = acc[v];
+}
+
+// in-register Gauss-Jordan inverse of an NF x NF block with partial pivoting
+template <int NF>
+__device__ __forceinline__ void block_inverse(double (&A)[NF * NF], double (&X)[NF * NF]) {
+#pragma unroll
+  for (int i = 0; i < NF * NF; i++) X[i] = (i % (NF + 1) == 0) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < NF; k++) {
+    int p = k;
+#pragma unroll
+    for (int i = k + 1; i < NF; i++)
+      if (fabs(A[i * NF + k]) > fabs(A[p * NF + k])) p = i;
+    if (p != k) {
+#pragma unroll
+      for (int j = 0; j < NF; j++) {
+        double t = A[k * NF + j];
+        A[k * NF + j] = A[p * NF + j];
+        A[p * NF + j] = t;
+        t = X[k * NF + j];
+        X[k * NF + j] = X[p * NF + j];
+        X[p * NF + j] = t;
+      }
+    }
+    const double inv = 1.0 / A[k * NF + k];
+#pragma unroll
+    for (int j = 0; j < NF; j++) {
+      A[k * NF + j] *= inv;
+      X[k * NF + j] *= inv;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+      if (i == k) continue;
+      const double f = A[i * NF + k];
+#pragma unroll
+      for (int j = 0; j < NF; j++) {
+        A[i * NF + j] -= f * A[k * NF + j];
+        X[i * NF + j] -= f * X[k * NF + j];
+      }
+    }
+  }
+}
+
+// dinv[i] = inverse of the diagonal block of row i (block-CSR, dpos = diagonal block position)
+template <int NF>
+__global__ __launch_bounds__(kB) void k_dinv(int nb, const int *__restrict__ dpos,
+                                             const double *__restrict__ v,
+                                             double *__restrict__ dinv) {
+  constexpr int NB = NF * NF;
+  const int i = blockIdx.x * kB + threadIdx.x;
+  if (i >= nb) return;
+  double A[NB], X[NB];
+#pragma unroll
+  for (int k = 0; k < NB; k++) A[k] = v[size_t(dpos[i]) * NB + k];
+  block_inverse<NF>(A, X);
+#pragma unroll
+  for (int k = 0; k < NB; k++) dinv[size_t(i) * NB + k] = X[k];
+}
+
+// coarsest level: ainv (column-major, n = nb * NF) = dense inverse of the block-CSR matrix by
+// Gauss-Jordan with partial pivoting, one workgroup (n <= kAmgMaxCoarse; the work matrix a is
+// L2-resident).  A singular pivot leaves zeros (the row's unknowns are then not corrected).
+constexpr int kGJ = 1024;
+__global__ __launch_bounds__(kGJ) void k_coarse_inverse(int nb, int nf, const int *__restrict__ rp,
+                                                        const int *__restrict__ col,
+                                                        const double *__restrict__ v,
+                                                        double *__restrict__ a,
+                                                        double *__restrict__ ainv) {
+  const int n = nb * nf, nbb = nf * nf, t = threadIdx.x;
+  __shared__ double fcol[kAmgMaxCoarse * 3];
+  __shared__ double pv[kGJ / 64];
+  __shared__ int pi[kGJ / 64];
+  __shared__ int piv;
+  // row-major work copy a, identity in ainv (row-major while eliminating, transposed at the end)
+  for (int k = t; k < n * n; k += kGJ) {
+    a[k] = 0.0;
+    ainv[k] = (k / n == k % n) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int r = t; r < nb; r += kGJ)
+    for (int q = rp[r]; q < rp[r + 1]; q++)
+      for (int e = 0; e < nbb; e++)
+        a[size_t(r * nf + e / nf) * n + col[q] * nf + e % nf] = v[size_t(q) * nbb + e];
+  __syncthreads();
+  for (int k = 0; k < n; k++) {
+    // pivot: argmax |a[i][k]|, i >= k (ties: lowest row)
+    double best = -1.0;
+    int bi = k;
+    for (int i = k + t; i < n; i += kGJ) {
+      const double m = fabs(a[size_t(i) * n + k]);
+      if (m > best) {
+        best = m;
+        bi = i;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (t % 64 == 0) {
+      pv[t / 64] = best;
+      pi[t / 64] = bi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double b = pv[0];
+      int p = pi[0];
+      for (int w = 1; w < kGJ / 64; w++)
+        if (pv[w] > b || (pv[w] == b && pi[w] < p)) {
+          b = pv[w];
+          p = pi[w];
+        }
+      piv = p;
+    }
+    __syncthreads();
+    const int p = piv;
+    if (p != k)
+      for (int j = t; j < n; j += kGJ) {
+        double x = a[size_t(k) * n + j];
+        a[size_t(k) * n + j] = a[size_t(p) * n + j];
+        a[size_t(p) * n + j] = x;
+        x = ainv[size_t(k) * n + j];
+        ainv[size_t(k) * n + j] = ainv[size_t(p) * n + j];
+        ainv[size_t(p) * n + j] = x;
+      }
+    __syncthreads();
+    const double d = a[size_t(k) * n + k];
+    const double inv = d != 0.0 ? 1.0 / d : 0.0;
+    for (int i = t; i < n; i += kGJ) fcol[i] = a[size_t(i) * n + k];
+    __syncthreads();
+    for (int j = t; j < n; j += kGJ) {
+      a[size_t(k) * n + j] *= inv;
+      ainv[size_t(k) * n + j] *= inv;
+    }
+    __syncthreads();
+    for (int e = t; e < n * n; e += kGJ) {
+      const int i = e / n, j = e % n;
+      if (i == k) continue;
+      const double f = fcol[i];
+      if (f == 0.0) continue;
+      a[e] -= f * a[size_t(k) * n + j];
+      ainv[e] -= f * ainv[size_t(k) * n + j];
+    }
+    __syncthreads();
+  }
+  // transpose ainv in place to column-major (coalesced GEMV reads)
+  for (int e = t; e < n * n; e += kGJ) {
+    const int i = e / n, j = e % n;
+    if (i < j) {
+      const double x = ainv[e];
+      ainv[e] = ainv[size_t(j) * n + i];
+      ainv[size_t(j) * n + i] = x;
+    }
+  }
+}
+
+// ---- V-cycle kernels ------------------------------------------------------------------------
+template <int NF>
+__device__ __forceinline__ void bmv_acc(const double *__restrict__ B, const double (&x)[NF],
+                                        double (&y)[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; f++)
+#pragma unroll
+    for (int g = 0; g < NF; g++) y[f] += B[f * NF + g] * x[g];
+}
+
+// coarse row J of level 1: b1 = sum over its members i of (d - A x0)_i (t = A x0);
+// x1 = omega Dinv_J b1 (pre-smoothing from zero) unless level 1 is the coarsest
+template <int NF>
+__global__ __launch_bounds__(kB) void k_restrict0(int nb1, const int *__restrict__ mptr,
+                                                  const int *__restrict__ mem,
+                                                  const double *__restrict__ d,
+                                                  const double *__restrict__ t,
+                                                  double *__restrict__ b1,
+                                                  const double *__restrict__ dinv1, double omega,
+                                                  double *__restrict__ x1) {
+  const int J = blockIdx.x * kB + threadIdx.x;
+  if (J >= nb1) return;
+  double s[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) s[f] = 0;
+  for (int m = mptr[J]; m < mptr[J + 1]; m++) {
+    const int i = mem[m];
+#pragma unroll
+    for (int f = 0; f < NF; f++) s[f] += d[size_t(i) * NF + f] - t[size_t(i) * NF + f];
+  }
+  store_nf<NF>(b1, size_t(J), s);
+  if (x1) {
+    double y[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) y[f] = 0;
+    bmv_acc<NF>(dinv1 + size_t(J) * NF * NF, s, y);
+#pragma unroll
+    for (int f = 0; f < NF; f++) y[f] *= omega;
+    store_nf<NF>(x1, size_t(J), y);
+  }
+}
+
+// level l -> l+1: b_{l+1}[J] = sum over members I of (b_l - A_l x_l)_I; pre-smoothing of l+1
+template <int NF>
+__global__ __launch_bounds__(kB) void k_resid_restrict(
+    int nbn, const int *__restrict__ mptr, const int *__restrict__ mem, const int *__restrict__ rp,
+    const int *__restrict__ col, const double *__restrict__ v, const double *__restrict__ x,
+    const double *__restrict__ b, double *__restrict__ bn, const double *__restrict__ dinvn,
+    double omega, double *__restrict__ xn) {
+  constexpr int NB = NF * NF;
+  const int J = blockIdx.x * kB + threadIdx.x;
+  if (J >= nbn) return;
+  double s[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) s[f] = 0;
+  for (int m = mptr[J]; m < mptr[J + 1]; m++) {
+    const int I = mem[m];
+    double ax[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) ax[f] = 0;
+    for (int q = rp[I]; q < rp[I + 1]; q++) {
+      double xj[NF];
+      load_nf<NF>(x, size_t(col[q]), xj);
+      bmv_acc<NF>(v + size_t(q) * NB, xj, ax);
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++) s[f] += b[size_t(I) * NF + f] - ax[f];
+  }
+  store_nf<NF>(bn, size_t(J), s);
+  if (xn) {
+    double y[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) y[f] = 0;
+    bmv_acc<NF>(dinvn + size_t(J) * NB, s, y);
+#pragma unroll
+    for (int f = 0; f < NF; f++) y[f] *= omega;
+    store_nf<NF>(xn, size_t(J), y);
+  }
+}
+
+// coarsest: x = Ainv b (ainv column-major n x n)
+__global__ __launch_bounds__(kB) void k_coarse_apply(int n, const double *__restrict__ ainv,
+                                                     const double *__restrict__ b,
+                                                     double *__restrict__ x) {
+  const int i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  double s = 0;
+  for (int j = 0; j < n; j++) s += ainv[size_t(j) * n + i] * b[j];
+  x[i] = s;
+}
+
+// post-smoothing of level l >= 1 with the coarse correction folded in:
+//   xc(j) = x[j] + e[agg[j]],  out[I] = xc(I) + omega Dinv_I (b_I - sum_j A_Ij xc(j))
+template <int NF>
+__global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
+                                             const int *__restrict__ col,
+                                             const double *__restrict__ v,
+                                             const int *__restrict__ agg,
+                                             const double *__restrict__ x,
+                                             const double *__restrict__ e,
+                                             const double *__restrict__ b,
+                                             const double *__restrict__ dinv, double omega,
+                                             double *__restrict__ out) {
+  constexpr int NB = NF * NF;
+  const int I = blockIdx.x * kB + threadIdx.x;
+  if (I >= nb) return;
+  double r[NF], xi[NF];
+  load_nf<NF>(b, size_t(I), r);
+  for (int q = rp[I]; q < rp[I + 1]; q++) {
+    const int j = col[q];
+    double xj[NF], ej[NF], mx[NF];
+    load_nf<NF>(x, size_t(j), xj);
+    load_nf<NF>(e, size_t(agg[j]), ej);
+#pragma unroll
+    for (int f = 0; f < NF; f++) mx[f] = -(xj[f] + ej[f]);
+    bmv_acc<NF>(v + size_t(q) * NB, mx, r);
+  }
+  {
+    double ei[NF];
+    load_nf<NF>(x, size_t(I), xi);
+    load_nf<NF>(e, size_t(agg[I]), ei);
+#pragma unroll
+    for (int f = 0; f < NF; f++) xi[f] += ei[f];
+  }
+  double y[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) y[f] = 0;
+  bmv_acc<NF>(dinv + size_t(I) * NB, r, y);
+#pragma unroll
+  for (int f = 0; f < NF; f++) xi[f] += omega * y[f];
+  store_nf<NF>(out, size_t(I), xi);
+}
+
+// level 0 prolongation: y = x0 + e1[agg0]
+template <int NF>
+__global__ __launch_bounds__(kB) void k_prolong0(int n, const int *__restrict__ agg,
+                                                 const double *__restrict__ x0,
+                                                 const double *__restrict__ e1,
+                                                 double *__restrict__ y) {
+  const int i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  double a[NF], c[NF];
+  load_nf<NF>(x0, size_t(i), a);
+  load_nf<NF>(e1, size_t(agg[i]), c);
+#pragma unroll
+  for (int f = 0; f < NF; f++) a[f] += c[f];
+  store_nf<NF>(y, size_t(i), a);
+}
+
+inline dim3 g1(long long n) { return dim3(unsigned((n + kB - 1) / kB)); }
+
+}  // namespace
+
+#define AMG_NF_DISPATCH(NF_, ...)         \
+  do {                                    \
+    if ((NF_) == 1) {                     \
+      constexpr int NFc = 1;              \
+      __VA_ARGS__;                        \
+    } else if ((NF_) == 3) {              \
+      constexpr int NFc = 3;              \
+      __VA_ARGS__;                        \
+    } else {                              \
+      return hipErrorInvalidValue;        \
+    }                                     \
+  } while (0)
+
+hipError_t launch_amg_galerkin0(const DevLayout &L, int nf, int pat, const double *kvals,
+                                long long nq, const long long *cptr, const int *csrc, double *cv,
+                                hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  if (nf == 3 && pat == kPatPnp)
+    hipLaunchKernelGGL((k_galerkin0<3, kPatPnp>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
+  else if (nf == 3 && pat == kPatPnpIE)
+    hipLaunchKernelGGL((k_galerkin0<3, kPatPnpIE>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
+  else if (nf == 1)
+    hipLaunchKernelGGL((k_galerkin0<1, kPatScalar>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_galerkin(int nf, long long nq, const long long *cptr, const int *csrc,
+                               const double *fv, double *cv, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_galerkin<NFc * NFc>), g1(nq), dim3(kB), 0, s, nq, cptr,
+                                          csrc, fv, cv));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, double *dinv,
+                           hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_dinv<NFc>), g1(nb), dim3(kB), 0, s, nb, dpos, v, dinv));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
+                                     const double *v, double *work, double *ainv, hipStream_t s) {
+  if (nb * nf > kAmgMaxCoarse * 3 || (nf != 1 && nf != 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_coarse_inverse, dim3(1), dim3(kGJ), 0, s, nb, nf, rp, col, v, work, ainv);
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_restrict0(int nf, int nb1, const int *mptr, const int *mem, const double *d,
+                                const double *t, double *b1, const double *dinv1, double omega,
+                                double *x1, hipStream_t s) {
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_restrict0<NFc>), g1(nb1), dim3(kB), 0, s, nb1, mptr,
+                                          mem, d, t, b1, dinv1, omega, x1));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_resid_restrict(int nf, int nbn, const int *mptr, const int *mem,
+                                     const int *rp, const int *col, const double *v,
+                                     const double *x, const double *b, double *bn,
+                                     const double *dinvn, double omega, double *xn, hipStream_t s) {
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid_restrict<NFc>), g1(nbn), dim3(kB), 0, s, nbn,
+                                          mptr, mem, rp, col, v, x, b, bn, dinvn, omega, xn));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(k_coarse_apply, g1(n), dim3(kB), 0, s, n, ainv, b, x);
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
+                           const int *agg, const double *x, const double *e, const double *b,
+                           const double *dinv, double omega, double *out, hipStream_t s) {
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc>), g1(nb), dim3(kB), 0, s, nb, rp, col, v,
+                                          agg, x, e, b, dinv, omega, out));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_prolong0(int nf, int n, const int *agg, const double *x0, const double *e1,
+                               double *y, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_prolong0<NFc>), g1(n), dim3(kB), 0, s, n, agg, x0, e1,
+                                          y));
+  return hipGetLastError();
+}
+
+}  // namespace pnp

@@ -242,6 +242,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   const uint64_t meta = L.rowmeta[row];
   const int len = int(meta & 63);
   const bool closed = (meta >> 6) & 1;
+  const unsigned brk = unsigned(meta >> 8);  // fan-break bits, bit s: no element after slot s
   const int *__restrict__ cix = L.colidx + off + lane;
   double *__restrict__ vc = a.vals + size_t(off) * NK;  // chunk base (k-form), see vin()
 
@@ -252,9 +253,6 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   double ai = 0, aq = 0;
   if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) ai = a.aux0[row];
   if constexpr (OP == OP_POISSON) aq = a.aux1[row];
-  unsigned dm = 0;
-#pragma unroll
-  for (int f = 0; f < NF; f++) dm |= unsigned(a.dmask[size_t(row) * NF + f] != 0) << f;
 
   double R[NF], D[NK], P[NK], F[NK];  // block coefficients, see OpTraits::NK
 #pragma unroll
@@ -316,7 +314,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
         jn = tnn > 0 ? cix[tnn * kRows] : -1;
       }
     }
-    const bool elem = t > 0 && !((meta >> (8 + s)) & 1);
+    const bool elem = t > 0 && !((brk >> s) & 1);
     if (elem) {
       Geo G;
       geometry(pi2.x, pi2.y, pc.x, pc.y, pn.x, pn.y, G);
@@ -366,7 +364,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 #pragma unroll
   for (int f = 0; f < NF; f++) {
     double rv = R[f] + a.cvec[size_t(row) * NF + f];
-    a.r[size_t(row) * NF + f] = ((dm >> f) & 1) ? 0.0 : rv;
+    a.r[size_t(row) * NF + f] = a.dmask[size_t(row) * NF + f] != 0 ? 0.0 : rv;
   }
 }
 
@@ -477,19 +475,23 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     const char *e = getenv("PNP_ASM_FANR");
     return !(e && atoi(e) == 0);
   }();
-  const bool fanr = fanr_ok && L.max_slots <= 12;
+  // column indices in registers: FANR - 1 >= the longest fan (max_slots - 1; 8 on all meshes
+  // seen), 12 as the general case, 0 (index loads in the walk) beyond
+  const int fanr = !fanr_ok ? 0 : (L.max_slots <= 9 ? 9 : (L.max_slots <= 12 ? 12 : 0));
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
     if (!fanr && a.jac)                                                            \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
     else if (!fanr)                                                                \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
-    else if (a.jac && waves == 3)                                                  \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
-    else if (a.jac)                                                                \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 4, 12>), grid, block, 0, s, L, a);    \
-    else                                                                           \
+    else if (!a.jac)                                                               \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, L, a);    \
+    else if (fanr == 12)                                                           \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
+    else if (waves == 3)                                                           \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 9>), grid, block, 0, s, L, a);     \
+    else                                                                           \
+      hipLaunchKernelGGL((k_assemble<OPK, 1, 4, 9>), grid, block, 0, s, L, a);     \
     break;
   switch (a.kind) {
     PNP_ASM_CASE(OP_PNP)

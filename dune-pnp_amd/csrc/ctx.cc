@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/pnp_capi.h"
+#include "amg.h"
 #include "kernels.h"
 #include "mesh.h"
 
@@ -125,6 +126,22 @@ struct pnp_ctx {
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
+
+  // aggregation AMG (PNP_PREC_AMG, amg.h): the pattern hierarchy is built once per context (it
+  // depends on the layout only), the coarse values after every assembly
+  pnp_amg_opts amg_opts{PNP_PREC_SSOR, pnp::kAmgMaxCoarse, 12, 0.8};
+  std::vector<pnp::AmgLevelHost> amg_h;
+  struct AmgDev {
+    int nb = 0;
+    DBuf<int> rp, col, dpos, mptr, mem, agg, csrc;
+    DBuf<long long> cptr;
+    DBuf<double> v, dinv, b, x, x2;
+  };
+  std::vector<std::unique_ptr<AmgDev>> amg_d;  // amg_d[k] = level k + 1
+  bool amg_built = false, amg_valid = false;
+  int amg_nf = 0;
+  double amg_setup_ms = 0;
+  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
 
   // vectors (sized n_local * 3)
   DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials, partials2;
@@ -383,6 +400,7 @@ struct pnp_ctx {
       assembled = true;
       lu_valid = false;
       split_of = 0;
+      amg_valid = false;
     }
     return PNP_OK;
   }
@@ -413,12 +431,133 @@ struct pnp_ctx {
     return PNP_OK;
   }
 
-  // v = M^{-1} d over owned rows (v sized n_local)
-  int precond(int prec, const double *d, double *vout) {
+  // ---- aggregation AMG ------------------------------------------------------------------------
+  template <typename T>
+  int upv(DBuf<T> &d, const std::vector<T> &h, const char *what) {
+    hipError_t e = d.alloc(std::max<size_t>(1, h.size()));
+    if (e == hipSuccess && !h.empty())
+      e = hipMemcpy(d.p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice);
+    return e == hipSuccess ? PNP_OK : hipfail(e, what);
+  }
+
+  // hierarchy patterns (once), value/vector buffers (per field count), coarse values (per
+  // assembly): Galerkin sums, block-diagonal inverses, the coarsest dense inverse
+  int amg_setup() {
     int rc;
-    if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
-    if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
-    hipEvent_t t0 = tb(T_PREC);
+    if (!assembled) return fail(PNP_E_STATE, "no Jacobian assembled");
+    if (!amg_built) {
+      amg_d.clear();
+      if (!pnp::amg_build(L, amg_opts.coarse_target, amg_opts.max_levels, amg_h, err))
+        return PNP_E_STATE;
+      for (const auto &H : amg_h) {
+        auto D = std::make_unique<AmgDev>();
+        D->nb = H.nb;
+        if ((rc = upv(D->rp, H.rp, "amg rp")) || (rc = upv(D->col, H.col, "amg col")) ||
+            (rc = upv(D->dpos, H.dpos, "amg dpos")) || (rc = upv(D->mptr, H.mptr, "amg mptr")) ||
+            (rc = upv(D->mem, H.mem, "amg mem")) || (rc = upv(D->agg, H.agg, "amg agg")) ||
+            (rc = upv(D->csrc, H.csrc, "amg csrc")) || (rc = upv(D->cptr, H.cptr, "amg cptr")))
+          return rc;
+        amg_d.push_back(std::move(D));
+      }
+      amg_built = true;
+      amg_nf = 0;
+    }
+    if (amg_d.empty()) return fail(PNP_E_STATE, "AMG: no owned rows");
+    const int K = int(amg_d.size());
+    if (amg_d[K - 1]->nb * nf > pnp::kAmgMaxCoarse * 3)
+      return fail(PNP_E_STATE, "AMG: coarsest level too large for the dense solve");
+    if (amg_nf != nf) {
+      const size_t nb2 = size_t(nf) * nf;
+      for (auto &D : amg_d) {
+        hipError_t e;
+        if ((e = D->v.alloc(std::max<size_t>(1, D->col.n) * nb2)) != hipSuccess ||
+            (e = D->dinv.alloc(size_t(D->nb) * nb2)) != hipSuccess ||
+            (e = D->b.alloc(size_t(D->nb) * nf)) != hipSuccess ||
+            (e = D->x.alloc(size_t(D->nb) * nf)) != hipSuccess ||
+            (e = D->x2.alloc(size_t(D->nb) * nf)) != hipSuccess)
+          return hipfail(e, "amg level buffers");
+      }
+      const size_t nc = size_t(amg_d[K - 1]->nb) * nf, nl = size_t(L.n_owned + L.n_ghost) * nf;
+      hipError_t e;
+      if ((e = amg_work.alloc(nc * nc)) != hipSuccess || (e = amg_ainv.alloc(nc * nc)) != hipSuccess ||
+          (e = amg_x0.alloc(nl)) != hipSuccess || (e = amg_t.alloc(nl)) != hipSuccess ||
+          (e = amg_y.alloc(nl)) != hipSuccess || (e = amg_r.alloc(nl)) != hipSuccess ||
+          (e = amg_z.alloc(nl)) != hipSuccess)
+        return hipfail(e, "amg vectors");
+      amg_nf = nf;
+      amg_valid = false;
+    }
+    const int sm = amg_opts.smoother;
+    if (sm == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (sm == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
+    if (amg_valid) return PNP_OK;
+    hipEvent_t t0 = tb(T_FACT);
+    double ts = now_s();
+    hipError_t e = pnp::launch_amg_galerkin0(dl, nf, pat, vals.p, (long long)amg_h[0].col.size(),
+                                             amg_d[0]->cptr.p, amg_d[0]->csrc.p, amg_d[0]->v.p,
+                                             stream);
+    for (int k = 1; k < K && e == hipSuccess; k++)
+      e = pnp::launch_amg_galerkin(nf, (long long)amg_h[k].col.size(), amg_d[k]->cptr.p,
+                                   amg_d[k]->csrc.p, amg_d[k - 1]->v.p, amg_d[k]->v.p, stream);
+    for (int k = 0; k + 1 < K && e == hipSuccess; k++)
+      e = pnp::launch_amg_dinv(nf, amg_d[k]->nb, amg_d[k]->dpos.p, amg_d[k]->v.p,
+                               amg_d[k]->dinv.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_amg_coarse_inverse(nf, amg_d[K - 1]->nb, amg_d[K - 1]->rp.p,
+                                         amg_d[K - 1]->col.p, amg_d[K - 1]->v.p, amg_work.p,
+                                         amg_ainv.p, stream);
+    if (e != hipSuccess) return hipfail(e, "amg setup");
+    te(T_FACT, t0);
+    amg_setup_ms = (now_s() - ts) * 1e3;  // host-side issue time (device time: T_FACT timers)
+    amg_valid = true;
+    return PNP_OK;
+  }
+
+  // one V-cycle: vout = B d (owned rows); see amg.hip for the kernels
+  int amg_apply(const double *d, double *vout) {
+    const int K = int(amg_d.size()), sm = amg_opts.smoother, n = L.n_owned;
+    const double om = amg_opts.omega;
+    const long long nn = nown();
+    int rc, nsp = 0;
+    hipError_t e;
+    // level 0 pre-smoothing from zero, residual, restriction (+ level-1 pre-smoothing)
+    if ((rc = smoother(sm, d, amg_x0.p))) return rc;
+    e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 0, nullptr, partials.p, &nsp,
+                         stream);
+    if (e == hipSuccess)
+      e = pnp::launch_amg_restrict0(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, d,
+                                    amg_t.p, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
+                                    K > 1 ? amg_d[0]->x.p : nullptr, stream);
+    for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
+      AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
+      e = pnp::launch_amg_resid_restrict(nf, N.nb, N.mptr.p, N.mem.p, C.rp.p, C.col.p, C.v.p,
+                                         C.x.p, C.b.p, N.b.p, N.dinv.p, om,
+                                         k + 2 < K ? N.x.p : nullptr, stream);
+    }
+    if (e == hipSuccess)
+      e = pnp::launch_amg_coarse_apply(amg_d[K - 1]->nb * nf, amg_ainv.p, amg_d[K - 1]->b.p,
+                                       amg_d[K - 1]->x.p, stream);
+    const double *res = amg_d[K - 1]->x.p;  // the solution of the level just finished
+    for (int k = K - 2; k >= 0 && e == hipSuccess; k--) {
+      AmgDev &C = *amg_d[k];
+      e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, amg_d[k + 1]->agg.p, C.x.p, res,
+                               C.b.p, C.dinv.p, om, C.x2.p, stream);
+      res = C.x2.p;
+    }
+    // level 0: prolongation, post-smoothing x += M^{-1} (d - A x)
+    if (e == hipSuccess) e = pnp::launch_amg_prolong0(nf, n, amg_d[0]->agg.p, amg_x0.p, res, amg_y.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_y.p, amg_t.p, 0, nullptr, partials.p, &nsp,
+                           stream);
+    if (e == hipSuccess) e = pnp::launch_axpby(nn, 1.0, d, -1.0, amg_t.p, amg_r.p, stream);
+    if (e != hipSuccess) return hipfail(e, "amg v-cycle");
+    if ((rc = smoother(sm, amg_r.p, amg_z.p))) return rc;
+    e = pnp::launch_axpby(nn, 1.0, amg_y.p, 1.0, amg_z.p, vout, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "amg v-cycle");
+  }
+
+  // the single-level preconditioners, untimed, prerequisites (split / factors) in place
+  int smoother(int prec, const double *d, double *vout) {
     hipError_t e = hipSuccess;
     if (prec == PNP_PREC_JACOBI) {
       e = pnp::launch_jacobi(dl, nf, pat, vals.p, d, vout, stream);
@@ -431,7 +570,22 @@ struct pnp_ctx {
     } else {
       e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
     }
-    if (e != hipSuccess) return hipfail(e, "preconditioner");
+    return e == hipSuccess ? PNP_OK : hipfail(e, "preconditioner");
+  }
+
+  // v = M^{-1} d over owned rows (v sized n_local)
+  int precond(int prec, const double *d, double *vout) {
+    int rc;
+    if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
+    if (prec == PNP_PREC_AMG && (rc = amg_setup())) return rc;
+    hipEvent_t t0 = tb(T_PREC);
+    if (prec == PNP_PREC_AMG) {
+      if ((rc = amg_apply(d, vout))) return rc;
+      te(T_PREC, t0);
+      return PNP_OK;
+    }
+    if ((rc = smoother(prec, d, vout))) return rc;
     te(T_PREC, t0);
     return PNP_OK;
   }
@@ -473,6 +627,7 @@ struct pnp_ctx {
     int prec = o.prec;
     if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (prec == PNP_PREC_AMG && (rc = amg_setup())) return rc;
     int nsp = 0;
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
@@ -1116,6 +1271,7 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   c->assembled = false;
   c->lu_valid = false;
   c->split_of = 0;
+  c->amg_valid = false;
   // SELL padding slots point at the row itself and are never written by the assembly, so they
   // must hold zeros in the k-form layout of THIS operator (the SpMV multiplies them)
   CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nks, c->stream),
@@ -1283,7 +1439,7 @@ extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const 
 }
 
 extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double *v) {
-  if (!c || !d || !v || prec < PNP_PREC_NONE || prec > PNP_PREC_JACOBI) return PNP_E_ARG;
+  if (!c || !d || !v || prec < PNP_PREC_NONE || prec > PNP_PREC_AMG) return PNP_E_ARG;
   if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
   hipSetDevice(c->device);
   int rc;
@@ -1291,6 +1447,51 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
   if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
   if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
   return c->download_ext(c->z.p, c->nf, v);
+}
+
+extern "C" int pnp_amg_configure(pnp_ctx *c, const pnp_amg_opts *o) {
+  if (!c || !o) return PNP_E_ARG;
+  if (o->smoother != PNP_PREC_SSOR && o->smoother != PNP_PREC_ILU0 && o->smoother != PNP_PREC_JACOBI)
+    return c->fail(PNP_E_ARG, "AMG smoother must be SSOR, ILU0 or JACOBI");
+  if (o->coarse_target < 1 || o->coarse_target > pnp::kAmgMaxCoarse || o->max_levels < 2 ||
+      o->max_levels > pnp::kAmgMaxLevels || !(o->omega > 0 && o->omega <= 2))
+    return c->fail(PNP_E_ARG, "AMG options out of range");
+  const bool rebuild = o->coarse_target != c->amg_opts.coarse_target ||
+                       o->max_levels != c->amg_opts.max_levels;
+  c->amg_opts = *o;
+  if (rebuild) c->amg_built = false;
+  c->amg_valid = false;
+  return PNP_OK;
+}
+
+extern "C" int pnp_amg_info(pnp_ctx *c, pnp_amg_stats *st) {
+  if (!c || !st) return PNP_E_ARG;
+  std::memset(st, 0, sizeof *st);
+  if (!c->amg_built) return c->fail(PNP_E_STATE, "AMG not set up (solve or apply with PNP_PREC_AMG)");
+  st->levels = int(c->amg_h.size()) + 1;
+  st->rows[0] = c->L.n_owned;
+  st->blocks[0] = c->L.nblocks;
+  for (size_t k = 0; k < c->amg_h.size() && k + 1 < 16; k++) {
+    st->rows[k + 1] = c->amg_h[k].nb;
+    st->blocks[k + 1] = (int64_t)c->amg_h[k].col.size();
+  }
+  st->omega = c->amg_opts.omega;
+  st->smoother = c->amg_opts.smoother;
+  return PNP_OK;
+}
+
+extern "C" int pnp_amg_aggregates(pnp_ctx *c, int32_t level, int32_t *agg) {
+  if (!c || !agg || level < 0) return PNP_E_ARG;
+  if (!c->amg_built) return c->fail(PNP_E_STATE, "AMG not set up");
+  if (level >= int(c->amg_h.size())) return c->fail(PNP_E_ARG, "no such AMG level");
+  const std::vector<int> &a = c->amg_h[level].agg;
+  if (level == 0) {  // global vertex numbering, -1 for vertices this rank does not own
+    for (int g = 0; g < c->mesh.nv; g++) agg[g] = -1;
+    for (int i = 0; i < c->L.n_owned; i++) agg[c->L.l2g[i]] = a[i];
+  } else {
+    std::copy(a.begin(), a.end(), agg);
+  }
+  return PNP_OK;
 }
 
 extern "C" int pnp_ion_flux(pnp_ctx *c, const double *x, int32_t nsurf, double *ip, double *im) {

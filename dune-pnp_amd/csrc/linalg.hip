@@ -33,9 +33,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // block-wide sum of K values, result written by thread 0 to out[0..K)
-template <int K>
+template <int K, int NT = kBlock>
 __device__ __forceinline__ void block_sum(double (&v)[K], double *out) {
-  __shared__ double sh[kBlock / 64][K > 0 ? K : 1];
+  __shared__ double sh[NT / 64][K > 0 ? K : 1];
   const int w = threadIdx.x / 64, l = threadIdx.x % 64;
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -47,7 +47,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double *out) {
 #pragma unroll
     for (int k = 0; k < K; k++) {
       double s = 0;
-      for (int i = 0; i < kBlock / 64; i++) s += sh[i][k];
+      for (int i = 0; i < NT / 64; i++) s += sh[i][k];
       out[k] = s;
     }
   }
@@ -600,33 +600,45 @@ __global__ __launch_bounds__(kBlock) void k_dot(long long n, const double *__res
 
 __device__ void derive(Scalars *S, int stage);
 
-__global__ __launch_bounds__(kBlock) void k_reduce(const double *__restrict__ partials, int np,
-                                                   int k, Scalars *__restrict__ S, int stage) {
-  if (S->done && stage != 0 && stage != 10) return;
-  double acc[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < np; i += kBlock)
-    for (int j = 0; j < k; j++) acc[j] += partials[size_t(i) * k + j];
-  double out[4];
-  block_sum<4>(acc, out);
-  if (threadIdx.x == 0) {
-    for (int j = 0; j < k; j++) S->red[j] = out[j];
-    if (stage >= 0) derive(S, stage);
+// Final reduction of per-workgroup partials (deterministic: fixed order for a given np).
+// One workgroup of kRedBlock threads; each thread issues its (up to kRedU) partial loads back to
+// back before adding, so the ~3K partials of a config-3 SpMV cost one memory round trip instead
+// of the ~11 dependent ones of a 256-thread strided loop (13.8 -> see DESIGN.md, reductions).
+constexpr int kRedBlock = 1024, kRedU = 4;
+
+template <int K>
+__device__ __forceinline__ void accum_partials(const double *__restrict__ p, int np, double *acc) {
+  for (int i0 = threadIdx.x; i0 < np; i0 += kRedU * kRedBlock) {
+    double v[kRedU][K];
+#pragma unroll
+    for (int u = 0; u < kRedU; u++) {
+      const int i = i0 + u * kRedBlock;
+#pragma unroll
+      for (int j = 0; j < K; j++) v[u][j] = i < np ? p[size_t(i) * K + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kRedU; u++)
+#pragma unroll
+      for (int j = 0; j < K; j++) acc[j] += v[u][j];
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_reduce2(const double *__restrict__ pa, int npa, int ka,
-                                                    const double *__restrict__ pb, int npb, int kb,
-                                                    Scalars *__restrict__ S, int stage) {
-  if (S->done) return;
-  double acc[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < npa; i += kBlock)
-    for (int j = 0; j < ka; j++) acc[j] += pa[size_t(i) * ka + j];
-  for (int i = threadIdx.x; i < npb; i += kBlock)
-    for (int j = 0; j < kb; j++) acc[ka + j] += pb[size_t(i) * kb + j];
-  double out[4];
-  block_sum<4>(acc, out);
+template <int KA, int KB>
+__global__ __launch_bounds__(kRedBlock) void k_reduce(const double *__restrict__ pa, int npa,
+                                                      const double *__restrict__ pb, int npb,
+                                                      Scalars *__restrict__ S, int stage) {
+  // the start stages (0 BiCGSTAB, 10 CG) run on a fresh state; everything else stops once done
+  if (S->done && stage != 0 && stage != 10) return;
+  double acc[KA + KB];
+#pragma unroll
+  for (int j = 0; j < KA + KB; j++) acc[j] = 0;
+  accum_partials<KA>(pa, npa, acc);
+  if constexpr (KB > 0) accum_partials<KB>(pb, npb, acc + KA);
+  double out[KA + KB];
+  block_sum<KA + KB, kRedBlock>(acc, out);
   if (threadIdx.x == 0) {
-    for (int j = 0; j < ka + kb; j++) S->red[j] = out[j];
+#pragma unroll
+    for (int j = 0; j < KA + KB; j++) S->red[j] = out[j];
     if (stage >= 0) derive(S, stage);
   }
 }
@@ -1031,15 +1043,28 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
 
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
                          int derive_stage) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, nparts, k, S, derive_stage);
+  const dim3 g(1), b(kRedBlock);
+  switch (k) {
+    case 1: hipLaunchKernelGGL((k_reduce<1, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage); break;
+    case 2: hipLaunchKernelGGL((k_reduce<2, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage); break;
+    case 3: hipLaunchKernelGGL((k_reduce<3, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage); break;
+    case 4: hipLaunchKernelGGL((k_reduce<4, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
                           Scalars *S, hipStream_t s, int derive_stage) {
-  if (ka + kb > 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_reduce2, dim3(1), dim3(kBlock), 0, s, pa, npa, ka, pb, npb, kb, S,
-                     derive_stage);
+  const dim3 g(1), b(kRedBlock);
+  if (ka == 2 && kb == 1)
+    hipLaunchKernelGGL((k_reduce<2, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
+  else if (ka == 1 && kb == 1)
+    hipLaunchKernelGGL((k_reduce<1, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
+  else if (ka == 2 && kb == 2)
+    hipLaunchKernelGGL((k_reduce<2, 2>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -31,10 +31,10 @@ HEADER = os.path.join(REPO_ROOT, "include", "pnp_capi.h")
 OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = \
     0, -1, -2, -3, -4, -5, -6, -7, -8
 OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
-PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI = range(4)
+PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG = range(5)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
-                "jacobi": PREC_JACOBI}
+                "jacobi": PREC_JACOBI, "amg": PREC_AMG}
 MAX_SURFACES = 64
 
 
@@ -105,6 +105,16 @@ class _SolveResult(C.Structure):
     _fields_ = [("converged", C.c_int32), ("iterations", C.c_int32), ("breakdown", C.c_int32),
                 ("it_half", C.c_double), ("defect0", C.c_double), ("defect", C.c_double),
                 ("reduction", C.c_double), ("elapsed", C.c_double)]
+
+
+class _AmgOpts(C.Structure):
+    _fields_ = [("smoother", C.c_int32), ("coarse_target", C.c_int32), ("max_levels", C.c_int32),
+                ("omega", C.c_double)]
+
+
+class _AmgStats(C.Structure):
+    _fields_ = [("levels", C.c_int32), ("smoother", C.c_int32), ("rows", C.c_int32 * 16),
+                ("blocks", C.c_int64 * 16), ("omega", C.c_double)]
 
 
 class _NewtonOpts(C.Structure):
@@ -473,6 +483,26 @@ class Context:
         v = np.zeros_like(d)
         self._ck(lib().pnp_prec_apply(self.h, int(prec), _ptr(d), _ptr(v)))
         return v
+
+    def amg_configure(self, smoother=PREC_SSOR, coarse_target=64, max_levels=12, omega=0.8):
+        """Options of PREC_AMG (the reference's CG_AMG_SSOR preconditioner); see pnp_capi.h."""
+        o = _AmgOpts(int(smoother), int(coarse_target), int(max_levels), float(omega))
+        self._ck(lib().pnp_amg_configure(self.h, C.byref(o)))
+
+    def amg_info(self):
+        st = _AmgStats()
+        self._ck(lib().pnp_amg_info(self.h, C.byref(st)))
+        n = st.levels
+        return {"levels": n, "rows": list(st.rows[:n]), "blocks": list(st.blocks[:n]),
+                "smoother": st.smoother, "omega": st.omega}
+
+    def amg_aggregates(self, level):
+        """level 0: aggregate per global vertex (-1: not owned); level l: per level-l row."""
+        info = self.amg_info()
+        n = self.mesh.nv if level == 0 else info["rows"][level]
+        agg = np.zeros(n, dtype=np.int32)
+        self._ck(lib().pnp_amg_aggregates(self.h, int(level), _ptr(agg)))
+        return agg
 
     def ion_flux(self, x=None, nsurf=None):
         """calcIonFlux (src/ionFlux.hh:8-96): per-surface (ip, im) of x = [phi|c+|c-] (or of

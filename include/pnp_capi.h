@@ -192,7 +192,9 @@ int pnp_jacobian(pnp_ctx *ctx, const double *x);
 int pnp_jacobian_export(pnp_ctx *ctx, int64_t *nnz, int32_t *rowptr, int32_t *col, double *val);
 
 /* ---- linear solve (ISTL BiCGSTABSolver semantics) ----------------------------------------- */
-enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3 };
+enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3,
+       PNP_PREC_AMG = 4 /* aggregation AMG V-cycle (ISTL Amg::AMG of LINEARSOLVER CG_AMG_SSOR,
+                            src/instationary_pnp_from_pb_md.hh:207-210); see pnp_amg_configure */ };
 enum { PNP_METHOD_BICGSTAB = 0, PNP_METHOD_CG = 1 };
 typedef struct {
   int32_t prec;       /* SSOR = one multicolour symmetric Gauss-Seidel sweep (k=1, w=1) */
@@ -214,6 +216,34 @@ typedef struct {
  * Multicolour semantics: SSOR = one forward + one backward multicolour
  * Gauss-Seidel sweep, ILU0 = ILU(0) of the stored block pattern in colour-major vertex order. */
 int pnp_prec_apply(pnp_ctx *ctx, int32_t prec, const double *d, double *v);
+
+/* ---- aggregation AMG (PNP_PREC_AMG) ---------------------------------------------------------
+ * Replaces the preconditioner of ISTLBackend_NOVLP_CG_AMG_SSOR (the reference's LINEARSOLVER
+ * CG_AMG_SSOR, src/instationary_pnp_from_pb_md.hh:24,207-210, constructed with maxiter from the
+ * config).  Greedy aggregation over the matrix graph, piecewise-constant prolongation, Galerkin
+ * coarse operators (nf x nf blocks), one V-cycle per application: the level-0 smoother below
+ * before and after the coarse correction, damped block-Jacobi (omega) on the coarse levels, a
+ * dense direct solve on the coarsest.  Rank-local (block-Jacobi across ranks, like the sweeps).
+ * With PNP_METHOD_CG and smoother SSOR this is CG_AMG_SSOR; it also preconditions BiCGSTAB. */
+typedef struct {
+  int32_t smoother;       /* level-0 smoother: PNP_PREC_SSOR (default), PNP_PREC_ILU0, PNP_PREC_JACOBI */
+  int32_t coarse_target;  /* coarsen until at most this many vertex blocks (1..64, default 64) */
+  int32_t max_levels;     /* levels including the fine one (2..16, default 12) */
+  double omega;           /* damped block-Jacobi weight on the coarse levels (default 0.8) */
+} pnp_amg_opts;
+int pnp_amg_configure(pnp_ctx *ctx, const pnp_amg_opts *opts);
+typedef struct {
+  int32_t levels;         /* including level 0 */
+  int32_t smoother;
+  int32_t rows[16];       /* vertex-block rows per level */
+  int64_t blocks[16];     /* stored blocks per level */
+  double omega;
+} pnp_amg_stats;
+/* valid after the first AMG application on this context */
+int pnp_amg_info(pnp_ctx *ctx, pnp_amg_stats *stats);
+/* aggregate map of level -> level+1 (test hook): level 0 indexed by global vertex (-1: not owned
+ * by this rank, agg sized nv), coarser levels by row */
+int pnp_amg_aggregates(pnp_ctx *ctx, int32_t level, int32_t *agg);
 
 /* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */
 int pnp_linear_solve(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,

@@ -19,6 +19,9 @@ rng = np.random.default_rng(20261015)
 nv = mesh.nv
 x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
                     0.06 * rng.uniform(0.5, 1.5, nv)])
+import hashlib  # noqa: E402
+J = ctx.jacobian(x)
+jh = hashlib.sha1(np.ascontiguousarray(J.data).tobytes()).hexdigest()[:12]
 ctx.state_set(x)
 ctx.assemble_state(5)
 res = []
@@ -37,7 +40,9 @@ for rep in range(5):
     ctx.bicgstab_iterations(10, P.PREC_ILU0)
     ti = ctx.timers(enable=False)
     ilu.append(ti['prec_ms'] / ti['prec_launches'] * 1e3)
-print(f"waves={os.environ.get('PNP_ASM_WAVES', '3')} fanr={os.environ.get('PNP_ASM_FANR', '1')} assemble_us median={np.median(res):.2f} "
+knobs = " ".join(f"{k[4:].lower()}={v}" for k, v in sorted(os.environ.items())
+                 if k.startswith("PNP_") and k != "PNP_AMD_LIB")
+print(f"{knobs or 'default'} jac={jh} assemble_us median={np.median(res):.2f} "
       f"min={np.min(res):.2f}  spmv_us={t['spmv_ms'] / t['spmv_launches'] * 1e3:.2f} "
       f"sgs_apply_us={t['prec_ms'] / t['prec_launches'] * 1e3:.2f} "
       f"ilu_apply_us={np.median(ilu):.2f} "
