@@ -44,14 +44,14 @@ hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, dou
 // work, ainv: (nb*nf)^2 doubles each
 hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
                                      const double *v, double *work, double *ainv, hipStream_t s);
-// x1 == nullptr: no pre-smoothing (level 1 is the coarsest)
-hipError_t launch_amg_restrict0(int nf, int nb1, const int *mptr, const int *mem, const double *d,
-                                const double *t, double *b1, const double *dinv1, double omega,
-                                double *x1, hipStream_t s);
-hipError_t launch_amg_resid_restrict(int nf, int nbn, const int *mptr, const int *mem,
-                                     const int *rp, const int *col, const double *v,
-                                     const double *x, const double *b, double *bn,
-                                     const double *dinvn, double omega, double *xn, hipStream_t s);
+// bn[J] = sum over the members i of aggregate J of (a - sub)_i (sub may be null); xn = omega
+// Dinv_J bn[J] (pre-smoothing from zero; xn null: none)
+hipError_t launch_amg_restrict(int nf, int nbn, const int *mptr, const int *mem, const double *a,
+                               const double *sub, double *bn, const double *dinvn, double omega,
+                               double *xn, hipStream_t s);
+// r = b - A x on a coarse level
+hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const double *v,
+                            const double *x, const double *b, double *r, hipStream_t s);
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s);
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,

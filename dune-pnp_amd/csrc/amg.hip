@@ -250,90 +250,114 @@ __device__ __forceinline__ void bmv_acc(const double *__restrict__ B, const doub
     for (int g = 0; g < NF; g++) y[f] += B[f * NF + g] * x[g];
 }
 
-// coarse row J of level 1: b1 = sum over its members i of (d - A x0)_i (t = A x0);
-// x1 = omega Dinv_J b1 (pre-smoothing from zero) unless level 1 is the coarsest
-template <int NF>
-__global__ __launch_bounds__(kB) void k_restrict0(int nb1, const int *__restrict__ mptr,
-                                                  const int *__restrict__ mem,
-                                                  const double *__restrict__ d,
-                                                  const double *__restrict__ t,
-                                                  double *__restrict__ b1,
-                                                  const double *__restrict__ dinv1, double omega,
-                                                  double *__restrict__ x1) {
-  const int J = blockIdx.x * kB + threadIdx.x;
-  if (J >= nb1) return;
-  double s[NF];
+// The coarse levels are small (68K .. 17 rows at config 3) with ~10-20 blocks per row, so one
+// thread per row leaves a chain of dependent gathers per thread and too few waves to hide it
+// (the first version took 470 us per V-cycle in these kernels).  Here LPR lanes share a row:
+// each takes every LPR-th block / member, and the lanes combine with cross-lane adds.
+constexpr int kLpr = 8;
+
+template <int NF, int LPR>
+__device__ __forceinline__ void lanes_sum(double (&v)[NF]) {
 #pragma unroll
-  for (int f = 0; f < NF; f++) s[f] = 0;
-  for (int m = mptr[J]; m < mptr[J + 1]; m++) {
-    const int i = mem[m];
+  for (int o = LPR / 2; o > 0; o >>= 1)
 #pragma unroll
-    for (int f = 0; f < NF; f++) s[f] += d[size_t(i) * NF + f] - t[size_t(i) * NF + f];
-  }
-  store_nf<NF>(b1, size_t(J), s);
-  if (x1) {
-    double y[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) y[f] = 0;
-    bmv_acc<NF>(dinv1 + size_t(J) * NF * NF, s, y);
-#pragma unroll
-    for (int f = 0; f < NF; f++) y[f] *= omega;
-    store_nf<NF>(x1, size_t(J), y);
-  }
+    for (int f = 0; f < NF; f++) v[f] += __shfl_xor(v[f], o, LPR);
 }
 
-// level l -> l+1: b_{l+1}[J] = sum over members I of (b_l - A_l x_l)_I; pre-smoothing of l+1
-template <int NF>
-__global__ __launch_bounds__(kB) void k_resid_restrict(
-    int nbn, const int *__restrict__ mptr, const int *__restrict__ mem, const int *__restrict__ rp,
-    const int *__restrict__ col, const double *__restrict__ v, const double *__restrict__ x,
-    const double *__restrict__ b, double *__restrict__ bn, const double *__restrict__ dinvn,
-    double omega, double *__restrict__ xn) {
+// r = b - A x on a coarse level (block-CSR)
+template <int NF, int LPR>
+__global__ __launch_bounds__(kB) void k_resid(int nb, const int *__restrict__ rp,
+                                              const int *__restrict__ col,
+                                              const double *__restrict__ v,
+                                              const double *__restrict__ x,
+                                              const double *__restrict__ b,
+                                              double *__restrict__ r) {
   constexpr int NB = NF * NF;
-  const int J = blockIdx.x * kB + threadIdx.x;
-  if (J >= nbn) return;
+  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR, q0 = gt % LPR;
+  const bool live = I < nb;
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0;
+  if (live)
+    for (int q = rp[I] + q0; q < rp[I + 1]; q += LPR) {
+      double xj[NF];
+      load_nf<NF>(x, size_t(col[q]), xj);
+      bmv_acc<NF>(v + size_t(q) * NB, xj, acc);
+    }
+  lanes_sum<NF, LPR>(acc);
+  if (!live || q0 != 0) return;
+  double o[NF];
+  load_nf<NF>(b, size_t(I), o);
+#pragma unroll
+  for (int f = 0; f < NF; f++) o[f] -= acc[f];
+  store_nf<NF>(r, size_t(I), o);
+}
+
+// restriction: bn[J] = sum over the members i of aggregate J of (a - s)_i (s may be null);
+// pre-smoothing of the coarse level from zero: xn = omega Dinv_J bn[J] (xn null: none)
+template <int NF, int LPR>
+__global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict__ mptr,
+                                                 const int *__restrict__ mem,
+                                                 const double *__restrict__ a,
+                                                 const double *__restrict__ sub,
+                                                 double *__restrict__ bn,
+                                                 const double *__restrict__ dinvn, double omega,
+                                                 double *__restrict__ xn) {
+  const int gt = blockIdx.x * kB + threadIdx.x, J = gt / LPR, q0 = gt % LPR;
+  const bool live = J < nbn;
   double s[NF];
 #pragma unroll
   for (int f = 0; f < NF; f++) s[f] = 0;
-  for (int m = mptr[J]; m < mptr[J + 1]; m++) {
-    const int I = mem[m];
-    double ax[NF];
+  if (live)
+    for (int m = mptr[J] + q0; m < mptr[J + 1]; m += LPR) {
+      const int i = mem[m];
+      double ai[NF];
+      load_nf<NF>(a, size_t(i), ai);
+      if (sub) {
+        double si[NF];
+        load_nf<NF>(sub, size_t(i), si);
 #pragma unroll
-    for (int f = 0; f < NF; f++) ax[f] = 0;
-    for (int q = rp[I]; q < rp[I + 1]; q++) {
-      double xj[NF];
-      load_nf<NF>(x, size_t(col[q]), xj);
-      bmv_acc<NF>(v + size_t(q) * NB, xj, ax);
+        for (int f = 0; f < NF; f++) ai[f] -= si[f];
+      }
+#pragma unroll
+      for (int f = 0; f < NF; f++) s[f] += ai[f];
     }
-#pragma unroll
-    for (int f = 0; f < NF; f++) s[f] += b[size_t(I) * NF + f] - ax[f];
-  }
+  lanes_sum<NF, LPR>(s);
+  if (!live || q0 != 0) return;
   store_nf<NF>(bn, size_t(J), s);
   if (xn) {
     double y[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) y[f] = 0;
-    bmv_acc<NF>(dinvn + size_t(J) * NB, s, y);
+    bmv_acc<NF>(dinvn + size_t(J) * NF * NF, s, y);
 #pragma unroll
     for (int f = 0; f < NF; f++) y[f] *= omega;
     store_nf<NF>(xn, size_t(J), y);
   }
 }
 
-// coarsest: x = Ainv b (ainv column-major n x n)
+// coarsest: x = Ainv b (ainv column-major n x n, n <= 3 kAmgMaxCoarse), one workgroup
 __global__ __launch_bounds__(kB) void k_coarse_apply(int n, const double *__restrict__ ainv,
                                                      const double *__restrict__ b,
                                                      double *__restrict__ x) {
-  const int i = blockIdx.x * kB + threadIdx.x;
+  __shared__ double bs[kAmgMaxCoarse * 3];
+  for (int j = threadIdx.x; j < n; j += kB) bs[j] = b[j];
+  __syncthreads();
+  const int i = threadIdx.x;
   if (i >= n) return;
-  double s = 0;
-  for (int j = 0; j < n; j++) s += ainv[size_t(j) * n + i] * b[j];
-  x[i] = s;
+  double s[4] = {0, 0, 0, 0};
+  int j = 0;
+  for (; j + 4 <= n; j += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) s[u] += ainv[size_t(j + u) * n + i] * bs[j + u];
+  }
+  for (; j < n; j++) s[0] += ainv[size_t(j) * n + i] * bs[j];
+  x[i] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // post-smoothing of level l >= 1 with the coarse correction folded in:
 //   xc(j) = x[j] + e[agg[j]],  out[I] = xc(I) + omega Dinv_I (b_I - sum_j A_Ij xc(j))
-template <int NF>
+template <int NF, int LPR>
 __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
                                              const int *__restrict__ col,
                                              const double *__restrict__ v,
@@ -344,26 +368,31 @@ __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
                                              const double *__restrict__ dinv, double omega,
                                              double *__restrict__ out) {
   constexpr int NB = NF * NF;
-  const int I = blockIdx.x * kB + threadIdx.x;
-  if (I >= nb) return;
-  double r[NF], xi[NF];
+  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR, q0 = gt % LPR;
+  const bool live = I < nb;
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0;
+  if (live)
+    for (int q = rp[I] + q0; q < rp[I + 1]; q += LPR) {
+      const int j = col[q];
+      double xj[NF], ej[NF];
+      load_nf<NF>(x, size_t(j), xj);
+      load_nf<NF>(e, size_t(agg[j]), ej);
+#pragma unroll
+      for (int f = 0; f < NF; f++) xj[f] += ej[f];
+      bmv_acc<NF>(v + size_t(q) * NB, xj, acc);
+    }
+  lanes_sum<NF, LPR>(acc);
+  if (!live || q0 != 0) return;
+  double r[NF], xi[NF], ei[NF];
   load_nf<NF>(b, size_t(I), r);
-  for (int q = rp[I]; q < rp[I + 1]; q++) {
-    const int j = col[q];
-    double xj[NF], ej[NF], mx[NF];
-    load_nf<NF>(x, size_t(j), xj);
-    load_nf<NF>(e, size_t(agg[j]), ej);
 #pragma unroll
-    for (int f = 0; f < NF; f++) mx[f] = -(xj[f] + ej[f]);
-    bmv_acc<NF>(v + size_t(q) * NB, mx, r);
-  }
-  {
-    double ei[NF];
-    load_nf<NF>(x, size_t(I), xi);
-    load_nf<NF>(e, size_t(agg[I]), ei);
+  for (int f = 0; f < NF; f++) r[f] -= acc[f];
+  load_nf<NF>(x, size_t(I), xi);
+  load_nf<NF>(e, size_t(agg[I]), ei);
 #pragma unroll
-    for (int f = 0; f < NF; f++) xi[f] += ei[f];
-  }
+  for (int f = 0; f < NF; f++) xi[f] += ei[f];
   double y[NF];
 #pragma unroll
   for (int f = 0; f < NF; f++) y[f] = 0;
@@ -443,34 +472,37 @@ hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *c
   return hipGetLastError();
 }
 
-hipError_t launch_amg_restrict0(int nf, int nb1, const int *mptr, const int *mem, const double *d,
-                                const double *t, double *b1, const double *dinv1, double omega,
-                                double *x1, hipStream_t s) {
-  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_restrict0<NFc>), g1(nb1), dim3(kB), 0, s, nb1, mptr,
-                                          mem, d, t, b1, dinv1, omega, x1));
+hipError_t launch_amg_restrict(int nf, int nbn, const int *mptr, const int *mem, const double *a,
+                               const double *sub, double *bn, const double *dinvn, double omega,
+                               double *xn, hipStream_t s) {
+  if (nbn == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_restrict<NFc, kLpr>), g1((long long)nbn * kLpr),
+                                         dim3(kB), 0, s, nbn, mptr, mem, a, sub, bn, dinvn, omega,
+                                         xn));
   return hipGetLastError();
 }
 
-hipError_t launch_amg_resid_restrict(int nf, int nbn, const int *mptr, const int *mem,
-                                     const int *rp, const int *col, const double *v,
-                                     const double *x, const double *b, double *bn,
-                                     const double *dinvn, double omega, double *xn, hipStream_t s) {
-  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid_restrict<NFc>), g1(nbn), dim3(kB), 0, s, nbn,
-                                          mptr, mem, rp, col, v, x, b, bn, dinvn, omega, xn));
+hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const double *v,
+                            const double *x, const double *b, double *r, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid<NFc, kLpr>), g1((long long)nb * kLpr), dim3(kB),
+                                         0, s, nb, rp, col, v, x, b, r));
   return hipGetLastError();
 }
 
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s) {
-  hipLaunchKernelGGL(k_coarse_apply, g1(n), dim3(kB), 0, s, n, ainv, b, x);
+  if (n > kB || n > kAmgMaxCoarse * 3) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_coarse_apply, dim3(1), dim3(kB), 0, s, n, ainv, b, x);
   return hipGetLastError();
 }
 
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
                            const int *agg, const double *x, const double *e, const double *b,
                            const double *dinv, double omega, double *out, hipStream_t s) {
-  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc>), g1(nb), dim3(kB), 0, s, nb, rp, col, v,
-                                          agg, x, e, b, dinv, omega, out));
+  if (nb == 0) return hipSuccess;
+  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr>), g1((long long)nb * kLpr), dim3(kB),
+                                         0, s, nb, rp, col, v, agg, x, e, b, dinv, omega, out));
   return hipGetLastError();
 }
 

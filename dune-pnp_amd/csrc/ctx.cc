@@ -525,14 +525,16 @@ struct pnp_ctx {
     e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 0, nullptr, partials.p, &nsp,
                          stream);
     if (e == hipSuccess)
-      e = pnp::launch_amg_restrict0(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, d,
-                                    amg_t.p, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
-                                    K > 1 ? amg_d[0]->x.p : nullptr, stream);
+      e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, d,
+                                   amg_t.p, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
+                                   K > 1 ? amg_d[0]->x.p : nullptr, stream);
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
-      e = pnp::launch_amg_resid_restrict(nf, N.nb, N.mptr.p, N.mem.p, C.rp.p, C.col.p, C.v.p,
-                                         C.x.p, C.b.p, N.b.p, N.dinv.p, om,
-                                         k + 2 < K ? N.x.p : nullptr, stream);
+      // residual of level k+1 into its x2 (free until its post-smoothing), then restriction
+      e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.x.p, C.b.p, C.x2.p, stream);
+      if (e == hipSuccess)
+        e = pnp::launch_amg_restrict(nf, N.nb, N.mptr.p, N.mem.p, C.x2.p, nullptr, N.b.p,
+                                     N.dinv.p, om, k + 2 < K ? N.x.p : nullptr, stream);
     }
     if (e == hipSuccess)
       e = pnp::launch_amg_coarse_apply(amg_d[K - 1]->nb * nf, amg_ainv.p, amg_d[K - 1]->b.p,
