@@ -207,3 +207,34 @@ def test_ion_flux_partitioned(nranks):
     for ip, im in outs:
         assert np.max(np.abs(ip - ipo)) <= 1e-12 * scale
         assert np.max(np.abs(im - imo)) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("nranks,kind", [(2, "pnp"), (3, "pb")])
+def test_amg_solve_partitioned(nranks, kind):
+    """PNP_PREC_AMG across ranks: each rank's hierarchy covers its owned rows (block-Jacobi of
+    AMGs, like the sweeps); the outer Krylov solve is global and reaches the reduction."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["newton_pnp_x0"] if kind == "pnp" else np.zeros(mesh.nv)
+    op = P.OP_PNP if kind == "pnp" else P.OP_PB
+    method = P.METHOD_BICGSTAB if kind == "pnp" else P.METHOD_CG
+
+    def fn(ctx, r):
+        ctx.set_operator(op)
+        if kind == "pnp":
+            ctx.amg_configure(smoother=P.PREC_ILU0, coarse_target=8)
+        else:
+            ctx.amg_configure(smoother=P.PREC_SSOR, coarse_target=8)
+        J = ctx.jacobian(x)
+        rhs = ctx.sync_vector(ctx.residual(x))
+        sol, res = ctx.linear_solve(rhs, prec=P.PREC_AMG, reduction=1e-8, maxit=5000,
+                                    method=method)
+        return ctx.sync_vector(sol), res, J, rhs, ctx.amg_info()
+    outs = run_ranks(nranks, mesh, par, fn)
+    J = sum(o[2] for o in outs)
+    rhs = outs[0][3]
+    for sol, res, _, _, info in outs:
+        assert res["converged"] == 1, res
+        assert np.linalg.norm(J @ sol - rhs) <= 1.001e-8 * np.linalg.norm(rhs)
+        assert info["levels"] >= 2
+    assert len({o[1]["iterations"] for o in outs}) == 1
+    assert sum(o[4]["rows"][0] for o in outs) == mesh.nv
