@@ -8,7 +8,7 @@
 //
 // usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb] [--steps n]
 //                 [--prec none|ssor|jacobi|ilu0] [--pb-prec ...] [--device d] [--out prefix]
-//                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi]
+//                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
 #include <algorithm>
@@ -39,7 +39,7 @@ static void usage() {
       "usage: pnp_main <config.cfg> [--refine k] [--mesh-scale s] [--mode stationary|instationary|md|pb]\n"
       "                [--steps n] [--prec none|ssor|jacobi|ilu0] [--pb-prec p] [--device d]\n"
       "                [--out prefix] [--md-reduction r]\n"
-      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi]\n");
+      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -296,6 +296,7 @@ int main(int argc, char **argv) {
       if (linsolver == "bcgs_noprec") lprec = PNP_PREC_NONE;
       else if (linsolver == "cg_noprec") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_NONE;
       else if (linsolver == "cg_jacobi") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_JACOBI;
+      else if (linsolver == "cg_amg_ssor") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_AMG;
       else if (linsolver != "bcgs_ssork")
         throw pnp_gpu::Error(PNP_E_ARG, "unknown --linear-solver " + linsolver);
       md_loop(ctx, s, u, nv, rank, steps, md_reduction, lprec, lmethod, out);
