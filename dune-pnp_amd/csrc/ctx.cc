@@ -630,16 +630,39 @@ struct pnp_ctx {
     if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
     if (prec == PNP_PREC_AMG && (rc = amg_setup())) return rc;
-    int nsp = 0;
+    int nsp = 0, npu = 0;
+    // ILU(0): the two vector updates that feed the preconditioner also do colour 0 of its
+    // forward sweep (launch_update_fwd0); PNP_FUSE=0 keeps them apart (A/B)
+    static const bool fuse_env = [] {
+      const char *ev = std::getenv("PNP_FUSE");
+      return !(ev && std::atoi(ev) == 0);
+    }();
+    const bool fuse = fuse_env && prec == PNP_PREC_ILU0 && L.color_ptr.size() > 2;
+    const int c0_end = L.color_ptr.size() > 1 ? L.color_ptr[1] : 0;
+    auto ilu_from1 = [&](const double *d, double *out) -> int {
+      hipEvent_t tp = tb(T_PREC);
+      hipError_t ee = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p,
+                                             d, out, stream, 1);
+      if (ee != hipSuccess) return hipfail(ee, "preconditioner");
+      te(T_PREC, tp);
+      return PNP_OK;
+    };
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
       t0 = tb(T_BLAS);
-      e = pnp::launch_update_p(n, S.p, rs.p, v.p, p.p, k == 0 ? 1 : 0, stream);
+      if (fuse)
+        e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 0, k == 0 ? 1 : 0, nullptr, nullptr,
+                                    rs.p, v.p, p.p, uvals.p, y.p, nullptr, nullptr, stream);
+      else
+        e = pnp::launch_update_p(n, S.p, rs.p, v.p, p.p, k == 0 ? 1 : 0, stream);
       if (e != hipSuccess) return hipfail(e, "update_p");
       te(T_BLAS, t0);
       // y = M^{-1} p ; v = A y ; h = <rt, v>
       const double *yin = p.p;
-      if (prec != PNP_PREC_NONE) {
+      if (fuse) {
+        if ((rc = ilu_from1(p.p, y.p))) return rc;
+        yin = y.p;
+      } else if (prec != PNP_PREC_NONE) {
         if ((rc = precond(prec, p.p, y.p))) return rc;
         yin = y.p;
       }
@@ -653,12 +676,19 @@ struct pnp_ctx {
       // with omega below -- one reduction and one allreduce fewer per iteration; the second
       // half's kernels ignore a converged first half, update_xr skips on S->done)
       t0 = tb(T_BLAS);
-      e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials2.p, stream);
+      if (fuse)
+        e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, zout, yin, rs.p, v.p, nullptr,
+                                    uvals.p, y.p, partials2.p, &npu, stream);
+      else
+        e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials2.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (1)");
       te(T_BLAS, t0);
       // y = M^{-1} r ; t = A y ; <t,r>, <t,t>
       const double *yin2 = rs.p;
-      if (prec != PNP_PREC_NONE) {
+      if (fuse) {
+        if ((rc = ilu_from1(rs.p, y.p))) return rc;
+        yin2 = y.p;
+      } else if (prec != PNP_PREC_NONE) {
         if ((rc = precond(prec, rs.p, y.p))) return rc;
         yin2 = y.p;
       }
@@ -667,7 +697,7 @@ struct pnp_ctx {
       e = pnp::launch_spmv(dl, nf, pat, vals.p, yin2, t.p, 2, rs.p, partials.p, &nsp, stream);
       if (e != hipSuccess) return hipfail(e, "spmv t");
       te(T_SPMV, t0);
-      if ((rc = reduce_derive2(nsp, 2, np, 1, 23))) return rc;
+      if ((rc = reduce_derive2(nsp, 2, fuse ? npu : np, 1, 23))) return rc;
       // x += omega y ; r -= omega t ; ||r||, <rt, r>
       t0 = tb(T_BLAS);
       e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
@@ -1175,7 +1205,10 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
                2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
                                     size_t(pnp::spmv_parts(L.n_owned))) + 64,
                "partials")) ||
-      (rc = al(c->partials2, size_t(pnp::blas_nparts(3LL * nloc)) + 64, "partials2")) ||
+      (rc = al(c->partials2,
+               std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
+                                size_t(pnp::spmv_parts(L.n_owned))) + 64,
+               "partials2")) ||
       (rc = al(c->S, 2, "scalars")) ||
       (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
       (rc = al(c->cvec, 3 * size_t(L.n_owned), "cvec")) || (rc = al(c->aux0, nloc, "aux0")) ||

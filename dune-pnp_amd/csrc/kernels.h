@@ -289,9 +289,17 @@ hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals
 // factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)
 hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                               double *lu, hipStream_t s);
+// c_first = 1: colour 0's forward step was already applied (launch_update_fwd0)
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                              const double *lv, const double *uv, const double *d, double *v,
-                             hipStream_t s);
+                             hipStream_t s, int c_first = 0);
+// BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
+// p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
+// r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0
+hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
+                              int which, int first, double *x, const double *yin, double *r,
+                              const double *v, double *p, const double *uv, double *yout,
+                              double *partials, int *nparts, hipStream_t s);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);

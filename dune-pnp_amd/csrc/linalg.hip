@@ -580,6 +580,69 @@ __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars
   }
 }
 
+// BiCGSTAB vector updates fused with colour 0 of the ILU(0) forward sweep that consumes them.
+// Colour-0 rows come first in the colour-major order, so they have no lower neighbours: their
+// forward step is y_i = Ld_i^-1 d_i, pointwise.  The update that produces d (WHICH 0: p = r +
+// beta (p - omega v); WHICH 1: x += alpha y, s = r - alpha v with the ||s||^2 partials) applies it
+// in the same pass, one row per thread, and the sweep starts at colour 1: one launch and one
+// re-read of d fewer per preconditioner application.  yin may alias yout (x += alpha y reads a
+// row's y before the row's new y is written, by the same thread).
+template <int NF, int PAT, int WHICH>
+__global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
+                                                        const Scalars *__restrict__ S, int first,
+                                                        double *__restrict__ x, const double *yin,
+                                                        double *__restrict__ r,
+                                                        const double *__restrict__ v,
+                                                        double *__restrict__ p,
+                                                        const double *__restrict__ uv,
+                                                        double *yout,
+                                                        double *__restrict__ partials) {
+  constexpr int NV = popc9(PAT);
+  if (S->done) return;  // uniform over the grid
+  const int row = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = row < L.n_owned;
+  double ss = 0;
+  if (live) {
+    double d[NF], vv[NF];
+    load_nf<NF>(r, size_t(row), d);
+    load_nf<NF>(v, size_t(row), vv);
+    if (WHICH == 0) {
+      const double beta = first ? 0.0 : (S->rho_new / S->rho) * (S->alpha / S->omega);
+      const double om = S->omega;
+      if (!first) {
+        double po[NF];
+        load_nf<NF>(p, size_t(row), po);
+#pragma unroll
+        for (int f = 0; f < NF; f++) d[f] = beta * (po[f] - om * vv[f]) + d[f];
+      }
+      store_nf<NF>(p, size_t(row), d);
+    } else {
+      const double a = S->alpha;
+      double xi[NF], yi[NF];
+      load_nf<NF>(x, size_t(row), xi);
+      load_nf<NF>(yin, size_t(row), yi);
+#pragma unroll
+      for (int f = 0; f < NF; f++) {
+        xi[f] += a * yi[f];
+        d[f] -= a * vv[f];
+        ss += d[f] * d[f];
+      }
+      store_nf<NF>(x, size_t(row), xi);
+      store_nf<NF>(r, size_t(row), d);
+    }
+    if (row < c0_end) {
+      double Dg[NV];
+      load_vals<NV>(uv + size_t(L.uchunk_off[row / kRows]) * NV, row % kRows, Dg);
+      diag_lower_solve<NF, PAT>(Dg, d);
+      store_nf<NF>(yout, size_t(row), d);
+    }
+  }
+  if (WHICH == 1) {
+    double a1[1] = {ss};
+    block_sum<1>(a1, partials + blockIdx.x);
+  }
+}
+
 template <int TWO>
 __global__ __launch_bounds__(kBlock) void k_dot(long long n, const double *__restrict__ a,
                                                 const double *__restrict__ b,
@@ -962,7 +1025,8 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
 }
 
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
-                             const double *uv, const double *d, double *v, hipStream_t s) {
+                             const double *uv, const double *d, double *v, hipStream_t s,
+                             int c_first) {
   if (L.n_owned == 0) return hipSuccess;
   const int nc = L.ncolors;
   PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
@@ -973,11 +1037,30 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
                            rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
                            d, v);
     };
-    // the last colour's backward step runs in its forward launch (kIluLast)
-    for (int c = 0; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
+    // the last colour's backward step runs in its forward launch (kIluLast); c_first = 1: colour
+    // 0's forward step was done by launch_update_fwd0
+    for (int c = c_first; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
     go(std::integral_constant<int, kIluLast>(), nc - 1);
     for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
   }));
+  return hipGetLastError();
+}
+
+hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
+                              int which, int first, double *x, const double *yin, double *r,
+                              const double *v, double *p, const double *uv, double *yout,
+                              double *partials, int *nparts, hipStream_t s) {
+  const dim3 g = rows_grid(L.n_owned);
+  if (nparts) *nparts = int(g.x);
+  if (L.n_owned == 0) return hipSuccess;
+  PNP_PAT_DISPATCH(nf, pat, {
+    if (which == 0)
+      hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, c0_end, S, first,
+                         x, yin, r, v, p, uv, yout, partials);
+    else
+      hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, c0_end, S, first,
+                         x, yin, r, v, p, uv, yout, partials);
+  });
   return hipGetLastError();
 }
 

@@ -34,16 +34,17 @@ ctx.timers(enable=True, reset=True)
 ctx.bicgstab_iterations(20, P.PREC_SSOR)
 t = ctx.timers(enable=False)
 ctx.bicgstab_iterations(2, P.PREC_ILU0)  # factorise
-ilu = []
+ilu, iltot = [], []
 for rep in range(5):
     ctx.timers(enable=True, reset=True)
     ctx.bicgstab_iterations(10, P.PREC_ILU0)
     ti = ctx.timers(enable=False)
     ilu.append(ti['prec_ms'] / ti['prec_launches'] * 1e3)
+    iltot.append((ti['prec_ms'] + ti['spmv_ms'] + ti['blas_ms']) / 10 * 1e3)
 knobs = " ".join(f"{k[4:].lower()}={v}" for k, v in sorted(os.environ.items())
                  if k.startswith("PNP_") and k != "PNP_AMD_LIB")
 print(f"{knobs or 'default'} jac={jh} assemble_us median={np.median(res):.2f} "
       f"min={np.min(res):.2f}  spmv_us={t['spmv_ms'] / t['spmv_launches'] * 1e3:.2f} "
       f"sgs_apply_us={t['prec_ms'] / t['prec_launches'] * 1e3:.2f} "
-      f"ilu_apply_us={np.median(ilu):.2f} "
+      f"ilu_apply_us={np.median(ilu):.2f} ilu_bicgstab_us_per_it={np.median(iltot):.1f} "
       f"blas_ms_per_it={t['blas_ms'] / 20:.4f}")
