@@ -615,6 +615,9 @@ struct pnp_ctx {
     pnp::Scalars &init = hS[2];  // pinned staging slot
     std::memset(&init, 0, sizeof init);
     init.reduction = fixed > 0 ? 0.0 : o.reduction;
+    // divergence guard for the AMG preconditioner only (a non-symmetric V-cycle can make
+    // BiCGSTAB diverge; ISTL semantics otherwise: run to maxit)
+    init.divguard = (o.prec == PNP_PREC_AMG && fixed <= 0) ? 1 : 0;
     e = hipMemcpyAsync(S.p, &init, sizeof init, hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return hipfail(e, "bicgstab scalars");
     hipEvent_t t0 = tb(T_BLAS);
@@ -1615,8 +1618,19 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
     pnp_solve_result sr{};
     double ts = now_s();
     if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
-    res->solve_seconds += now_s() - ts;
     res->linear_iterations += sr.iterations;
+    if (lo.prec == PNP_PREC_AMG && (sr.breakdown || !sr.converged)) {
+      // AMG fallback: the V-cycle of a non-symmetric system can fail where its level-0
+      // smoother alone converges (a far-from-converged state); redo this step's solve with the
+      // smoother as the preconditioner
+      lo.prec = c->amg_opts.smoother;
+      CK(hipMemcpyAsync(c->b.p, c->r.p, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream),
+         "rhs");
+      if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
+      res->linear_iterations += sr.iterations;
+      res->linear_fallbacks++;
+    }
+    res->solve_seconds += now_s() - ts;
     if (sr.breakdown) {
       res->status = PNP_E_BREAKDOWN;
       break;

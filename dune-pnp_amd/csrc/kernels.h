@@ -251,7 +251,7 @@ struct Scalars {
   int done;              // 0 running, 1 converged, 2 breakdown
   int breakdown;         // 1 rho, 2 omega, 3 h
   int iter;              // full iterations started
-  int pad;
+  int divguard;          // 1: stop with breakdown 4 once ||r|| > 1e10 ||r0|| (AMG solves)
 };
 
 // ---- launchers (return hipError_t of the launch) ----------------------------------------------

@@ -781,6 +781,9 @@ __device__ void derive(Scalars *S, int stage) {
     S->rho_new = S->red[1];
     if (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) {
       S->done = 1;
+    } else if (S->divguard && !(S->norm <= 1e10 * S->norm0)) {  // diverged (or not finite)
+      S->done = 2;
+      S->breakdown = 4;
     } else if (fabs(S->rho) <= kEps) {
       S->done = 2;
       S->breakdown = 1;

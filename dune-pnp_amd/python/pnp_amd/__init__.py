@@ -127,7 +127,8 @@ class _NewtonResult(C.Structure):
     _fields_ = [("converged", C.c_int32), ("iterations", C.c_int32),
                 ("linear_iterations", C.c_int32), ("status", C.c_int32),
                 ("first_defect", C.c_double), ("defect", C.c_double), ("elapsed", C.c_double),
-                ("assemble_seconds", C.c_double), ("solve_seconds", C.c_double)]
+                ("assemble_seconds", C.c_double), ("solve_seconds", C.c_double),
+                ("linear_fallbacks", C.c_int32)]
 
 
 class _Timers(C.Structure):

@@ -206,7 +206,8 @@ typedef struct {
                          src/instationary_pnp_from_pb_md.hh:198-206) */
 } pnp_solve_opts;
 typedef struct {
-  int32_t converged, iterations, breakdown; /* iterations = ceil(half-step counter) */
+  int32_t converged, iterations, breakdown; /* iterations = ceil(half-step counter); breakdown:
+      1 rho, 2 omega, 3 h (ISTL's 1e-80 tests), 4 diverged (PNP_PREC_AMG only) */
   double it_half, defect0, defect, reduction, elapsed;
 } pnp_solve_result;
 
@@ -260,6 +261,9 @@ typedef struct {
       PNP_E_NOT_CONVERGED (NewtonNotConverged / NewtonLinearSolverError / line search),
       PNP_E_BREAKDOWN */
   double first_defect, defect, elapsed, assemble_seconds, solve_seconds;
+  int32_t linear_fallbacks; /* PNP_PREC_AMG only: Newton steps whose AMG-preconditioned solve
+      failed (diverged: ||r|| > 1e10 ||r0||, breakdown or maxit) and were re-solved with the
+      AMG's level-0 smoother alone; linear_iterations counts both solves */
 } pnp_newton_result;
 int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
 

@@ -21,6 +21,15 @@ sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
 import pnp_amd as P  # noqa: E402
 
 DATA = os.path.join(ROOT, "data")
+# preconditioner of the PNP Newton solves (configs 2, 4, 5): ilu0 (default) or amg (PNP_PREC_AMG
+# with the ILU(0) smoother, coarse omega 1)
+PNP_PREC = P.PREC_BY_NAME[os.environ.get("PNP_BENCH_PREC", "ilu0")]
+
+
+def pnp_prec(ctx):
+    if PNP_PREC == P.PREC_AMG:
+        ctx.amg_configure(smoother=P.PREC_ILU0, omega=1.0)
+    return PNP_PREC
 
 
 def rates(ctx, nasm=10, nit=20, prec=P.PREC_ILU0):
@@ -66,7 +75,7 @@ def config2():
     x0 = ctx.initial_state(phi)
     ctx.set_operator(P.OP_PNP)
     t0 = time.perf_counter()
-    u, res = ctx.newton(x0, reduction=1e-8, prec=P.PREC_ILU0)
+    u, res = ctx.newton(x0, reduction=1e-8, prec=pnp_prec(ctx))
     tn = time.perf_counter() - t0
     ctx.state_set(x0)
     r = rates(ctx)
@@ -90,7 +99,7 @@ def config4(nsteps=100):
         ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=dt, x_old=u)
         # abs_limit 1e-9: from step 1 on the first defect is ~1e-2 and the residual's rounding
         # floor ~2e-10, so reduction 1e-8 alone (with PDELab's 1e-12 absolute limit) stalls
-        u, res = ctx.newton(u, reduction=1e-8, abs_limit=1e-9, prec=P.PREC_ILU0)
+        u, res = ctx.newton(u, reduction=1e-8, abs_limit=1e-9, prec=pnp_prec(ctx))
         if not res["converged"]:
             return {"config": 4, "failed_step": i, "result": res}
         lin += res["linear_iterations"]
@@ -123,7 +132,7 @@ def config5():
     r = rates(ctx)
     n = 3 * mesh.nv
     t0 = time.perf_counter()
-    u, res = ctx.newton(x0, prec=P.PREC_ILU0, reduction=cfg.system["newtonReduction"],
+    u, res = ctx.newton(x0, prec=pnp_prec(ctx), reduction=cfg.system["newtonReduction"],
                         min_linear_reduction=cfg.system["newtonMinLinearReduction"])
     t_pnp = time.perf_counter() - t0
     return {"config": "5 (pore_without_dna.geo meshed natively, scale 0.85, k=6, one GPU)",
@@ -154,4 +163,5 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["1", "2", "4", "5"]
     for w in which:
         out = {"1": config1, "2": config2, "4": config4, "5": config5, "5f": config5_fallback}[w]()
+        out["pnp_preconditioner"] = os.environ.get("PNP_BENCH_PREC", "ilu0")
         print(json.dumps(out), flush=True)
