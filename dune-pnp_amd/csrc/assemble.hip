@@ -231,6 +231,8 @@ __device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, i
 // loads and stores in issue order: an index load issued behind an element's SELL block stores
 // could not be consumed before those stores drained (the FANR = 0 path waits vmcnt(0) per
 // element).
+// (Non-temporal loads of the once-read row streams -- fan metadata, column indices, constant
+// load, mask -- and a non-temporal residual store: 77 -> 96 us, profiles/r01/ab_asm_nt_row_streams.log)
 template <int OP, int JAC, int MINW, int FANR>
 __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
@@ -363,8 +365,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   }
 #pragma unroll
   for (int f = 0; f < NF; f++) {
-    double rv = R[f] + a.cvec[size_t(row) * NF + f];
-    a.r[size_t(row) * NF + f] = a.dmask[size_t(row) * NF + f] != 0 ? 0.0 : rv;
+    const size_t q = size_t(row) * NF + f;
+    const double rv = R[f] + a.cvec[q];
+    a.r[q] = a.dmask[q] != 0 ? 0.0 : rv;
   }
 }
 

@@ -76,19 +76,31 @@ def numpy_vcycle(A0, nf, aggs, omega, d):
     return y + (d - A0 @ y) / diag0
 
 
-@pytest.mark.parametrize("kind", ["pb", "pnp"])
+@pytest.mark.parametrize("kind", ["pb", "pnp", "pnp_ie", "diff", "poisson"])
 def test_amg_vcycle_matches_numpy_restatement(kind):
     mesh, par = problem("cylinder_config.cfg", 2)
     nv = mesh.nv
     ctx = P.Context(mesh, par)
     rng = np.random.default_rng(7)
+
+    def state3():
+        return np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                               0.06 * rng.uniform(0.5, 1.5, nv)])
+    nf = 3 if kind.startswith("pnp") else 1
     if kind == "pnp":
-        nf = 3
         ctx.set_operator(P.OP_PNP)
-        x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
-                            0.06 * rng.uniform(0.5, 1.5, nv)])
+        x = state3()
+    elif kind == "pnp_ie":
+        ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=0.5, x_old=state3())
+        x = state3()
+    elif kind == "diff":
+        ctx.set_operator(P.OP_DIFF, z=-1.0, field=2, phi=rng.uniform(-1, 1, nv))
+        x = 0.06 * rng.uniform(0.5, 1.5, nv)
+    elif kind == "poisson":
+        ctx.set_operator(P.OP_POISSON, cp=0.06 * rng.uniform(0.5, 1.5, nv),
+                         cm=0.06 * rng.uniform(0.5, 1.5, nv))
+        x = rng.uniform(-1, 1, nv)
     else:
-        nf = 1
         ctx.set_operator(P.OP_PB)
         x = rng.uniform(-1, 1, nv)
     J = ctx.jacobian(x)
@@ -160,4 +172,5 @@ def test_amg_newton_pnp_matches_ilu0_newton():
     ua, ra = ctx.newton(x0, prec=P.PREC_AMG, reduction=1e-10)
     ui, ri = ctx.newton(x0, prec=P.PREC_ILU0, reduction=1e-10)
     assert ra["converged"] == 1 and ri["converged"] == 1
+    assert ra["linear_fallbacks"] == 0 and ri["linear_fallbacks"] == 0
     assert np.max(np.abs(ua - ui)) <= 1e-6 * np.max(np.abs(ui))
