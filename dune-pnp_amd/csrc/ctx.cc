@@ -129,7 +129,7 @@ struct pnp_ctx {
 
   // aggregation AMG (PNP_PREC_AMG, amg.h): the pattern hierarchy is built once per context (it
   // depends on the layout only), the coarse values after every assembly
-  pnp_amg_opts amg_opts{PNP_PREC_SSOR, pnp::kAmgMaxCoarse, 12, 0.8};
+  pnp_amg_opts amg_opts{PNP_PREC_SSOR, pnp::kAmgMaxCoarse, 12, 0.8, 2};
   std::vector<pnp::AmgLevelHost> amg_h;
   struct AmgDev {
     int nb = 0;
@@ -141,7 +141,8 @@ struct pnp_ctx {
   bool amg_built = false, amg_valid = false;
   int amg_nf = 0;
   double amg_setup_ms = 0;
-  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
+  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z, amg_zero;
+
 
   // vectors (sized n_local * 3)
   DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials, partials2;
@@ -482,7 +483,8 @@ struct pnp_ctx {
       if ((e = amg_work.alloc(nc * nc)) != hipSuccess || (e = amg_ainv.alloc(nc * nc)) != hipSuccess ||
           (e = amg_x0.alloc(nl)) != hipSuccess || (e = amg_t.alloc(nl)) != hipSuccess ||
           (e = amg_y.alloc(nl)) != hipSuccess || (e = amg_r.alloc(nl)) != hipSuccess ||
-          (e = amg_z.alloc(nl)) != hipSuccess)
+          (e = amg_z.alloc(nl)) != hipSuccess ||
+          (e = amg_zero.alloc(size_t(amg_d[0]->nb) * nf)) != hipSuccess)
         return hipfail(e, "amg vectors");
       amg_nf = nf;
       amg_valid = false;
@@ -520,16 +522,21 @@ struct pnp_ctx {
     const long long nn = nown();
     int rc, nsp = 0;
     hipError_t e;
-    // level 0 pre-smoothing from zero, residual, restriction (+ level-1 pre-smoothing)
+    // level 0 pre-smoothing from zero, residual (SpMV residual mode), restriction (+ level-1
+    // pre-smoothing)
     if ((rc = smoother(sm, d, amg_x0.p))) return rc;
-    e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 0, nullptr, partials.p, &nsp,
-                         stream);
+    e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 3, d, partials.p, &nsp, stream);
     if (e == hipSuccess)
-      e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, d,
-                                   amg_t.p, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
+      e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, amg_t.p,
+                                   nullptr, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
                                    K > 1 ? amg_d[0]->x.p : nullptr, stream);
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
+      for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more pre-smoothing
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, N.agg.p, C.x.p, amg_zero.p,
+                                 C.b.p, C.dinv.p, om, C.x2.p, stream);
+        std::swap(C.x.p, C.x2.p);
+      }
       // residual of level k+1 into its x2 (free until its post-smoothing), then restriction
       e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.x.p, C.b.p, C.x2.p, stream);
       if (e == hipSuccess)
@@ -545,14 +552,23 @@ struct pnp_ctx {
       e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, amg_d[k + 1]->agg.p, C.x.p, res,
                                C.b.p, C.dinv.p, om, C.x2.p, stream);
       res = C.x2.p;
+      for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more post-smoothing
+        double *out = res == C.x2.p ? C.x.p : C.x2.p;
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, amg_d[k + 1]->agg.p, res,
+                                 amg_zero.p, C.b.p, C.dinv.p, om, out, stream);
+        res = out;
+      }
     }
     // level 0: prolongation, post-smoothing x += M^{-1} (d - A x)
     if (e == hipSuccess) e = pnp::launch_amg_prolong0(nf, n, amg_d[0]->agg.p, amg_x0.p, res, amg_y.p, stream);
     if (e == hipSuccess)
-      e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_y.p, amg_t.p, 0, nullptr, partials.p, &nsp,
-                           stream);
-    if (e == hipSuccess) e = pnp::launch_axpby(nn, 1.0, d, -1.0, amg_t.p, amg_r.p, stream);
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_y.p, amg_r.p, 3, d, partials.p, &nsp, stream);
     if (e != hipSuccess) return hipfail(e, "amg v-cycle");
+    if (sm == PNP_PREC_ILU0) {  // vout = y + M^-1 r, written by the backward sweep
+      e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, amg_r.p,
+                                 amg_z.p, stream, 0, amg_y.p, vout);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "amg v-cycle");
+    }
     if ((rc = smoother(sm, amg_r.p, amg_z.p))) return rc;
     e = pnp::launch_axpby(nn, 1.0, amg_y.p, 1.0, amg_z.p, vout, stream);
     return e == hipSuccess ? PNP_OK : hipfail(e, "amg v-cycle");
@@ -1492,7 +1508,8 @@ extern "C" int pnp_amg_configure(pnp_ctx *c, const pnp_amg_opts *o) {
   if (o->smoother != PNP_PREC_SSOR && o->smoother != PNP_PREC_ILU0 && o->smoother != PNP_PREC_JACOBI)
     return c->fail(PNP_E_ARG, "AMG smoother must be SSOR, ILU0 or JACOBI");
   if (o->coarse_target < 1 || o->coarse_target > pnp::kAmgMaxCoarse || o->max_levels < 2 ||
-      o->max_levels > pnp::kAmgMaxLevels || !(o->omega > 0 && o->omega <= 2))
+      o->max_levels > pnp::kAmgMaxLevels || !(o->omega > 0 && o->omega <= 2) ||
+      o->coarse_sweeps < 1 || o->coarse_sweeps > 8)
     return c->fail(PNP_E_ARG, "AMG options out of range");
   const bool rebuild = o->coarse_target != c->amg_opts.coarse_target ||
                        o->max_levels != c->amg_opts.max_levels;

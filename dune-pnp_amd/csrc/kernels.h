@@ -263,7 +263,7 @@ hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi
                              const double *x_old, double *cvec, hipStream_t s);
 
 // y = A x over owned rows; optional fused dots: out partials[block*k + j]
-//   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2)
+//   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2); 3: y = w - A x (no dots)
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
                        hipStream_t s);
@@ -289,10 +289,12 @@ hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals
 // factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)
 hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                               double *lu, hipStream_t s);
-// c_first = 1: colour 0's forward step was already applied (launch_update_fwd0)
+// c_first = 1: colour 0's forward step was already applied (launch_update_fwd0); add != null:
+// also out = add + v (written row by row as the backward sweep finishes them)
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                              const double *lv, const double *uv, const double *d, double *v,
-                             hipStream_t s, int c_first = 0);
+                             hipStream_t s, int c_first = 0, const double *add = nullptr,
+                             double *out = nullptr);
 // BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
 // p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
 // r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0

@@ -133,8 +133,14 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
       for (int f = 0; f < NF; f++)
         if ((dm >> f) & 1) acc[f] = xr[f];
     }
+    if constexpr (MODE == 3) {  // residual: y = w - A x
+      double wr[NF];
+      load_nf<NF>(w, size_t(row), wr);
+#pragma unroll
+      for (int f = 0; f < NF; f++) acc[f] = wr[f] - acc[f];
+    }
     store_nf<NF>(y, size_t(row), acc);
-    if constexpr (MODE >= 1) {
+    if constexpr (MODE == 1 || MODE == 2) {
       double wr[NF];
       load_nf<NF>(w, size_t(row), wr);
 #pragma unroll
@@ -438,12 +444,16 @@ __device__ __forceinline__ void diag_upper_solve(const double (&Dg)[NV], double 
 // 24 V pore case, measured -- DESIGN.md §4.)
 enum { kIluFwd = 0, kIluBwd = 1, kIluLast = 2 };
 
-template <int NF, int PAT, int KIND, int LPR, int B, int NT>
+// ADD = 1 (backward / last-colour launches): also out_i = add_i + v_i for the finished rows (the
+// AMG's post-smoothing update y + M^-1 r without a separate pass)
+template <int NF, int PAT, int KIND, int LPR, int B, int NT, int ADD = 0>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
                                                        const double *__restrict__ lv,
                                                        const double *__restrict__ uv,
                                                        const double *__restrict__ d,
-                                                       double *__restrict__ v) {
+                                                       double *__restrict__ v,
+                                                       const double *__restrict__ add = nullptr,
+                                                       double *__restrict__ out = nullptr) {
   constexpr int NV = popc9(PAT);
   constexpr bool FWD = KIND != kIluBwd;
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
@@ -463,6 +473,13 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
   if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
   store_nf<NF>(v, size_t(row), acc);
+  if constexpr (ADD && KIND != kIluFwd) {
+    double ad[NF];
+    load_nf<NF>(add, size_t(row), ad);
+#pragma unroll
+    for (int f = 0; f < NF; f++) ad[f] += acc[f];
+    store_nf<NF>(out, size_t(row), ad);
+  }
 }
 
 // split storage position p takes the block (row, slot) = (src >> 6, src & 63) of the full SELL:
@@ -929,8 +946,10 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
       (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials);
     else if (mode == 1)
       (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials);
-    else
+    else if (mode == 2)
       (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials);
+    else
+      (spmv_launch<NFc, PATc, 3>)(g, s, L, vals, x, y, w, partials);
   });
   return hipGetLastError();
 }
@@ -1029,16 +1048,21 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
 
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
                              const double *uv, const double *d, double *v, hipStream_t s,
-                             int c_first) {
+                             int c_first, const double *add, double *out) {
   if (L.n_owned == 0) return hipSuccess;
   const int nc = L.ncolors;
   PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
     auto go = [&](auto kind, int c) {
       const int n = cp[c + 1] - cp[c];
-      if (n > 0)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc>),
+      if (n <= 0) return;
+      if (add && decltype(kind)::value != kIluFwd)
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 1>),
                            rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
-                           d, v);
+                           d, v, add, out);
+      else
+        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 0>),
+                           rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
+                           d, v, nullptr, nullptr);
     };
     // the last colour's backward step runs in its forward launch (kIluLast); c_first = 1: colour
     // 0's forward step was done by launch_update_fwd0

@@ -231,6 +231,7 @@ typedef struct {
   int32_t coarse_target;  /* coarsen until at most this many vertex blocks (1..64, default 64) */
   int32_t max_levels;     /* levels including the fine one (2..16, default 12) */
   double omega;           /* damped block-Jacobi weight on the coarse levels (default 0.8) */
+  int32_t coarse_sweeps;  /* block-Jacobi sweeps per coarse pre-/post-smoothing (1..8, default 2) */
 } pnp_amg_opts;
 int pnp_amg_configure(pnp_ctx *ctx, const pnp_amg_opts *opts);
 typedef struct {

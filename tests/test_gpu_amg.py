@@ -34,9 +34,10 @@ def interleave(A, nv, nf):
     return A[perm][:, perm].tocsr(), perm
 
 
-def numpy_vcycle(A0, nf, aggs, omega, d):
-    """The V-cycle of amg.hip restated: Jacobi (pointwise) smoothing on level 0, damped
-    block-Jacobi on the coarse levels, exact solve on the coarsest."""
+def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2):
+    """The V-cycle of amg.hip restated: Jacobi (pointwise) smoothing on level 0, `sweeps` damped
+    block-Jacobi sweeps before and after the correction on the coarse levels, exact solve on the
+    coarsest."""
     As, Ps = [A0], []
     for agg in aggs:
         n = As[-1].shape[0] // nf
@@ -65,6 +66,8 @@ def numpy_vcycle(A0, nf, aggs, omega, d):
     if K > 1:
         x[1] = omega * bj(As[1], Dis[1], b[1])
     for k in range(1, K):
+        for _ in range(sweeps - 1):
+            x[k] = x[k] + omega * bj(As[k], Dis[k], b[k] - As[k] @ x[k])
         b[k + 1] = Ps[k].T @ (b[k] - As[k] @ x[k])
         if k + 1 < K:
             x[k + 1] = omega * bj(As[k + 1], Dis[k + 1], b[k + 1])
@@ -72,12 +75,15 @@ def numpy_vcycle(A0, nf, aggs, omega, d):
     for k in range(K - 1, 0, -1):
         xc = x[k] + Ps[k] @ e
         e = xc + omega * bj(As[k], Dis[k], b[k] - As[k] @ xc)
+        for _ in range(sweeps - 1):
+            e = e + omega * bj(As[k], Dis[k], b[k] - As[k] @ e)
     y = x0 + Ps[0] @ e
     return y + (d - A0 @ y) / diag0
 
 
-@pytest.mark.parametrize("kind", ["pb", "pnp", "pnp_ie", "diff", "poisson"])
-def test_amg_vcycle_matches_numpy_restatement(kind):
+@pytest.mark.parametrize("kind,sweeps", [("pb", 1), ("pb", 2), ("pnp", 1), ("pnp", 3),
+                                         ("pnp_ie", 2), ("diff", 2), ("poisson", 2)])
+def test_amg_vcycle_matches_numpy_restatement(kind, sweeps):
     mesh, par = problem("cylinder_config.cfg", 2)
     nv = mesh.nv
     ctx = P.Context(mesh, par)
@@ -104,7 +110,7 @@ def test_amg_vcycle_matches_numpy_restatement(kind):
         ctx.set_operator(P.OP_PB)
         x = rng.uniform(-1, 1, nv)
     J = ctx.jacobian(x)
-    ctx.amg_configure(smoother=P.PREC_JACOBI, coarse_target=16, omega=0.8)
+    ctx.amg_configure(smoother=P.PREC_JACOBI, coarse_target=16, omega=0.8, coarse_sweeps=sweeps)
     d = rng.standard_normal(nf * nv)
     v = ctx.prec_apply(d, P.PREC_AMG)
     info = ctx.amg_info()
@@ -113,7 +119,7 @@ def test_amg_vcycle_matches_numpy_restatement(kind):
     assert aggs[0].min() >= 0 and aggs[0].max() + 1 == info["rows"][1]
     Ji, perm = interleave(J, nv, nf)
     vn = np.empty_like(d)
-    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm])
+    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps)
     assert np.max(np.abs(v - vn)) <= 1e-10 * np.max(np.abs(vn))
 
 
