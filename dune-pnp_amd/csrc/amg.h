@@ -54,6 +54,7 @@ hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const
                             const double *x, const double *b, double *r, hipStream_t s);
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s);
+// e == nullptr: a plain damped block-Jacobi sweep (no correction; agg unused)
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
                            const int *agg, const double *x, const double *e, const double *b,
                            const double *dinv, double omega, double *out, hipStream_t s);

@@ -264,28 +264,28 @@ __device__ __forceinline__ void lanes_sum(double (&v)[NF]) {
     for (int f = 0; f < NF; f++) v[f] += __shfl_xor(v[f], o, LPR);
 }
 
+// Row tasks of the grid kernels below: row I, lane q of its LPR lanes; every lane of a row calls
+// (live or not: the cross-lane adds need all).
+
 // r = b - A x on a coarse level (block-CSR)
 template <int NF, int LPR>
-__global__ __launch_bounds__(kB) void k_resid(int nb, const int *__restrict__ rp,
-                                              const int *__restrict__ col,
-                                              const double *__restrict__ v,
-                                              const double *__restrict__ x,
-                                              const double *__restrict__ b,
-                                              double *__restrict__ r) {
+__device__ __forceinline__ void resid_task(int I, int q, bool live, const int *__restrict__ rp,
+                                           const int *__restrict__ col,
+                                           const double *__restrict__ v,
+                                           const double *__restrict__ x,
+                                           const double *__restrict__ b, double *__restrict__ r) {
   constexpr int NB = NF * NF;
-  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR, q0 = gt % LPR;
-  const bool live = I < nb;
   double acc[NF];
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] = 0;
   if (live)
-    for (int q = rp[I] + q0; q < rp[I + 1]; q += LPR) {
+    for (int k = rp[I] + q; k < rp[I + 1]; k += LPR) {
       double xj[NF];
-      load_nf<NF>(x, size_t(col[q]), xj);
-      bmv_acc<NF>(v + size_t(q) * NB, xj, acc);
+      load_nf<NF>(x, size_t(col[k]), xj);
+      bmv_acc<NF>(v + size_t(k) * NB, xj, acc);
     }
   lanes_sum<NF, LPR>(acc);
-  if (!live || q0 != 0) return;
+  if (!live || q != 0) return;
   double o[NF];
   load_nf<NF>(b, size_t(I), o);
 #pragma unroll
@@ -293,23 +293,21 @@ __global__ __launch_bounds__(kB) void k_resid(int nb, const int *__restrict__ rp
   store_nf<NF>(r, size_t(I), o);
 }
 
-// restriction: bn[J] = sum over the members i of aggregate J of (a - s)_i (s may be null);
+// restriction: bn[J] = sum over the members i of aggregate J of (a - sub)_i (sub may be null);
 // pre-smoothing of the coarse level from zero: xn = omega Dinv_J bn[J] (xn null: none)
 template <int NF, int LPR>
-__global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict__ mptr,
-                                                 const int *__restrict__ mem,
-                                                 const double *__restrict__ a,
-                                                 const double *__restrict__ sub,
-                                                 double *__restrict__ bn,
-                                                 const double *__restrict__ dinvn, double omega,
-                                                 double *__restrict__ xn) {
-  const int gt = blockIdx.x * kB + threadIdx.x, J = gt / LPR, q0 = gt % LPR;
-  const bool live = J < nbn;
+__device__ __forceinline__ void restrict_task(int J, int q, bool live, const int *__restrict__ mptr,
+                                              const int *__restrict__ mem,
+                                              const double *__restrict__ a,
+                                              const double *__restrict__ sub,
+                                              double *__restrict__ bn,
+                                              const double *__restrict__ dinvn, double omega,
+                                              double *__restrict__ xn) {
   double s[NF];
 #pragma unroll
   for (int f = 0; f < NF; f++) s[f] = 0;
   if (live)
-    for (int m = mptr[J] + q0; m < mptr[J + 1]; m += LPR) {
+    for (int m = mptr[J] + q; m < mptr[J + 1]; m += LPR) {
       const int i = mem[m];
       double ai[NF];
       load_nf<NF>(a, size_t(i), ai);
@@ -323,7 +321,7 @@ __global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict_
       for (int f = 0; f < NF; f++) s[f] += ai[f];
     }
   lanes_sum<NF, LPR>(s);
-  if (!live || q0 != 0) return;
+  if (!live || q != 0) return;
   store_nf<NF>(bn, size_t(J), s);
   if (xn) {
     double y[NF];
@@ -334,6 +332,95 @@ __global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict_
     for (int f = 0; f < NF; f++) y[f] *= omega;
     store_nf<NF>(xn, size_t(J), y);
   }
+}
+
+// one damped block-Jacobi sweep, with the coarse correction folded in when CORR:
+//   xc(j) = x[j] (+ e[agg[j]]),  out[I] = xc(I) + omega Dinv_I (b_I - sum_j A_Ij xc(j))
+template <int NF, int LPR, int CORR>
+__device__ __forceinline__ void jacobi_task(int I, int q, bool live, const int *__restrict__ rp,
+                                            const int *__restrict__ col,
+                                            const double *__restrict__ v,
+                                            const int *__restrict__ agg,
+                                            const double *__restrict__ x,
+                                            const double *__restrict__ e,
+                                            const double *__restrict__ b,
+                                            const double *__restrict__ dinv, double omega,
+                                            double *__restrict__ out) {
+  constexpr int NB = NF * NF;
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0;
+  if (live)
+    for (int k = rp[I] + q; k < rp[I + 1]; k += LPR) {
+      const int j = col[k];
+      double xj[NF];
+      load_nf<NF>(x, size_t(j), xj);
+      if (CORR) {
+        double ej[NF];
+        load_nf<NF>(e, size_t(agg[j]), ej);
+#pragma unroll
+        for (int f = 0; f < NF; f++) xj[f] += ej[f];
+      }
+      bmv_acc<NF>(v + size_t(k) * NB, xj, acc);
+    }
+  lanes_sum<NF, LPR>(acc);
+  if (!live || q != 0) return;
+  double r[NF], xi[NF];
+  load_nf<NF>(b, size_t(I), r);
+#pragma unroll
+  for (int f = 0; f < NF; f++) r[f] -= acc[f];
+  load_nf<NF>(x, size_t(I), xi);
+  if (CORR) {
+    double ei[NF];
+    load_nf<NF>(e, size_t(agg[I]), ei);
+#pragma unroll
+    for (int f = 0; f < NF; f++) xi[f] += ei[f];
+  }
+  double y[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) y[f] = 0;
+  bmv_acc<NF>(dinv + size_t(I) * NB, r, y);
+#pragma unroll
+  for (int f = 0; f < NF; f++) xi[f] += omega * y[f];
+  store_nf<NF>(out, size_t(I), xi);
+}
+
+template <int NF, int LPR>
+__global__ __launch_bounds__(kB) void k_resid(int nb, const int *__restrict__ rp,
+                                              const int *__restrict__ col,
+                                              const double *__restrict__ v,
+                                              const double *__restrict__ x,
+                                              const double *__restrict__ b,
+                                              double *__restrict__ r) {
+  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR;
+  resid_task<NF, LPR>(I, gt % LPR, I < nb, rp, col, v, x, b, r);
+}
+
+template <int NF, int LPR>
+__global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict__ mptr,
+                                                 const int *__restrict__ mem,
+                                                 const double *__restrict__ a,
+                                                 const double *__restrict__ sub,
+                                                 double *__restrict__ bn,
+                                                 const double *__restrict__ dinvn, double omega,
+                                                 double *__restrict__ xn) {
+  const int gt = blockIdx.x * kB + threadIdx.x, J = gt / LPR;
+  restrict_task<NF, LPR>(J, gt % LPR, J < nbn, mptr, mem, a, sub, bn, dinvn, omega, xn);
+}
+
+// post-smoothing sweep (CORR = 1: with the coarse correction e folded in; 0: plain sweep)
+template <int NF, int LPR, int CORR>
+__global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
+                                             const int *__restrict__ col,
+                                             const double *__restrict__ v,
+                                             const int *__restrict__ agg,
+                                             const double *__restrict__ x,
+                                             const double *__restrict__ e,
+                                             const double *__restrict__ b,
+                                             const double *__restrict__ dinv, double omega,
+                                             double *__restrict__ out) {
+  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR;
+  jacobi_task<NF, LPR, CORR>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega, out);
 }
 
 // coarsest: x = Ainv b (ainv column-major n x n, n <= 3 kAmgMaxCoarse), one workgroup
@@ -355,52 +442,11 @@ __global__ __launch_bounds__(kB) void k_coarse_apply(int n, const double *__rest
   x[i] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
-// post-smoothing of level l >= 1 with the coarse correction folded in:
-//   xc(j) = x[j] + e[agg[j]],  out[I] = xc(I) + omega Dinv_I (b_I - sum_j A_Ij xc(j))
-template <int NF, int LPR>
-__global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
-                                             const int *__restrict__ col,
-                                             const double *__restrict__ v,
-                                             const int *__restrict__ agg,
-                                             const double *__restrict__ x,
-                                             const double *__restrict__ e,
-                                             const double *__restrict__ b,
-                                             const double *__restrict__ dinv, double omega,
-                                             double *__restrict__ out) {
-  constexpr int NB = NF * NF;
-  const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR, q0 = gt % LPR;
-  const bool live = I < nb;
-  double acc[NF];
-#pragma unroll
-  for (int f = 0; f < NF; f++) acc[f] = 0;
-  if (live)
-    for (int q = rp[I] + q0; q < rp[I + 1]; q += LPR) {
-      const int j = col[q];
-      double xj[NF], ej[NF];
-      load_nf<NF>(x, size_t(j), xj);
-      load_nf<NF>(e, size_t(agg[j]), ej);
-#pragma unroll
-      for (int f = 0; f < NF; f++) xj[f] += ej[f];
-      bmv_acc<NF>(v + size_t(q) * NB, xj, acc);
-    }
-  lanes_sum<NF, LPR>(acc);
-  if (!live || q0 != 0) return;
-  double r[NF], xi[NF], ei[NF];
-  load_nf<NF>(b, size_t(I), r);
-#pragma unroll
-  for (int f = 0; f < NF; f++) r[f] -= acc[f];
-  load_nf<NF>(x, size_t(I), xi);
-  load_nf<NF>(e, size_t(agg[I]), ei);
-#pragma unroll
-  for (int f = 0; f < NF; f++) xi[f] += ei[f];
-  double y[NF];
-#pragma unroll
-  for (int f = 0; f < NF; f++) y[f] = 0;
-  bmv_acc<NF>(dinv + size_t(I) * NB, r, y);
-#pragma unroll
-  for (int f = 0; f < NF; f++) xi[f] += omega * y[f];
-  store_nf<NF>(out, size_t(I), xi);
-}
+// (Running the small levels -- pre-smoothing, residual, restriction, coarsest solve,
+// post-smoothing -- inside ONE workgroup with __syncthreads() between the steps was measured and
+// lost: 120 us for the levels <= 2048 rows against ~50 us of separate launches, and still +11 us
+// per V-cycle for the levels <= 256 rows (profiles/r01/ab_amg_tail_*.log): one CU cannot hide the
+// dependent gathers that ~4.5 us launches spread over the whole chip.)
 
 // level 0 prolongation: y = x0 + e1[agg0]
 template <int NF>
@@ -501,8 +547,14 @@ hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const 
                            const int *agg, const double *x, const double *e, const double *b,
                            const double *dinv, double omega, double *out, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr>), g1((long long)nb * kLpr), dim3(kB),
-                                         0, s, nb, rp, col, v, agg, x, e, b, dinv, omega, out));
+  if (e)
+    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr, 1>), g1((long long)nb * kLpr),
+                                           dim3(kB), 0, s, nb, rp, col, v, agg, x, e, b, dinv,
+                                           omega, out));
+  else
+    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr, 0>), g1((long long)nb * kLpr),
+                                           dim3(kB), 0, s, nb, rp, col, v, agg, x, e, b, dinv,
+                                           omega, out));
   return hipGetLastError();
 }
 

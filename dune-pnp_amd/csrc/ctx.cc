@@ -141,7 +141,7 @@ struct pnp_ctx {
   bool amg_built = false, amg_valid = false;
   int amg_nf = 0;
   double amg_setup_ms = 0;
-  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z, amg_zero;
+  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
 
 
   // vectors (sized n_local * 3)
@@ -483,8 +483,7 @@ struct pnp_ctx {
       if ((e = amg_work.alloc(nc * nc)) != hipSuccess || (e = amg_ainv.alloc(nc * nc)) != hipSuccess ||
           (e = amg_x0.alloc(nl)) != hipSuccess || (e = amg_t.alloc(nl)) != hipSuccess ||
           (e = amg_y.alloc(nl)) != hipSuccess || (e = amg_r.alloc(nl)) != hipSuccess ||
-          (e = amg_z.alloc(nl)) != hipSuccess ||
-          (e = amg_zero.alloc(size_t(amg_d[0]->nb) * nf)) != hipSuccess)
+          (e = amg_z.alloc(nl)) != hipSuccess)
         return hipfail(e, "amg vectors");
       amg_nf = nf;
       amg_valid = false;
@@ -533,12 +532,13 @@ struct pnp_ctx {
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
       for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more pre-smoothing
-        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, N.agg.p, C.x.p, amg_zero.p,
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, nullptr, C.x.p, nullptr,
                                  C.b.p, C.dinv.p, om, C.x2.p, stream);
         std::swap(C.x.p, C.x2.p);
       }
       // residual of level k+1 into its x2 (free until its post-smoothing), then restriction
-      e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.x.p, C.b.p, C.x2.p, stream);
+      if (e == hipSuccess)
+        e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.x.p, C.b.p, C.x2.p, stream);
       if (e == hipSuccess)
         e = pnp::launch_amg_restrict(nf, N.nb, N.mptr.p, N.mem.p, C.x2.p, nullptr, N.b.p,
                                      N.dinv.p, om, k + 2 < K ? N.x.p : nullptr, stream);
@@ -554,8 +554,8 @@ struct pnp_ctx {
       res = C.x2.p;
       for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more post-smoothing
         double *out = res == C.x2.p ? C.x.p : C.x2.p;
-        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, amg_d[k + 1]->agg.p, res,
-                                 amg_zero.p, C.b.p, C.dinv.p, om, out, stream);
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, nullptr, res, nullptr, C.b.p,
+                                 C.dinv.p, om, out, stream);
         res = out;
       }
     }
