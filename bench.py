@@ -318,10 +318,10 @@ def main():
             "bicgstab_ms_per_iter": 1e3 * t_bicg / (args.steps * args.bicg_iters),
             "roofline": {"bound": "hbm", "achieved": achieved_asm, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_asm / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("k_assemble<0, 1, 3,"),
+                         "traffic": pmc_traffic("k_assemble_ga<0, 1, 2, 9"),
                          "traffic_source": "profiles/r01/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
                                            "+ WRITE_SIZE per launch, separate passes)",
-                         "kernel": "k_assemble<OP_PNP,1>",
+                         "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
                          "bytes_per_launch": B_asm, "avg_launch_us": asm_avg_s * 1e6},
             "roofline_bicgstab": {"bound": "hbm", "bytes_per_iter": B_it,
                                   "event_ms_per_iter": it_time_ev * 1e3,

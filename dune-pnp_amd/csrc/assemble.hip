@@ -371,6 +371,116 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   }
 }
 
+// Gather-all variant (GA): every neighbour's data (coordinates, NF dofs, frozen fields) of the
+// row's fan is loaded into registers before the walk, so the gathers of the whole fan are in
+// flight together (one memory round trip per row instead of one per element; the pipelined walk
+// above keeps ~1 element of loads in flight), and the block stores of the walk never sit in front
+// of a load the walk still waits for.  Same element() calls with the same operands in the same
+// order as k_assemble (the compiler's FMA contraction may still differ in the last bit).  Fans of
+// at most FANR - 1 neighbours.  Config 3: 76.5 -> 72.2 us at 2 waves/SIMD (180 VGPRs); at 3 waves
+// it spills (80.8 us) and a split gather (slots 1-4 first) ties at 72.9 us
+// (profiles/r01/ab_asm_gather_all.log).
+// SPLIT < FANR: only slots 1 .. SPLIT-1 are gathered up front; the rest are issued after element
+// SPLIT-2, when the first elements' neighbour registers are free again (fewer live VGPRs).
+template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR>
+__global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs a) {
+  using T = OpTraits<OP>;
+  constexpr int NF = T::NF, NK = T::NK, NS = FANR;
+  constexpr bool AUX0 = OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON;
+  constexpr bool AUX1 = OP == OP_POISSON;
+  const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * blockDim.x + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk];
+  const uint64_t meta = L.rowmeta[row];
+  const int len = int(meta & 63);
+  const bool closed = (meta >> 6) & 1;
+  const unsigned brk = unsigned(meta >> 8);  // fan-break bits, bit s: no element after slot s
+  const int *__restrict__ cix = L.colidx + off + lane;
+  double *__restrict__ vc = a.vals + size_t(off) * NK;  // chunk base (k-form), see vin()
+
+  int cj[NS];
+#pragma unroll
+  for (int k = 1; k < NS; k++) cj[k] = cix[(k < len ? k : 0) * kRows];  // past the fan: the row
+  const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
+  double ui[NF];
+  load_nf<NF>(a.x, size_t(row), ui);
+  double ai = 0, aq = 0;
+  if constexpr (AUX0) ai = a.aux0[row];
+  if constexpr (AUX1) aq = a.aux1[row];
+  double2 pn[NS];
+  double un[NS][NF], a0[NS], a1[NS];
+  auto gather = [&](int k) {
+    pn[k] = reinterpret_cast<const double2 *>(L.xy)[cj[k]];
+    load_nf<NF>(a.x, size_t(cj[k]), un[k]);
+    a0[k] = AUX0 ? a.aux0[cj[k]] : 0.0;
+    a1[k] = AUX1 ? a.aux1[cj[k]] : 0.0;
+  };
+#pragma unroll
+  for (int k = 1; k < SPLIT; k++) gather(k);
+
+  double R[NF], D[NK], P[NK], F[NK];
+#pragma unroll
+  for (int f = 0; f < NF; f++) R[f] = 0;
+#pragma unroll
+  for (int v = 0; v < NK; v++) D[v] = P[v] = F[v] = 0;
+#pragma unroll
+  for (int s = 1; s < NS; s++) {
+    if (SPLIT < NS && s == (SPLIT > 2 ? SPLIT - 2 : 1)) {
+#pragma unroll
+      for (int k = SPLIT; k < NS; k++) gather(k);
+    }
+    if (s < len) {
+      const bool has_next = s + 1 < len;
+      const int sn = (s + 1 < NS) ? s + 1 : 1;  // static slot of v_{s+1}
+      const bool elem = (has_next || closed) && !((brk >> s) & 1);
+      if (elem) {
+        // v_t = v_{s+1}, or v_1 when a closed fan wraps
+        const double2 pt = has_next ? pn[sn] : pn[1];
+        double ut[NF];
+#pragma unroll
+        for (int f = 0; f < NF; f++) ut[f] = has_next ? un[sn][f] : un[1][f];
+        const double at0 = has_next ? a0[sn] : a0[1], at1 = has_next ? a1[sn] : a1[1];
+        Geo G;
+        geometry(pi2.x, pi2.y, pn[s].x, pn[s].y, pt.x, pt.y, G);
+        double Ct[NK];
+#pragma unroll
+        for (int v = 0; v < NK; v++) Ct[v] = 0;
+        element<OP, JAC>(a, G, pi2.y, pn[s].y, pt.y, ui, un[s], ut, ai, a0[s], at0, aq, a1[s],
+                         at1, R, D, P, Ct);
+        if constexpr (JAC) {
+          if (s == 1 && closed) {
+#pragma unroll
+            for (int v = 0; v < NK; v++) F[v] = P[v];
+          } else {
+            store_block<OP>(vc, lane, s, P);
+          }
+#pragma unroll
+          for (int v = 0; v < NK; v++) P[v] = Ct[v];
+        }
+      } else if constexpr (JAC) {
+        store_block<OP>(vc, lane, s, P);
+#pragma unroll
+        for (int v = 0; v < NK; v++) P[v] = 0;
+      }
+    }
+  }
+  if constexpr (JAC) {
+    if (closed) {
+#pragma unroll
+      for (int v = 0; v < NK; v++) F[v] += P[v];
+      store_block<OP>(vc, lane, 1, F);
+    }
+    store_block<OP>(vc, lane, 0, D);
+  }
+#pragma unroll
+  for (int f = 0; f < NF; f++) {
+    const size_t q = size_t(row) * NF + f;
+    const double rv = R[f] + a.cvec[q];
+    a.r[q] = a.dmask[q] != 0 ? 0.0 : rv;
+  }
+}
+
 // cvec[row] -= M(x_old)[row]: PnpTOperator (tau * (c+ + c-) into the c+ row, Q2) or the
 // DiffusionTOperator mass, for the implicit Euler residual M(u) - M(u_old) + dt R(u).
 template <int OP>
@@ -478,6 +588,12 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     const char *e = getenv("PNP_ASM_FANR");
     return !(e && atoi(e) == 0);
   }();
+  // A/B knob PNP_ASM_GA: 0 = the pipelined walk (k_assemble), 1 = gather-all at 3 waves/SIMD
+  // (spills), 2 = gather-all at 2 waves (default), 3 = gather 4 neighbours first at 3 waves
+  static const int ga = [] {
+    const char *e = getenv("PNP_ASM_GA");
+    return e ? atoi(e) : 2;
+  }();
   // column indices in registers: FANR - 1 >= the longest fan (max_slots - 1; 8 on all meshes
   // seen), 12 as the general case, 0 (index loads in the walk) beyond
   const int fanr = !fanr_ok ? 0 : (L.max_slots <= 9 ? 9 : (L.max_slots <= 12 ? 12 : 0));
@@ -489,6 +605,12 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
     else if (!a.jac)                                                               \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, L, a);    \
+    else if (ga == 1 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9>), grid, block, 0, s, L, a);  \
+    else if (ga == 2 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
+    else if (ga == 3 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
     else if (fanr == 12)                                                           \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
     else if (waves == 3)                                                           \
