@@ -9,6 +9,9 @@
 #include "pnp_oracle.h"
 
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 
@@ -816,6 +819,90 @@ void orc_op_jacobian(const orc_mesh *m, const orc_params *p, const orc_operator 
       if (op->mask[i])
         for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++)
           A->val[k] = (A->col[k] == i) ? 1.0 : 0.0;
+}
+
+/* ----------------------------------------------------------------------------------------
+ * all-core CPU baseline (SURVEY.md §8(d) "CPU baseline (ii)"): the same reference algorithm
+ * (element residual + NumericalJacobianVolume forward differences + BCRS-style scatter) with
+ * the elements coloured so that no two elements of a colour share a vertex; each colour is an
+ * OpenMP parallel loop with race-free scatters.  Test/bench infrastructure, like the rest.
+ * ---------------------------------------------------------------------------------------- */
+int orc_element_colors(const orc_mesh *m, int *color) {
+  /* greedy: smallest colour not used by an element already coloured around its vertices */
+  unsigned long long *used = (unsigned long long *)calloc((size_t)m->nv, sizeof *used);
+  int ncol = 0;
+  for (int e = 0; e < m->nt; e++) {
+    const int *t = m->tri + 3 * e;
+    unsigned long long u = used[t[0]] | used[t[1]] | used[t[2]];
+    int c = 0;
+    while (c < 64 && ((u >> c) & 1ULL)) c++;
+    if (c == 64) {
+      free(used);
+      return -1;
+    }
+    color[e] = c;
+    for (int a = 0; a < 3; a++) used[t[a]] |= 1ULL << c;
+    if (c + 1 > ncol) ncol = c + 1;
+  }
+  free(used);
+  return ncol;
+}
+
+void orc_assemble_mt(const orc_mesh *m, const orc_params *p, const orc_operator *op,
+                     const double *x, const int *eorder, const int *cptr, int ncol, orc_csr *A,
+                     double *r) {
+  int nf = orc_operator_nfields(op);
+  int nl = 3 * nf, nv = m->nv, n = nf * nv;
+  memset(A->val, 0, sizeof(double) * A->nnz);
+  memset(r, 0, sizeof(double) * n);
+  for (int c = 0; c < ncol; c++) {
+#pragma omp parallel for schedule(static)
+    for (int k = cptr[c]; k < cptr[c + 1]; k++) {
+      const int e = eorder[k];
+      const int *t = m->tri + 3 * e;
+      double xl[9], u[9], down[9], up[9], Jl[81];
+      elgeo G;
+      element_geometry(m, e, &G);
+      gather(m, e, nf, x, xl);
+      memcpy(u, xl, sizeof(double) * nl);
+      op_volume(m, p, op, e, &G, u, down);
+      scatter_add(m, e, nf, down, r);
+      for (int j = 0; j < nl; j++) {
+        double delta = 1e-7 * (1.0 + fabs(u[j]));
+        u[j] += delta;
+        op_volume(m, p, op, e, &G, u, up);
+        for (int i = 0; i < nl; i++) Jl[i * nl + j] = (up[i] - down[i]) / delta;
+        u[j] = xl[j];
+      }
+      for (int i = 0; i < nl; i++) {
+        int I = (i / 3) * nv + t[i % 3];
+        for (int j = 0; j < nl; j++) {
+          int Jc = (j / 3) * nv + t[j % 3];
+          *csr_find(A, I, Jc) += Jl[i * nl + j];
+        }
+      }
+    }
+  }
+  if (op->kind == ORC_OP_PNP) boundary_flux(m, p, op->flux, 3, 0, 1.0, r);
+  if (op->kind == ORC_OP_PB || op->kind == ORC_OP_POISSON)
+    boundary_flux(m, p, op->flux, 1, 0, 1.0, r);
+  if (op->mask) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+      if (op->mask[i]) {
+        r[i] = 0.0;
+        for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++)
+          A->val[k] = (A->col[k] == i) ? 1.0 : 0.0;
+      }
+  }
+}
+
+int orc_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }
 
 /* ----------------------------------------------------------------------------------------

@@ -127,6 +127,15 @@ int orc_operator_nfields(const orc_operator *op);
 /* residual of the (possibly time-discrete) operator, constraints applied */
 void orc_op_residual(const orc_mesh *m, const orc_params *p, const orc_operator *op,
                      const double *x, double *r);
+/* All-core CPU baseline (bench only): element colouring (no two elements of a colour share a
+ * vertex; returns the colour count or -1) and the residual + forward-difference Jacobian
+ * assembly of the ops's PnpOperator / PB / Poisson path with OpenMP over the elements of each
+ * colour (eorder lists the elements colour by colour, cptr[ncol+1] the colour offsets). */
+int orc_element_colors(const orc_mesh *m, int *color);
+void orc_assemble_mt(const orc_mesh *m, const orc_params *p, const orc_operator *op,
+                     const double *x, const int *eorder, const int *cptr, int ncol, orc_csr *A,
+                     double *r);
+int orc_num_threads(void);
 /* Jacobian into A (pattern from orc_csr_pattern).  fd=1: PDELab NumericalJacobianVolume
  * forward differences (reference-faithful); fd=0: analytic. Constrained rows -> identity. */
 void orc_op_jacobian(const orc_mesh *m, const orc_params *p, const orc_operator *op,

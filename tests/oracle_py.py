@@ -186,6 +186,37 @@ class Problem:
         L.orc_csr_free(C.byref(A))
         return dt, sp.csr_matrix((val, col, rp), shape=(n, n))
 
+    def time_fd_assembly_mt(self, op, x, seconds):
+        """All-core CPU baseline: the same residual + forward-difference Jacobian assembly with
+        OpenMP over element colours (orc_assemble_mt).  Returns (s/assembly, threads, A, r)."""
+        import time
+        import scipy.sparse as sp
+        L = lib()
+        col = np.zeros(self.mesh.nt, dtype=np.int32)
+        ncol = L.orc_element_colors(C.byref(self.m), _p(col))
+        assert ncol > 0
+        order = np.argsort(col, kind="stable").astype(np.int32)
+        cptr = np.zeros(ncol + 1, dtype=np.int32)
+        cptr[1:] = np.cumsum(np.bincount(col, minlength=ncol))
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        r = np.zeros(self.nfields(op) * self.nv)
+        A = OrcCsr()
+        L.orc_csr_pattern(C.byref(self.m), self.nfields(op), C.byref(A))
+        n, t0 = 0, time.perf_counter()
+        while True:
+            L.orc_assemble_mt(C.byref(self.m), C.byref(self.p), C.byref(op), _p(x), _p(order),
+                              _p(cptr), int(ncol), C.byref(A), _p(r))
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = (time.perf_counter() - t0) / n
+        rp = np.ctypeslib.as_array(A.rowptr, shape=(A.n + 1,)).copy()
+        cc = np.ctypeslib.as_array(A.col, shape=(A.nnz,)).copy()
+        val = np.ctypeslib.as_array(A.val, shape=(A.nnz,)).copy()
+        nn = A.n
+        L.orc_csr_free(C.byref(A))
+        return dt, int(L.orc_num_threads()), sp.csr_matrix((val, cc, rp), shape=(nn, nn)), r
+
     def newton(self, op, u, reduction=1e-9, abs_limit=1e-12, min_linear_reduction=1e-8, maxit=50,
                line_search_maxit=500, linear_maxit=20000, prec=PREC_NONE, fd=False):
         u = np.ascontiguousarray(u, dtype=np.float64).copy()
