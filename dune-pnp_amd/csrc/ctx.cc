@@ -129,7 +129,8 @@ struct pnp_ctx {
 
   // aggregation AMG (PNP_PREC_AMG, amg.h): the pattern hierarchy is built once per context (it
   // depends on the layout only), the coarse values after every assembly
-  pnp_amg_opts amg_opts{PNP_PREC_SSOR, pnp::kAmgMaxCoarse, 12, 0.8, 2};
+  pnp_amg_opts amg_opts{PNP_PREC_SSOR, pnp::kAmgMaxCoarse, 12, 0.8, 2, -1};
+  bool amg_symmetric = true;  // set per solve: CG needs the symmetric V-cycle
   std::vector<pnp::AmgLevelHost> amg_h;
   struct AmgDev {
     int nb = 0;
@@ -522,13 +523,22 @@ struct pnp_ctx {
     int rc, nsp = 0;
     hipError_t e;
     // level 0 pre-smoothing from zero, residual (SpMV residual mode), restriction (+ level-1
-    // pre-smoothing)
-    if ((rc = smoother(sm, d, amg_x0.p))) return rc;
-    e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 3, d, partials.p, &nsp, stream);
+    // pre-smoothing); without level-0 pre-smoothing x0 = 0 and the restriction takes d itself
+    // amg_opts.level0_presmooth: 1 always, 0 never, -1 (auto) only when the V-cycle must stay
+    // symmetric (CG, or a bare pnp_prec_apply); BiCGSTAB takes the post-smoothing-only cycle
+    const bool pre0 = amg_opts.level0_presmooth > 0 ||
+                      (amg_opts.level0_presmooth < 0 && amg_symmetric);
+    if (pre0) {
+      if ((rc = smoother(sm, d, amg_x0.p))) return rc;
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 3, d, partials.p, &nsp,
+                           stream);
+    } else {
+      e = hipMemsetAsync(amg_x0.p, 0, sizeof(double) * nn, stream);
+    }
     if (e == hipSuccess)
-      e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p, amg_t.p,
-                                   nullptr, amg_d[0]->b.p, amg_d[0]->dinv.p, om,
-                                   K > 1 ? amg_d[0]->x.p : nullptr, stream);
+      e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p,
+                                   pre0 ? amg_t.p : d, nullptr, amg_d[0]->b.p, amg_d[0]->dinv.p,
+                                   om, K > 1 ? amg_d[0]->x.p : nullptr, stream);
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
       for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more pre-smoothing
@@ -822,9 +832,18 @@ struct pnp_ctx {
 
   // the linear solver selected by o.method
   int krylov(const double *bdev, double *zout, const pnp_solve_opts &o, pnp_solve_result &res) {
-    if (o.method == PNP_METHOD_CG) return cg(bdev, zout, o, res);
-    if (o.method != PNP_METHOD_BICGSTAB) return fail(PNP_E_ARG, "unknown solver method");
-    return bicgstab(bdev, zout, o, res, 0);
+    int rc;
+    if (o.method == PNP_METHOD_CG) {
+      amg_symmetric = true;
+      rc = cg(bdev, zout, o, res);
+    } else if (o.method == PNP_METHOD_BICGSTAB) {
+      amg_symmetric = false;
+      rc = bicgstab(bdev, zout, o, res, 0);
+    } else {
+      return fail(PNP_E_ARG, "unknown solver method");
+    }
+    amg_symmetric = true;
+    return rc;
   }
 };
 
@@ -1509,7 +1528,8 @@ extern "C" int pnp_amg_configure(pnp_ctx *c, const pnp_amg_opts *o) {
     return c->fail(PNP_E_ARG, "AMG smoother must be SSOR, ILU0 or JACOBI");
   if (o->coarse_target < 1 || o->coarse_target > pnp::kAmgMaxCoarse || o->max_levels < 2 ||
       o->max_levels > pnp::kAmgMaxLevels || !(o->omega > 0 && o->omega <= 2) ||
-      o->coarse_sweeps < 1 || o->coarse_sweeps > 8)
+      o->coarse_sweeps < 1 || o->coarse_sweeps > 8 || o->level0_presmooth < -1 ||
+      o->level0_presmooth > 1)
     return c->fail(PNP_E_ARG, "AMG options out of range");
   const bool rebuild = o->coarse_target != c->amg_opts.coarse_target ||
                        o->max_levels != c->amg_opts.max_levels;
@@ -1764,7 +1784,10 @@ extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_
   CK(hipMemcpyAsync(c->b.p, c->r.p, sizeof(double) * c->nown(), hipMemcpyDeviceToDevice,
                     c->stream),
      "rhs");
-  return c->bicgstab(c->b.p, c->z.p, o, *res, n);
+  c->amg_symmetric = false;  // as in krylov(): BiCGSTAB
+  int rc = c->bicgstab(c->b.p, c->z.p, o, *res, n);
+  c->amg_symmetric = true;
+  return rc;
 }
 
 extern "C" int pnp_timers_enable(pnp_ctx *c, int32_t on) {

@@ -109,7 +109,8 @@ class _SolveResult(C.Structure):
 
 class _AmgOpts(C.Structure):
     _fields_ = [("smoother", C.c_int32), ("coarse_target", C.c_int32), ("max_levels", C.c_int32),
-                ("omega", C.c_double), ("coarse_sweeps", C.c_int32)]
+                ("omega", C.c_double), ("coarse_sweeps", C.c_int32),
+                ("level0_presmooth", C.c_int32)]
 
 
 class _AmgStats(C.Structure):
@@ -486,10 +487,10 @@ class Context:
         return v
 
     def amg_configure(self, smoother=PREC_SSOR, coarse_target=64, max_levels=12, omega=0.8,
-                      coarse_sweeps=2):
+                      coarse_sweeps=2, level0_presmooth=-1):
         """Options of PREC_AMG (the reference's CG_AMG_SSOR preconditioner); see pnp_capi.h."""
         o = _AmgOpts(int(smoother), int(coarse_target), int(max_levels), float(omega),
-                     int(coarse_sweeps))
+                     int(coarse_sweeps), int(level0_presmooth))
         self._ck(lib().pnp_amg_configure(self.h, C.byref(o)))
 
     def amg_info(self):

@@ -232,6 +232,10 @@ typedef struct {
   int32_t max_levels;     /* levels including the fine one (2..16, default 12) */
   double omega;           /* damped block-Jacobi weight on the coarse levels (default 0.8) */
   int32_t coarse_sweeps;  /* block-Jacobi sweeps per coarse pre-/post-smoothing (1..8, default 2) */
+  int32_t level0_presmooth; /* level-0 pre-smoothing: 1 yes, 0 no (post-smoothing only), -1 auto
+                             (default): yes for CG and pnp_prec_apply (the V-cycle must be
+                             symmetric), no for BiCGSTAB (same iterations at 2/3 of the cycle's
+                             cost on config 3) */
 } pnp_amg_opts;
 int pnp_amg_configure(pnp_ctx *ctx, const pnp_amg_opts *opts);
 typedef struct {

@@ -34,7 +34,7 @@ def interleave(A, nv, nf):
     return A[perm][:, perm].tocsr(), perm
 
 
-def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2):
+def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True):
     """The V-cycle of amg.hip restated: Jacobi (pointwise) smoothing on level 0, `sweeps` damped
     block-Jacobi sweeps before and after the correction on the coarse levels, exact solve on the
     coarsest."""
@@ -60,7 +60,7 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2):
 
     Dis = [None] + [dinv(As[k]) for k in range(1, K)]
     diag0 = A0.diagonal()
-    x0 = d / diag0
+    x0 = d / diag0 if pre0 else np.zeros_like(d)
     b, x = [None] * (K + 1), [None] * (K + 1)
     b[1] = Ps[0].T @ (d - A0 @ x0)
     if K > 1:
@@ -81,9 +81,10 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2):
     return y + (d - A0 @ y) / diag0
 
 
-@pytest.mark.parametrize("kind,sweeps", [("pb", 1), ("pb", 2), ("pnp", 1), ("pnp", 3),
-                                         ("pnp_ie", 2), ("diff", 2), ("poisson", 2)])
-def test_amg_vcycle_matches_numpy_restatement(kind, sweeps):
+@pytest.mark.parametrize("kind,sweeps,pre0", [("pb", 1, 1), ("pb", 2, 1), ("pnp", 1, 1),
+                                              ("pnp", 3, 1), ("pnp_ie", 2, 1), ("diff", 2, 1),
+                                              ("poisson", 2, 1), ("pnp", 2, 0), ("pb", 2, 0)])
+def test_amg_vcycle_matches_numpy_restatement(kind, sweeps, pre0):
     mesh, par = problem("cylinder_config.cfg", 2)
     nv = mesh.nv
     ctx = P.Context(mesh, par)
@@ -110,7 +111,8 @@ def test_amg_vcycle_matches_numpy_restatement(kind, sweeps):
         ctx.set_operator(P.OP_PB)
         x = rng.uniform(-1, 1, nv)
     J = ctx.jacobian(x)
-    ctx.amg_configure(smoother=P.PREC_JACOBI, coarse_target=16, omega=0.8, coarse_sweeps=sweeps)
+    ctx.amg_configure(smoother=P.PREC_JACOBI, coarse_target=16, omega=0.8, coarse_sweeps=sweeps,
+                      level0_presmooth=pre0)
     d = rng.standard_normal(nf * nv)
     v = ctx.prec_apply(d, P.PREC_AMG)
     info = ctx.amg_info()
@@ -119,7 +121,7 @@ def test_amg_vcycle_matches_numpy_restatement(kind, sweeps):
     assert aggs[0].min() >= 0 and aggs[0].max() + 1 == info["rows"][1]
     Ji, perm = interleave(J, nv, nf)
     vn = np.empty_like(d)
-    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps)
+    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps, bool(pre0))
     assert np.max(np.abs(v - vn)) <= 1e-10 * np.max(np.abs(vn))
 
 
