@@ -28,7 +28,7 @@ PNP_PREC = P.PREC_BY_NAME[os.environ.get("PNP_BENCH_PREC", "ilu0")]
 
 def pnp_prec(ctx):
     if PNP_PREC == P.PREC_AMG:
-        ctx.amg_configure(smoother=P.PREC_ILU0, omega=1.0, coarse_sweeps=2)
+        ctx.amg_configure(smoother=P.PREC_ILU0)  # defaults: omega 0.8, 2 coarse sweeps
     return PNP_PREC
 
 
