@@ -10,7 +10,11 @@
 
 namespace pnp {
 
-constexpr int kAmgMaxCoarse = 64;  // coarsest level: at most this many vertex blocks (dense solve)
+// coarsest level: a dense inverse of at most kAmgMaxDense unknowns, i.e. at most kAmgMaxCoarse
+// vertex blocks of 3 fields (170; coarsening stops there, so the same hierarchy serves the
+// scalar and the 3-field operators)
+constexpr int kAmgMaxDense = 512;
+constexpr int kAmgMaxCoarse = kAmgMaxDense / 3;
 constexpr int kAmgMaxLevels = 16;
 
 // One coarse level l >= 1 (block-CSR, dense NF x NF blocks, columns sorted, diagonal present)

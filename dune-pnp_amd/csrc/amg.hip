@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kB) void k_dinv(int nb, const int *__restrict__ dpo
 }
 
 // coarsest level: ainv (column-major, n = nb * NF) = dense inverse of the block-CSR matrix by
-// Gauss-Jordan with partial pivoting, one workgroup (n <= kAmgMaxCoarse; the work matrix a is
+// Gauss-Jordan with partial pivoting, one workgroup (n <= kAmgMaxDense; the work matrix a is
 // L2-resident).  A singular pivot leaves zeros (the row's unknowns are then not corrected).
 constexpr int kGJ = 1024;
 __global__ __launch_bounds__(kGJ) void k_coarse_inverse(int nb, int nf, const int *__restrict__ rp,
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kGJ) void k_coarse_inverse(int nb, int nf, const in
                                                         double *__restrict__ a,
                                                         double *__restrict__ ainv) {
   const int n = nb * nf, nbb = nf * nf, t = threadIdx.x;
-  __shared__ double fcol[kAmgMaxCoarse * 3];
+  __shared__ double fcol[kAmgMaxDense];
   __shared__ double pv[kGJ / 64];
   __shared__ int pi[kGJ / 64];
   __shared__ int piv;
@@ -423,23 +423,29 @@ __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
   jacobi_task<NF, LPR, CORR>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega, out);
 }
 
-// coarsest: x = Ainv b (ainv column-major n x n, n <= 3 kAmgMaxCoarse), one workgroup
-__global__ __launch_bounds__(kB) void k_coarse_apply(int n, const double *__restrict__ ainv,
-                                                     const double *__restrict__ b,
-                                                     double *__restrict__ x) {
-  __shared__ double bs[kAmgMaxCoarse * 3];
-  for (int j = threadIdx.x; j < n; j += kB) bs[j] = b[j];
+// coarsest: x = Ainv b (ainv column-major n x n, n <= kAmgMaxDense): 64 rows per workgroup, the
+// columns split over 16 lane groups (coalesced column reads), partial sums combined in LDS
+constexpr int kCaRows = 64, kCaParts = 16;
+__global__ __launch_bounds__(kCaRows * kCaParts) void k_coarse_apply(int n,
+                                                                     const double *__restrict__ ainv,
+                                                                     const double *__restrict__ b,
+                                                                     double *__restrict__ x) {
+  __shared__ double bs[kAmgMaxDense];
+  __shared__ double part[kCaParts][kCaRows];
+  for (int j = threadIdx.x; j < n; j += kCaRows * kCaParts) bs[j] = b[j];
   __syncthreads();
-  const int i = threadIdx.x;
-  if (i >= n) return;
-  double s[4] = {0, 0, 0, 0};
-  int j = 0;
-  for (; j + 4 <= n; j += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; u++) s[u] += ainv[size_t(j + u) * n + i] * bs[j + u];
+  const int r = threadIdx.x % kCaRows, q = threadIdx.x / kCaRows;
+  const int i = blockIdx.x * kCaRows + r;
+  double s = 0;
+  if (i < n)
+    for (int j = q; j < n; j += kCaParts) s += ainv[size_t(j) * n + i] * bs[j];
+  part[q][r] = s;
+  __syncthreads();
+  if (q == 0 && i < n) {
+    double t = 0;
+    for (int k = 0; k < kCaParts; k++) t += part[k][r];
+    x[i] = t;
   }
-  for (; j < n; j++) s[0] += ainv[size_t(j) * n + i] * bs[j];
-  x[i] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // (Running the small levels -- pre-smoothing, residual, restriction, coarsest solve,
@@ -513,7 +519,7 @@ hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, dou
 
 hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
                                      const double *v, double *work, double *ainv, hipStream_t s) {
-  if (nb * nf > kAmgMaxCoarse * 3 || (nf != 1 && nf != 3)) return hipErrorInvalidValue;
+  if (nb * nf > kAmgMaxDense || (nf != 1 && nf != 3)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_coarse_inverse, dim3(1), dim3(kGJ), 0, s, nb, nf, rp, col, v, work, ainv);
   return hipGetLastError();
 }
@@ -538,8 +544,9 @@ hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const
 
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s) {
-  if (n > kB || n > kAmgMaxCoarse * 3) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_coarse_apply, dim3(1), dim3(kB), 0, s, n, ainv, b, x);
+  if (n > kAmgMaxDense) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_coarse_apply, dim3((n + kCaRows - 1) / kCaRows), dim3(kCaRows * kCaParts), 0,
+                     s, n, ainv, b, x);
   return hipGetLastError();
 }
 

@@ -134,7 +134,7 @@ bool amg_build(const LocalLayout &L, int coarse_target, int max_levels,
       ap[I + 1] = int(aj.size());
     }
   }
-  if (levels.back().nb > kAmgMaxCoarse * 3) {
+  if (levels.back().nb > kAmgMaxDense) {
     err = "AMG: coarsest level has " + std::to_string(levels.back().nb) +
           " blocks (graph does not coarsen; max levels reached?)";
     return false;

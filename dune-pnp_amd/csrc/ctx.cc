@@ -466,7 +466,7 @@ struct pnp_ctx {
     }
     if (amg_d.empty()) return fail(PNP_E_STATE, "AMG: no owned rows");
     const int K = int(amg_d.size());
-    if (amg_d[K - 1]->nb * nf > pnp::kAmgMaxCoarse * 3)
+    if (amg_d[K - 1]->nb * nf > pnp::kAmgMaxDense)
       return fail(PNP_E_STATE, "AMG: coarsest level too large for the dense solve");
     if (amg_nf != nf) {
       const size_t nb2 = size_t(nf) * nf;
