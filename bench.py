@@ -255,6 +255,9 @@ def main():
     newton_amg = None
     if not args.no_solve and not args.no_amg:
         ctx.amg_configure(smoother=P.PREC_ILU0)  # defaults: omega 0.8, 2 coarse sweeps
+        # warm-up (untimed): first AMG setup loads rocSOLVER's getrf/getri kernels
+        ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=P.PREC_AMG,
+                   linear_maxit=20, maxit=1)
         barrier_sync(dist, world)
         t0 = time.perf_counter()
         _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred,

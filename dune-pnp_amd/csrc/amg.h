@@ -10,10 +10,10 @@
 
 namespace pnp {
 
-// coarsest level: a dense inverse of at most kAmgMaxDense unknowns, i.e. at most kAmgMaxCoarse
-// vertex blocks of 3 fields (170; coarsening stops there, so the same hierarchy serves the
-// scalar and the 3-field operators)
-constexpr int kAmgMaxDense = 512;
+// coarsest level: a dense inverse (rocSOLVER getrf + getri, once per assembly) of at most
+// kAmgMaxDense unknowns, i.e. at most kAmgMaxCoarse vertex blocks of 3 fields (coarsening stops
+// there, so the same hierarchy serves the scalar and the 3-field operators)
+constexpr int kAmgMaxDense = 3072;
 constexpr int kAmgMaxCoarse = kAmgMaxDense / 3;
 constexpr int kAmgMaxLevels = 16;
 
@@ -45,9 +45,9 @@ hipError_t launch_amg_galerkin(int nf, long long nq, const long long *cptr, cons
                                const double *fv, double *cv, hipStream_t s);
 hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, double *dinv,
                            hipStream_t s);
-// work, ainv: (nb*nf)^2 doubles each
-hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
-                                     const double *v, double *work, double *ainv, hipStream_t s);
+// dense (column-major, n = nb*nf, zero-filled here) copy of the coarsest block-CSR matrix
+hipError_t launch_amg_coarse_dense(int nf, int nb, const int *rp, const int *col, const double *v,
+                                   double *dense, hipStream_t s);
 // bn[J] = sum over the members i of aggregate J of (a - sub)_i (sub may be null); xn = omega
 // Dinv_J bn[J] (pre-smoothing from zero; xn null: none)
 hipError_t launch_amg_restrict(int nf, int nbn, const int *mptr, const int *mem, const double *a,

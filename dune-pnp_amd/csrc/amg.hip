@@ -139,105 +139,18 @@ __global__ __launch_bounds__(kB) void k_dinv(int nb, const int *__restrict__ dpo
   for (int k = 0; k < NB; k++) dinv[size_t(i) * NB + k] = X[k];
 }
 
-// coarsest level: ainv (column-major, n = nb * NF) = dense inverse of the block-CSR matrix by
-// Gauss-Jordan with partial pivoting, one workgroup (n <= kAmgMaxDense; the work matrix a is
-// L2-resident).  A singular pivot leaves zeros (the row's unknowns are then not corrected).
-constexpr int kGJ = 1024;
-__global__ __launch_bounds__(kGJ) void k_coarse_inverse(int nb, int nf, const int *__restrict__ rp,
-                                                        const int *__restrict__ col,
-                                                        const double *__restrict__ v,
-                                                        double *__restrict__ a,
-                                                        double *__restrict__ ainv) {
-  const int n = nb * nf, nbb = nf * nf, t = threadIdx.x;
-  __shared__ double fcol[kAmgMaxDense];
-  __shared__ double pv[kGJ / 64];
-  __shared__ int pi[kGJ / 64];
-  __shared__ int piv;
-  // row-major work copy a, identity in ainv (row-major while eliminating, transposed at the end)
-  for (int k = t; k < n * n; k += kGJ) {
-    a[k] = 0.0;
-    ainv[k] = (k / n == k % n) ? 1.0 : 0.0;
-  }
-  __syncthreads();
-  for (int r = t; r < nb; r += kGJ)
-    for (int q = rp[r]; q < rp[r + 1]; q++)
-      for (int e = 0; e < nbb; e++)
-        a[size_t(r * nf + e / nf) * n + col[q] * nf + e % nf] = v[size_t(q) * nbb + e];
-  __syncthreads();
-  for (int k = 0; k < n; k++) {
-    // pivot: argmax |a[i][k]|, i >= k (ties: lowest row)
-    double best = -1.0;
-    int bi = k;
-    for (int i = k + t; i < n; i += kGJ) {
-      const double m = fabs(a[size_t(i) * n + k]);
-      if (m > best) {
-        best = m;
-        bi = i;
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ob > best || (ob == best && oi < bi)) {
-        best = ob;
-        bi = oi;
-      }
-    }
-    if (t % 64 == 0) {
-      pv[t / 64] = best;
-      pi[t / 64] = bi;
-    }
-    __syncthreads();
-    if (t == 0) {
-      double b = pv[0];
-      int p = pi[0];
-      for (int w = 1; w < kGJ / 64; w++)
-        if (pv[w] > b || (pv[w] == b && pi[w] < p)) {
-          b = pv[w];
-          p = pi[w];
-        }
-      piv = p;
-    }
-    __syncthreads();
-    const int p = piv;
-    if (p != k)
-      for (int j = t; j < n; j += kGJ) {
-        double x = a[size_t(k) * n + j];
-        a[size_t(k) * n + j] = a[size_t(p) * n + j];
-        a[size_t(p) * n + j] = x;
-        x = ainv[size_t(k) * n + j];
-        ainv[size_t(k) * n + j] = ainv[size_t(p) * n + j];
-        ainv[size_t(p) * n + j] = x;
-      }
-    __syncthreads();
-    const double d = a[size_t(k) * n + k];
-    const double inv = d != 0.0 ? 1.0 / d : 0.0;
-    for (int i = t; i < n; i += kGJ) fcol[i] = a[size_t(i) * n + k];
-    __syncthreads();
-    for (int j = t; j < n; j += kGJ) {
-      a[size_t(k) * n + j] *= inv;
-      ainv[size_t(k) * n + j] *= inv;
-    }
-    __syncthreads();
-    for (int e = t; e < n * n; e += kGJ) {
-      const int i = e / n, j = e % n;
-      if (i == k) continue;
-      const double f = fcol[i];
-      if (f == 0.0) continue;
-      a[e] -= f * a[size_t(k) * n + j];
-      ainv[e] -= f * ainv[size_t(k) * n + j];
-    }
-    __syncthreads();
-  }
-  // transpose ainv in place to column-major (coalesced GEMV reads)
-  for (int e = t; e < n * n; e += kGJ) {
-    const int i = e / n, j = e % n;
-    if (i < j) {
-      const double x = ainv[e];
-      ainv[e] = ainv[size_t(j) * n + i];
-      ainv[size_t(j) * n + i] = x;
-    }
-  }
+// coarsest level: column-major dense copy of the block-CSR matrix (the inverse is computed by
+// rocSOLVER getrf/getri in place, ctx.cc amg_setup)
+__global__ __launch_bounds__(kB) void k_coarse_dense(int nb, int nf, const int *__restrict__ rp,
+                                                     const int *__restrict__ col,
+                                                     const double *__restrict__ v,
+                                                     double *__restrict__ dense) {
+  const int r = blockIdx.x * kB + threadIdx.x;
+  if (r >= nb) return;
+  const int n = nb * nf, nbb = nf * nf;
+  for (int q = rp[r]; q < rp[r + 1]; q++)
+    for (int e = 0; e < nbb; e++)  // entry (r*nf + e/nf, col*nf + e%nf)
+      dense[size_t(col[q] * nf + e % nf) * n + r * nf + e / nf] = v[size_t(q) * nbb + e];
 }
 
 // ---- V-cycle kernels ------------------------------------------------------------------------
@@ -423,9 +336,10 @@ __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
   jacobi_task<NF, LPR, CORR>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega, out);
 }
 
-// coarsest: x = Ainv b (ainv column-major n x n, n <= kAmgMaxDense): 64 rows per workgroup, the
-// columns split over 16 lane groups (coalesced column reads), partial sums combined in LDS
-constexpr int kCaRows = 64, kCaParts = 16;
+// coarsest: x = Ainv b (ainv column-major n x n, n <= kAmgMaxDense): 16 rows per workgroup, the
+// columns split over 64 lane groups (each reads 128-B row segments of a column), partial sums
+// combined in LDS; n / 16 workgroups (~170 at n = 2772) stream the 61 MB inverse
+constexpr int kCaRows = 16, kCaParts = 64;
 __global__ __launch_bounds__(kCaRows * kCaParts) void k_coarse_apply(int n,
                                                                      const double *__restrict__ ainv,
                                                                      const double *__restrict__ b,
@@ -517,10 +431,12 @@ hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, dou
   return hipGetLastError();
 }
 
-hipError_t launch_amg_coarse_inverse(int nf, int nb, const int *rp, const int *col,
-                                     const double *v, double *work, double *ainv, hipStream_t s) {
-  if (nb * nf > kAmgMaxDense || (nf != 1 && nf != 3)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_coarse_inverse, dim3(1), dim3(kGJ), 0, s, nb, nf, rp, col, v, work, ainv);
+hipError_t launch_amg_coarse_dense(int nf, int nb, const int *rp, const int *col, const double *v,
+                                   double *dense, hipStream_t s) {
+  const size_t n = size_t(nb) * nf;
+  hipError_t e = hipMemsetAsync(dense, 0, sizeof(double) * n * n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_coarse_dense, g1(nb), dim3(kB), 0, s, nb, nf, rp, col, v, dense);
   return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 // device-resident BiCGSTAB (ISTL semantics) and PDELab-semantics Newton, host-orchestrated.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <chrono>
@@ -142,7 +143,9 @@ struct pnp_ctx {
   bool amg_built = false, amg_valid = false;
   int amg_nf = 0;
   double amg_setup_ms = 0;
-  DBuf<double> amg_work, amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
+  DBuf<double> amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
+  DBuf<int> amg_ipiv, amg_info;
+  rocblas_handle blas = nullptr;  // rocSOLVER getrf/getri of the AMG's coarsest level
 
 
   // vectors (sized n_local * 3)
@@ -170,6 +173,7 @@ struct pnp_ctx {
     for (auto e : ev_pool) hipEventDestroy(e);
     if (hS) hipHostFree(hS);
     if (comm) ncclCommDestroy(comm);
+    if (blas) rocblas_destroy_handle(blas);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -481,7 +485,8 @@ struct pnp_ctx {
       }
       const size_t nc = size_t(amg_d[K - 1]->nb) * nf, nl = size_t(L.n_owned + L.n_ghost) * nf;
       hipError_t e;
-      if ((e = amg_work.alloc(nc * nc)) != hipSuccess || (e = amg_ainv.alloc(nc * nc)) != hipSuccess ||
+      if ((e = amg_ainv.alloc(nc * nc)) != hipSuccess || (e = amg_ipiv.alloc(nc)) != hipSuccess ||
+          (e = amg_info.alloc(1)) != hipSuccess ||
           (e = amg_x0.alloc(nl)) != hipSuccess || (e = amg_t.alloc(nl)) != hipSuccess ||
           (e = amg_y.alloc(nl)) != hipSuccess || (e = amg_r.alloc(nl)) != hipSuccess ||
           (e = amg_z.alloc(nl)) != hipSuccess)
@@ -505,10 +510,30 @@ struct pnp_ctx {
       e = pnp::launch_amg_dinv(nf, amg_d[k]->nb, amg_d[k]->dpos.p, amg_d[k]->v.p,
                                amg_d[k]->dinv.p, stream);
     if (e == hipSuccess)
-      e = pnp::launch_amg_coarse_inverse(nf, amg_d[K - 1]->nb, amg_d[K - 1]->rp.p,
-                                         amg_d[K - 1]->col.p, amg_d[K - 1]->v.p, amg_work.p,
-                                         amg_ainv.p, stream);
+      e = pnp::launch_amg_coarse_dense(nf, amg_d[K - 1]->nb, amg_d[K - 1]->rp.p,
+                                       amg_d[K - 1]->col.p, amg_d[K - 1]->v.p, amg_ainv.p, stream);
     if (e != hipSuccess) return hipfail(e, "amg setup");
+    {  // coarsest inverse in place: LU with partial pivoting, then the inverse (column-major)
+      if (!blas) {
+        if (rocblas_create_handle(&blas) != rocblas_status_success)
+          return fail(PNP_E_HIP, "rocblas_create_handle failed");
+      }
+      if (rocblas_set_stream(blas, stream) != rocblas_status_success)
+        return fail(PNP_E_HIP, "rocblas_set_stream failed");
+      const int nc = amg_d[K - 1]->nb * nf;
+      if (rocsolver_dgetrf(blas, nc, nc, amg_ainv.p, nc, amg_ipiv.p, amg_info.p) !=
+              rocblas_status_success ||
+          rocsolver_dgetri(blas, nc, amg_ainv.p, nc, amg_ipiv.p, amg_info.p) !=
+              rocblas_status_success)
+        return fail(PNP_E_HIP, "rocsolver getrf/getri of the AMG coarsest level failed");
+      int info = 0;
+      e = hipMemcpyAsync(&info, amg_info.p, sizeof info, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return hipfail(e, "amg setup");
+      if (info != 0)
+        return fail(PNP_E_STATE, "AMG: coarsest matrix singular (getrf info " +
+                                     std::to_string(info) + ")");
+    }
     te(T_FACT, t0);
     amg_setup_ms = (now_s() - ts) * 1e3;  // host-side issue time (device time: T_FACT timers)
     amg_valid = true;

@@ -486,7 +486,7 @@ class Context:
         self._ck(lib().pnp_prec_apply(self.h, int(prec), _ptr(d), _ptr(v)))
         return v
 
-    def amg_configure(self, smoother=PREC_SSOR, coarse_target=170, max_levels=12, omega=0.8,
+    def amg_configure(self, smoother=PREC_SSOR, coarse_target=1024, max_levels=12, omega=0.8,
                       coarse_sweeps=2, level0_presmooth=-1):
         """Options of PREC_AMG (the reference's CG_AMG_SSOR preconditioner); see pnp_capi.h."""
         o = _AmgOpts(int(smoother), int(coarse_target), int(max_levels), float(omega),

@@ -228,8 +228,9 @@ int pnp_prec_apply(pnp_ctx *ctx, int32_t prec, const double *d, double *v);
  * With PNP_METHOD_CG and smoother SSOR this is CG_AMG_SSOR; it also preconditions BiCGSTAB. */
 typedef struct {
   int32_t smoother;       /* level-0 smoother: PNP_PREC_SSOR (default), PNP_PREC_ILU0, PNP_PREC_JACOBI */
-  int32_t coarse_target;  /* coarsen until at most this many vertex blocks (1..170, default 170:
-                             the coarsest is a dense inverse of <= 512 unknowns) */
+  int32_t coarse_target;  /* coarsen until at most this many vertex blocks (1..1024, default 1024:
+                             the coarsest level is inverted densely, rocSOLVER getrf/getri,
+                             <= 3072 unknowns) */
   int32_t max_levels;     /* levels including the fine one (2..16, default 12) */
   double omega;           /* damped block-Jacobi weight on the coarse levels (default 0.8) */
   int32_t coarse_sweeps;  /* block-Jacobi sweeps per coarse pre-/post-smoothing (1..8, default 2) */
