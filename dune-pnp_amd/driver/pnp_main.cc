@@ -7,7 +7,8 @@
 //                                                 ion current to current.dat)
 //
 // usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb] [--steps n]
-//                 [--prec none|ssor|jacobi|ilu0] [--pb-prec ...] [--device d] [--out prefix]
+//                 [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec ...] [--amg-smoother s]
+//                 [--device d] [--out prefix]
 //                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
@@ -31,13 +32,15 @@ static int prec_of(const std::string &s) {
   if (s == "ssor") return PNP_PREC_SSOR;
   if (s == "jacobi") return PNP_PREC_JACOBI;
   if (s == "ilu0") return PNP_PREC_ILU0;
+  if (s == "amg") return PNP_PREC_AMG;  // level-0 smoother: --amg-smoother (PB: ssor, PNP: ilu0)
   throw pnp_gpu::Error(PNP_E_ARG, "unknown preconditioner " + s);
 }
 
 static void usage() {
   std::printf(
       "usage: pnp_main <config.cfg> [--refine k] [--mesh-scale s] [--mode stationary|instationary|md|pb]\n"
-      "                [--steps n] [--prec none|ssor|jacobi|ilu0] [--pb-prec p] [--device d]\n"
+      "                [--steps n] [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec p] [--device d]\n"
+      "                [--amg-smoother ssor|ilu0|jacobi]\n"
       "                [--out prefix] [--md-reduction r]\n"
       "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n");
 }
@@ -162,6 +165,7 @@ int main(int argc, char **argv) {
     return argc < 2 ? 1 : 0;
   }
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
+  std::string amg_smoother;  // empty: SSOR for the PB phase, ILU(0) for the PNP phases
   int refine = 0, steps = -1, device = -1;
   double mesh_scale = 1.0;  // size scale when the mesh comes from a .geo (gmsh -clscale)
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
@@ -179,6 +183,7 @@ int main(int argc, char **argv) {
     else if (a == "--steps") steps = std::atoi(next().c_str());
     else if (a == "--prec") prec = next();
     else if (a == "--pb-prec") pb_prec = next();
+    else if (a == "--amg-smoother") amg_smoother = next();
     else if (a == "--device") device = std::atoi(next().c_str());
     else if (a == "--out") out = next();
     else if (a == "--md-reduction") md_reduction = std::atof(next().c_str());
@@ -225,6 +230,10 @@ int main(int argc, char **argv) {
     pnp_gpu::GridOperator<V> pbgo(ctx, pblop);
     pnp_gpu::BiCGStabBackend<V> pbls(ctx, s.cfg.linear_solver_iterations, prec_of(pb_prec),
                                      rank == 0 ? s.cfg.verbosity : 0);
+    auto amg_for = [&](const char *dflt) {  // PNP_PREC_AMG's level-0 smoother for a phase
+      ctx.amg_configure(prec_of(amg_smoother.empty() ? std::string(dflt) : amg_smoother));
+    };
+    if (pb_prec == "amg") amg_for("ssor");
     V pbu(nv, 0.0);
     pnp_gpu::Newton<V> pbnewton(pbgo, pbu, pbls);
     pbnewton.setReduction(s.cfg.newton_reduction);
@@ -247,6 +256,7 @@ int main(int argc, char **argv) {
     pnp_gpu::check(pnp_initial_state(ctx.get(), pbu.data(), u.data()), ctx.get());
     pnp_gpu::BiCGStabBackend<V> ls(ctx, s.cfg.linear_solver_iterations, prec_of(prec),
                                    rank == 0 ? s.cfg.verbosity : 0);
+    if (prec == "amg") amg_for("ilu0");
     auto configure = [&](pnp_gpu::Newton<V> &nw) {
       nw.setReduction(s.cfg.newton_reduction);
       nw.setMinLinearReduction(s.cfg.newton_min_linear_reduction);

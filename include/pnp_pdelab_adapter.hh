@@ -121,6 +121,12 @@ class Context {
   void sync(V &v, int nfields) const {
     check(pnp_sync_vector(ctx_, data(v), nfields), ctx_);
   }
+  // PNP_PREC_AMG options (ISTLBackend_NOVLP_CG_AMG_SSOR's AMG; defaults: SSOR smoother)
+  void amg_configure(int smoother = PNP_PREC_SSOR, int coarse_target = 1024, int max_levels = 12,
+                     double omega = 0.8, int coarse_sweeps = 2, int level0_presmooth = -1) {
+    pnp_amg_opts o{smoother, coarse_target, max_levels, omega, coarse_sweeps, level0_presmooth};
+    check(pnp_amg_configure(ctx_, &o), ctx_);
+  }
 
  private:
   pnp_ctx *ctx_ = nullptr;

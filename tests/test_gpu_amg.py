@@ -182,3 +182,20 @@ def test_amg_newton_pnp_matches_ilu0_newton():
     assert ra["converged"] == 1 and ri["converged"] == 1
     assert ra["linear_fallbacks"] == 0 and ri["linear_fallbacks"] == 0
     assert np.max(np.abs(ua - ui)) <= 1e-6 * np.max(np.abs(ui))
+
+
+def test_cpp_driver_amg_matches_ilu0(tmp_path):
+    """pnp_main --prec amg --pb-prec amg (the C++ driver over the PDELab-shaped adapter) reaches
+    the same stationary PNP state as the ILU(0) run."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    outs = {}
+    for prec in ("amg", "ilu0"):
+        out = subprocess.run([exe, cfgp, "--refine", "1", "--prec", prec, "--pb-prec", prec,
+                              "--out", str(tmp_path / prec)],
+                             capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stdout + out.stderr
+        outs[prec] = np.loadtxt(tmp_path / f"{prec}_pnp.dat")
+    scale = np.max(np.abs(outs["ilu0"]))
+    assert np.max(np.abs(outs["amg"] - outs["ilu0"])) <= 1e-6 * scale
