@@ -603,6 +603,8 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
     else if (!fanr)                                                                \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
+    else if (!a.jac && fanr == 9 && ga)                                            \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9>), grid, block, 0, s, L, a);  \
     else if (!a.jac)                                                               \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, L, a);    \
     else if (ga == 1 && fanr == 9)                                                 \

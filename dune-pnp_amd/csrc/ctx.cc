@@ -1789,10 +1789,11 @@ extern "C" int pnp_state_get(pnp_ctx *c, double *x) {
 }
 
 extern "C" int pnp_assemble_state(pnp_ctx *c, int32_t n) {
-  if (!c || n < 0) return PNP_E_ARG;
+  if (!c) return PNP_E_ARG;
   hipSetDevice(c->device);
-  for (int k = 0; k < n; k++) {
-    int rc = c->assemble(c->x.p, 1);
+  const int jac = n >= 0 ? 1 : 0;  // n < 0: |n| residual-only assemblies (line-search kernel)
+  for (int k = 0; k < (n >= 0 ? n : -n); k++) {
+    int rc = c->assemble(c->x.p, jac);
     if (rc) return rc;
   }
   CK(hipStreamSynchronize(c->stream), "assemble_state");

@@ -30,6 +30,13 @@ for rep in range(10):
     ctx.assemble_state(20)
     t = ctx.timers(enable=False)
     res.append(t["assemble_ms"] / t["assemble_launches"] * 1e3)
+resid = []
+for rep in range(5):
+    ctx.timers(enable=True, reset=True)
+    ctx.assemble_state(-20)
+    t = ctx.timers(enable=False)
+    resid.append(t["assemble_ms"] / t["assemble_launches"] * 1e3)
+ctx.assemble_state(1)
 ctx.timers(enable=True, reset=True)
 ctx.bicgstab_iterations(20, P.PREC_SSOR)
 t = ctx.timers(enable=False)
@@ -44,7 +51,7 @@ for rep in range(5):
 knobs = " ".join(f"{k[4:].lower()}={v}" for k, v in sorted(os.environ.items())
                  if k.startswith("PNP_") and k != "PNP_AMD_LIB")
 print(f"{knobs or 'default'} jac={jh} assemble_us median={np.median(res):.2f} "
-      f"min={np.min(res):.2f}  spmv_us={t['spmv_ms'] / t['spmv_launches'] * 1e3:.2f} "
+      f"min={np.min(res):.2f} residual_only_us={np.median(resid):.2f}  spmv_us={t['spmv_ms'] / t['spmv_launches'] * 1e3:.2f} "
       f"sgs_apply_us={t['prec_ms'] / t['prec_launches'] * 1e3:.2f} "
       f"ilu_apply_us={np.median(ilu):.2f} ilu_bicgstab_us_per_it={np.median(iltot):.1f} "
       f"blas_ms_per_it={t['blas_ms'] / 20:.4f}")
