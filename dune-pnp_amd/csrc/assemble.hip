@@ -377,9 +377,11 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 // above keeps ~1 element of loads in flight), and the block stores of the walk never sit in front
 // of a load the walk still waits for.  Same element() calls with the same operands in the same
 // order as k_assemble (the compiler's FMA contraction may still differ in the last bit).  Fans of
-// at most FANR - 1 neighbours.  Config 3: 76.5 -> 72.2 us at 2 waves/SIMD (180 VGPRs); at 3 waves
-// it spills (80.8 us) and a split gather (slots 1-4 first) ties at 72.9 us
-// (profiles/r01/ab_asm_gather_all.log).
+// at most FANR - 1 neighbours.  Rows come in the spatial block order (row_block, DevLayout::
+// blkmap), so an XCD's rows share the neighbours they gather in its L2.  Config 3: pipelined walk
+// 76.5 us; gather-all at 2 waves/SIMD (180 VGPRs) 72.2 us, with the block map 58.5 us; slots 1-5
+// first and 6-8 after element 4 (SPLIT 6) fits 3 waves in 160 VGPRs: 54.5 us
+// (profiles/r01/ab_asm_gather_all.log, ab_blkmap_gather_all.log, ab_asm_ga_split_blkmap.log).
 // SPLIT < FANR: only slots 1 .. SPLIT-1 are gathered up front; the rest are issued after element
 // SPLIT-2, when the first elements' neighbour registers are free again (fewer live VGPRs).
 template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR>
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   constexpr int NF = T::NF, NK = T::NK, NS = FANR;
   constexpr bool AUX0 = OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON;
   constexpr bool AUX1 = OP == OP_POISSON;
-  const int row = xcd_block(blockIdx.x, gridDim.x, L.xcd_remap) * blockDim.x + threadIdx.x;
+  const int row = row_block(L, blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = L.chunk_off[chunk];
@@ -589,10 +591,11 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     return !(e && atoi(e) == 0);
   }();
   // A/B knob PNP_ASM_GA: 0 = the pipelined walk (k_assemble), 1 = gather-all at 3 waves/SIMD
-  // (spills), 2 = gather-all at 2 waves (default), 3 = gather 4 neighbours first at 3 waves
+  // (spills), 2 = gather-all at 2 waves, 3 / 4 / 5 = gather slots 1-4 / 1-5 / 1-2 first and the
+  // rest two elements later at 3 waves; 4 is the default (profiles/r01/ab_asm_ga_*.log)
   static const int ga = [] {
     const char *e = getenv("PNP_ASM_GA");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;
   }();
   // column indices in registers: FANR - 1 >= the longest fan (max_slots - 1; 8 on all meshes
   // seen), 12 as the general case, 0 (index loads in the walk) beyond
@@ -613,6 +616,10 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
+    else if (ga == 4 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, L, a); \
+    else if (ga == 5 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 3>), grid, block, 0, s, L, a); \
     else if (fanr == 12)                                                           \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
     else if (waves == 3)                                                           \

@@ -1159,11 +1159,13 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
     g_err = c->err;
     return rc;
   }
-  {  // spatial block order (DevLayout::blkmap).  It paid 4 us of SpMV while the matrix streams
-     // went through the caches; with non-temporal matrix streams it costs ~1 us
-     // (profiles/r01/ab_blkmap_nt.log), so it is off unless PNP_BLKMAP=1
+  {  // spatial block order (DevLayout::blkmap) for the whole-matrix kernels (assembly, SpMV):
+     // each XCD takes one spatial slice of every colour, so the neighbour gathers of its rows
+     // share its L2.  With the gather-all assembly it pays 72.7 -> 58.8 us (the pipelined walk
+     // was latency-bound and did not see it; SpMV and sweeps neutral,
+     // profiles/r01/ab_blkmap_gather_all.log).  PNP_BLKMAP=0 turns it off (A/B)
     const char *e = getenv("PNP_BLKMAP");
-    if (e && atoi(e) == 1 && L.n_owned > 0) {
+    if (!(e && atoi(e) == 0) && L.n_owned > 0) {
       int nblk = (L.n_owned + 255) / 256;
       std::vector<double> key(nblk);
       for (int b = 0; b < nblk; b++) {
