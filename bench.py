@@ -158,6 +158,8 @@ def main():
                     help="skip the time-to-solution PNP Newton after the timed regions")
     ap.add_argument("--no-amg", action="store_true",
                     help="skip the AMG-preconditioned time-to-solution leg")
+    ap.add_argument("--amg-multi", action="store_true",
+                    help="run the AMG time-to-solution leg at N>1 too (default: N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-refine", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
@@ -253,7 +255,8 @@ def main():
     # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB:
     # fewer, dearer iterations (reported beside the metric; the metric stays on --prec)
     newton_amg = None
-    if not args.no_solve and not args.no_amg:
+    # (N=1 only unless --amg-multi: the scaling runs time the metric, not this leg)
+    if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
         ctx.amg_configure(smoother=P.PREC_ILU0)  # defaults: omega 0.8, 2 coarse sweeps
         # warm-up (untimed): first AMG setup loads rocSOLVER's getrf/getri kernels
         ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=P.PREC_AMG,

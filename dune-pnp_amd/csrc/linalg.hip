@@ -973,7 +973,7 @@ static int sweep_cfg() {
     int l = 1, b = 4;
     if (e && std::sscanf(e, "%dx%d", &l, &b) != 2) l = 1, b = 4;
     const int code = l * 16 + b;
-    return (code == 18 || code == 34 || code == 36) ? code : 20;
+    return (code == 18 || code == 34 || code == 36 || code == 24 || code == 40) ? code : 20;
   }();
   return v;
 }
@@ -994,6 +994,14 @@ static bool sweep_nt() {  // default on: ILU0 apply -7 %, SGS -7 % (profiles/r01
       } break;                                     \
       case 34: {                                   \
         constexpr int LPRc = 2, Bc = 2, NTc = 0;   \
+        CALL;                                      \
+      } break;                                     \
+      case 24: {                                   \
+        constexpr int LPRc = 1, Bc = 8, NTc = 1;   \
+        CALL;                                      \
+      } break;                                     \
+      case 40: {                                   \
+        constexpr int LPRc = 2, Bc = 8, NTc = 1;   \
         CALL;                                      \
       } break;                                     \
       case 36: {                                   \

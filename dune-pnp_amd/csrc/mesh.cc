@@ -597,25 +597,77 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
     }
     return true;
   };
+  // Kempe interchange: when the bounded chains above fail for a top-colour vertex v, look for
+  // two colours a, b below the top such that the (a,b)-component grown from v's a-neighbours
+  // contains none of v's b-neighbours; swapping a<->b in that component frees colour a at v.
+  // Components larger than PNP_KEMPE_CAP vertices are abandoned (0 turns this off).
+  const char *kc_env = std::getenv("PNP_KEMPE_CAP");
+  const int kempe_cap = kc_env ? std::atoi(kc_env) : 4096;
+  std::vector<int> kstamp(nv, 0), kmark(nv, 0), kcomp, kstack;
+  int kepoch = 0;
+  auto kempe = [&](int v, int top) -> bool {
+    for (int a = 0; a < top; a++)
+      for (int b = 0; b < top; b++) {
+        if (a == b) continue;
+        ++kepoch;
+        kcomp.clear();
+        kstack.clear();
+        for (int k = f.ptr[v]; k < f.ptr[v + 1]; k++) {
+          const int u = f.nbr[k];
+          if (!owned_nbr(u)) continue;
+          if (color[u] == b) kmark[u] = kepoch;
+          if (color[u] == a && kstamp[u] != kepoch) {
+            kstamp[u] = kepoch;
+            kstack.push_back(u);
+          }
+        }
+        bool ok = true;
+        while (!kstack.empty() && ok) {
+          const int x = kstack.back();
+          kstack.pop_back();
+          kcomp.push_back(x);
+          if (int(kcomp.size()) > kempe_cap) ok = false;
+          for (int k = f.ptr[x]; k < f.ptr[x + 1] && ok; k++) {
+            const int y = f.nbr[k];
+            if (y == v || !owned_nbr(y) || kstamp[y] == kepoch) continue;
+            if (color[y] != a && color[y] != b) continue;
+            if (kmark[y] == kepoch) ok = false;  // reaches a b-neighbour of v
+            kstamp[y] = kepoch;
+            kstack.push_back(y);
+          }
+        }
+        if (!ok) continue;
+        for (int x : kcomp) color[x] = color[x] == a ? b : a;
+        color[v] = a;
+        return true;
+      }
+    return false;
+  };
   while (recolor && ncolors > 1) {
     const int top = ncolors - 1;
     int left = 0, ntop = 0;
     for (int v : owned) ntop += color[v] == top;
     if (ntop * 16 > int(owned.size())) break;
-    for (int v : owned) {
-      if (color[v] != top) continue;
-      bool moved = false;
-      for (int c = 0; c < top && !moved; c++) {
-        const size_t mark = undo.size();
-        setc(v, c);
-        if (fix(v, top, recolor_depth)) {
-          moved = true;
-        } else {
-          rollback(mark);
+    // repeated passes: the moves of one pass open room for vertices that failed earlier
+    for (int pass = 0, prev = ntop; pass < 16; pass++, prev = left) {
+      left = 0;
+      for (int v : owned) {
+        if (color[v] != top) continue;
+        bool moved = false;
+        for (int c = 0; c < top && !moved; c++) {
+          const size_t mark = undo.size();
+          setc(v, c);
+          if (fix(v, top, recolor_depth)) {
+            moved = true;
+          } else {
+            rollback(mark);
+          }
         }
+        undo.clear();
+        if (!moved && kempe_cap > 0) moved = kempe(v, top);
+        if (!moved) left++;
       }
-      undo.clear();
-      if (!moved) left++;
+      if (left == 0 || left == prev) break;
     }
     if (left > 0) break;
     ncolors--;

@@ -295,7 +295,8 @@ def test_multicolour_ssor_diverges_where_natural_order_converges():
     """Why the GPU test on config 5's geometry uses ILU(0): on the first PNP Newton system of
     test/pore_without_dna (meshed natively, refined once) ISTL SSOR(k=1, w=1) in the file's
     vertex order converges, but the same SSOR in the multicolour vertex-blocked order the GPU
-    sweeps use (pnp_layout: colour-major, fields inside a vertex) diverges -- Gauss-Seidel on a
+    sweeps use (pnp_layout: colour-major, fields inside a vertex) does not converge in 2000
+    iterations (it diverges or stalls, depending on the colouring) -- Gauss-Seidel on a
     drift-dominated non-symmetric system depends on the order.  ILU(0) in that order converges
     with ~25 % more iterations than in the natural order.  All on the oracle (CPU)."""
     import pnp_amd as P
@@ -317,7 +318,7 @@ def test_multicolour_ssor_diverges_where_natural_order_converges():
     _, ilu_nat = O.bicgstab(J, r, prec=O.PREC_ILU0, reduction=1e-8)
     _, ilu_mc = O.bicgstab(Jp, r[perm], prec=O.PREC_ILU0, reduction=1e-8)
     assert nat.converged == 1
-    assert mc.converged == 0 and mc.reduction > 1.0
+    assert mc.converged == 0 and mc.reduction > 1e-3
     assert ilu_nat.converged == 1 and ilu_mc.converged == 1
     assert ilu_mc.iterations < 1.5 * ilu_nat.iterations
 
