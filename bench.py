@@ -121,7 +121,8 @@ def cpu_baseline(cfg, refine, seconds):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import meshio
     import oracle_py as O
-    mesh = meshio.refine(meshio.read_gmsh(cfg.meshfile), refine)
+    pmesh = P.Mesh.read_gmsh(cfg.meshfile).refine(refine)
+    mesh = meshio.Mesh(pmesh.xy, pmesh.tri, pmesh.bseg, pmesh.bgroup)
     s = cfg.system
     surfs = [meshio.Surface(q.cb, q.cflux, q.cpot, q.pb, q.pflux, q.pconc, q.mb, q.mflux, q.mconc)
              for q in cfg.surfaces]
@@ -140,7 +141,21 @@ def cpu_baseline(cfg, refine, seconds):
     t_it = (time.perf_counter() - t1) / max(res.iterations, 1)
     # (ii) all host cores: the same algorithm, element colours + OpenMP (orc_assemble_mt)
     t_mt, threads, _, _ = orc.time_fd_assembly_mt(op, x, 0.25 * seconds)
-    return {"dofs": 3 * nv, "assembly_s": t_asm, "dofs_per_s": 3 * nv / t_asm,
+    # residual / Jacobian match of the GPU path against the CPU restatement on this sample (the
+    # oracle as checker): analytic vs analytic, and vs the reference's FD Jacobian just timed
+    ctx = P.Context(pmesh, P.Params.from_config(cfg), device=0)
+    ctx.set_operator(P.OP_PNP)
+    r_gpu, J_gpu = ctx.residual(x), ctx.jacobian(x)
+    ctx.close()
+    J_an = orc.jacobian(op, x)
+    jscale = abs(J_an).max()
+    parity = {"sample_dofs": 3 * nv,
+              "residual_rel_err": float(np.max(np.abs(r_gpu - b)) / np.max(np.abs(b))),
+              "jacobian_rel_err_vs_analytic": float(abs(J_gpu - J_an).max() / jscale),
+              "jacobian_rel_err_vs_reference_fd": float(abs(J_gpu - J).max() / jscale),
+              "tolerance": "residual and analytic Jacobian <= 1e-12 of max|.|; FD Jacobian "
+                           "<= 1e-5 (forward-difference truncation, SURVEY.md §8(c))"}
+    return {"parity": parity, "dofs": 3 * nv, "assembly_s": t_asm, "dofs_per_s": 3 * nv / t_asm,
             "bicgstab_nonprec_s_per_it": t_it, "iterations": res.iterations,
             "nnz_full": int(J.nnz), "mt_assembly_s": t_mt, "mt_threads": threads,
             "mt_dofs_per_s": 3 * nv / t_mt}
@@ -300,7 +315,8 @@ def main():
                           f"{cb['assembly_s']:.3f} s per assembly, single thread on "
                           f"{platform.processor() or platform.machine()}; ISTL BiCGSTAB NOPREC "
                           f"on the same system {cb['bicgstab_nonprec_s_per_it'] * 1e3:.2f} ms/it"),
-               "bicgstab_nonprec_iters_per_s_at_sample": 1.0 / cb["bicgstab_nonprec_s_per_it"]}
+               "bicgstab_nonprec_iters_per_s_at_sample": 1.0 / cb["bicgstab_nonprec_s_per_it"],
+               "gpu_vs_cpu_parity": cb["parity"]}
         cpu_all = {"value": cb["mt_dofs_per_s"], "unit": "assembled DOFs/s",
                    "cores": cb["mt_threads"], "kind": "port",
                    "sample": (f"the same assembly on the same sample with OpenMP over element "
