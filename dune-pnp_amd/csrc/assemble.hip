@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 // (profiles/r01/ab_asm_gather_all.log, ab_blkmap_gather_all.log, ab_asm_ga_split_blkmap.log).
 // SPLIT < FANR: only slots 1 .. SPLIT-1 are gathered up front; the rest are issued after element
 // SPLIT-2, when the first elements' neighbour registers are free again (fewer live VGPRs).
-template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR>
+template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR, int STAGE = 0>
 __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
   constexpr int NF = T::NF, NK = T::NK, NS = FANR;
@@ -426,11 +426,36 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   for (int f = 0; f < NF; f++) R[f] = 0;
 #pragma unroll
   for (int v = 0; v < NK; v++) D[v] = P[v] = F[v] = 0;
+  // STAGE: blocks finished before the second-half gathers are issued (slots 1 .. SPLIT-3) wait
+  // in LDS and go out right after those gathers: vmcnt retires loads and stores in issue order,
+  // so a gather issued behind a store also waits for the store (A/B knob PNP_ASM_GA=6)
+  constexpr int NSTG = (STAGE && JAC && SPLIT < NS && SPLIT > 3) ? SPLIT - 3 : 0;
+  __shared__ double stg[NSTG > 0 ? NSTG * NK * 256 : 1];
+  unsigned staged = 0;
+  auto put = [&](int s, const double *Kc) {
+    if (NSTG > 0 && s <= NSTG) {
+#pragma unroll
+      for (int v = 0; v < NK; v++) stg[((s - 1) * NK + v) * 256 + threadIdx.x] = Kc[v];
+      staged |= 1u << s;
+    } else {
+      store_block<OP>(vc, lane, s, Kc);
+    }
+  };
 #pragma unroll
   for (int s = 1; s < NS; s++) {
     if (SPLIT < NS && s == (SPLIT > 2 ? SPLIT - 2 : 1)) {
 #pragma unroll
       for (int k = SPLIT; k < NS; k++) gather(k);
+      if constexpr (NSTG > 0) {
+#pragma unroll
+        for (int q = 1; q <= NSTG; q++)
+          if ((staged >> q) & 1) {
+            double K[NK];
+#pragma unroll
+            for (int v = 0; v < NK; v++) K[v] = stg[((q - 1) * NK + v) * 256 + threadIdx.x];
+            store_block<OP>(vc, lane, q, K);
+          }
+      }
     }
     if (s < len) {
       const bool has_next = s + 1 < len;
@@ -455,13 +480,13 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
 #pragma unroll
             for (int v = 0; v < NK; v++) F[v] = P[v];
           } else {
-            store_block<OP>(vc, lane, s, P);
+            put(s, P);
           }
 #pragma unroll
           for (int v = 0; v < NK; v++) P[v] = Ct[v];
         }
       } else if constexpr (JAC) {
-        store_block<OP>(vc, lane, s, P);
+        put(s, P);
 #pragma unroll
         for (int v = 0; v < NK; v++) P[v] = 0;
       }
@@ -620,6 +645,8 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, L, a); \
     else if (ga == 5 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 3>), grid, block, 0, s, L, a); \
+    else if (ga == 6 && fanr == 9)                                                 \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 1>), grid, block, 0, s, L, a); \
     else if (fanr == 12)                                                           \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
     else if (waves == 3)                                                           \
