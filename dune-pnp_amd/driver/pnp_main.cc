@@ -42,7 +42,8 @@ static void usage() {
       "                [--steps n] [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec p] [--device d]\n"
       "                [--amg-smoother ssor|ilu0|jacobi]\n"
       "                [--out prefix] [--md-reduction r]\n"
-      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n");
+      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
+      "                [--abs-limit a] [--dump-steps n1,n2,...]\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -169,6 +170,10 @@ int main(int argc, char **argv) {
   int refine = 0, steps = -1, device = -1;
   double mesh_scale = 1.0;  // size scale when the mesh comes from a .geo (gmsh -clscale)
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
+  // Newton absolute limit (PDELab NewtonTerminate abs_limit, default 1e-12 as in PDELab); the
+  // instationary run needs it above the residual's rounding floor
+  double abs_limit = 1e-12;
+  std::vector<int> dump_steps;  // instationary: write the state after these steps (1-based)
   // md mode: PbLS, the compile-time LINEARSOLVER of src/instationary_pnp_from_pb_md.hh:20-32,188-211
   std::string linsolver = "bcgs_ssork";
   for (int i = 2; i < argc; i++) {
@@ -188,7 +193,16 @@ int main(int argc, char **argv) {
     else if (a == "--out") out = next();
     else if (a == "--md-reduction") md_reduction = std::atof(next().c_str());
     else if (a == "--linear-solver") linsolver = next();
-    else {
+    else if (a == "--abs-limit") abs_limit = std::atof(next().c_str());
+    else if (a == "--dump-steps") {
+      std::string l = next();
+      for (size_t p = 0; p < l.size();) {
+        size_t q = l.find(',', p);
+        if (q == std::string::npos) q = l.size();
+        dump_steps.push_back(std::atoi(l.substr(p, q - p).c_str()));
+        p = q + 1;
+      }
+    } else {
       usage();
       return 1;
     }
@@ -262,6 +276,7 @@ int main(int argc, char **argv) {
       nw.setMinLinearReduction(s.cfg.newton_min_linear_reduction);
       nw.setMaxIterations(s.cfg.newton_max_iterations);
       nw.setLineSearchMaxIterations(s.cfg.newton_line_search_max_iteration);
+      nw.setAbsoluteLimit(abs_limit);
       nw.setVerbosityLevel(rank == 0 ? 1 : 0);
     };
     int status = 0;
@@ -278,6 +293,7 @@ int main(int argc, char **argv) {
       }
     } else if (mode == "instationary") {  // :409-431, implicit Euler, dt = tau
       int n = steps > 0 ? steps : 100;
+      if (!out.empty() && rank == 0) write_vector(out + "_x0.dat", u, nv);
       for (int i = 0; i < n; i++) {
         if (i > 0) ctx.sync(u, 3);
         V uold = u;
@@ -299,6 +315,12 @@ int main(int argc, char **argv) {
           std::printf("step %d t=%g newton it %d (linear %d) defect %.3e\n", i, (i + 1) * s.cfg.tau,
                       newton.result().iterations, newton.result().linear_iterations,
                       newton.result().defect);
+        if (std::find(dump_steps.begin(), dump_steps.end(), i + 1) != dump_steps.end()) {
+          V g = u;
+          ctx.sync(g, 3);
+          if (!out.empty() && rank == 0)
+            write_vector(out + "_step" + std::to_string(i + 1) + ".dat", g, nv);
+        }
       }
     } else if (mode == "md") {  // src/instationary_pnp_from_pb_md.hh:295-454
       if (!out.empty() && rank == 0) write_vector(out + "_x0.dat", u, nv);
