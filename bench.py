@@ -15,9 +15,21 @@ recorded on the library's own stream around every assembly launch; `roofline.tra
 HBM-side byte count per launch of the same kernel from rocprofv3 PMC passes (FETCH_SIZE x2 +
 WRITE_SIZE, tools/pmc_summary.py), read from the committed profiles/<round>/pmc_summary.json.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling -- the mesh is N mirrored
-copies of the pore glued at their outflow/inflow planes, partitioned by RCB (one copy per GPU),
-with RCCL halo exchange per SpMV and allreduce per BiCGSTAB reduction.
+Beside the warm (back-to-back) assembly the line carries a cache-cold one: 1 GiB of scratch is
+read between launches, so the matrix is not re-dirtied inside the 256 MiB Infinity Cache
+(`roofline_cold`).  The BiCGSTAB line carries two byte models: the contract's CSR bytes
+ and the bytes the stored formats move (k-form SELL values + one column index
+per slot, split L/U factors), per kernel class, so every `frac` is <= 1 on its own model.
+
+Multi-GPU (torch.distributed.run, one rank per GPU):
+  * the primary line (`--scaling weak`, the default): the mesh is N mirrored copies of the pore
+    glued at their outflow/inflow planes, partitioned by RCB (one copy per GPU), with RCCL halo
+    exchange per SpMV and allreduce per BiCGSTAB reduction;
+  * the `strong_scaling` object (config 5, BASELINE.json configs[4], the north star's ~10M-DOF
+    system): test/pore_without_dna/pore_without_dna.geo meshed natively (scale 0.85), refined
+    k=6 (8.87 M DOF), ONE mesh RCB-split over the N ranks (src/pnp_solver_main.cc:106-108
+    loadBalance), run at every N (N=1 included: its single-GPU, past-the-Infinity-Cache rates).
+    `--scaling strong` makes it the primary line.
 """
 import argparse
 import json
@@ -32,14 +44,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
 import pnp_amd as P  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6290
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured copy rate is in
+#                       the line (`measured_copy_gbs`)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
+SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
 
 
 def pmc_traffic(kernel_prefix):
     """Per-launch HBM-side bytes of a kernel from the committed rocprofv3 PMC summary, or None."""
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(PMC_SUMMARY if os.path.exists(PMC_SUMMARY)
+                  else PMC_SUMMARY.replace("r02", "r01")) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
@@ -133,14 +148,21 @@ def cpu_baseline(cfg, refine, seconds):
     x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
                         0.06 * rng.uniform(0.5, 1.5, nv)])
     op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
-    t_asm, J = orc.time_fd_assembly(op, x, 0.6 * seconds)
+    t_asm, J = orc.time_fd_assembly(op, x, 0.5 * seconds)
     b = orc.residual(op, x)
-    it_budget = max(5, int(0.4 * seconds / max(t_asm / 20, 1e-4)))
+    # ISTL BiCGSTAB NOPREC (the reference's stationary backend) on the assembled system: a fixed
+    # number of iterations (reduction 1e-30 never stops it), single thread, then all host cores
+    # (OpenMP row-parallel SpMV / dots / updates, orc_set_parallel)
     t1 = time.perf_counter()
-    _, res = O.bicgstab(J, b, prec=O.PREC_NONE, reduction=1e-30, maxit=min(it_budget, 2000))
+    _, res = O.bicgstab(J, b, prec=O.PREC_NONE, reduction=1e-30, maxit=8)
     t_it = (time.perf_counter() - t1) / max(res.iterations, 1)
+    O.lib().orc_set_parallel(1)
+    t1 = time.perf_counter()
+    _, res_mt = O.bicgstab(J, b, prec=O.PREC_NONE, reduction=1e-30, maxit=16)
+    t_it_mt = (time.perf_counter() - t1) / max(res_mt.iterations, 1)
+    O.lib().orc_set_parallel(0)
     # (ii) all host cores: the same algorithm, element colours + OpenMP (orc_assemble_mt)
-    t_mt, threads, _, _ = orc.time_fd_assembly_mt(op, x, 0.25 * seconds)
+    t_mt, threads, _, _ = orc.time_fd_assembly_mt(op, x, 0.2 * seconds)
     # residual / Jacobian match of the GPU path against the CPU restatement on this sample (the
     # oracle as checker): analytic vs analytic, and vs the reference's FD Jacobian just timed
     ctx = P.Context(pmesh, P.Params.from_config(cfg), device=0)
@@ -157,8 +179,142 @@ def cpu_baseline(cfg, refine, seconds):
                            "<= 1e-5 (forward-difference truncation, SURVEY.md §8(c))"}
     return {"parity": parity, "dofs": 3 * nv, "assembly_s": t_asm, "dofs_per_s": 3 * nv / t_asm,
             "bicgstab_nonprec_s_per_it": t_it, "iterations": res.iterations,
+            "bicgstab_nonprec_s_per_it_mt": t_it_mt,
             "nnz_full": int(J.nnz), "mt_assembly_s": t_mt, "mt_threads": threads,
             "mt_dofs_per_s": 3 * nv / t_mt}
+
+
+def measured_copy_gbs(device):
+    """Device copy rate (read + write bytes / s) of a 1 GiB buffer, past the Infinity Cache."""
+    import torch
+    n = (1 << 30) // 8
+    a = torch.empty(n, dtype=torch.float64, device=f"cuda:{device}").fill_(1.0)
+    b = torch.empty_like(a)
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * n * 8 * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def byte_models(info, nf, N_local, T_local, prec):
+    """Per-launch bytes: SURVEY.md §8(d) contract (reduced CSR) and the stored formats."""
+    V = info["nv_owned"]
+    nnz_red = info["nvb"] * info["nblocks"]
+    n_loc = nf * (info["nv_owned"] + info["nv_ghost"])
+    B_asm = 8 * nnz_red + 16 * N_local + 12 * T_local + 16 * V
+    pre = prec != P.PREC_NONE
+    B_it = (48 if pre else 24) * nnz_red + (304 if pre else 232) * N_local
+    # stored formats: SpMV = k-form values + a 4-B column index per slot, x gathered once, y
+    # written, the fused dot's operand read
+    spmv = info["nslots"] * (8 * info["nks"] + 4) + 8 * n_loc + 16 * N_local
+    # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
+    # written, re-read by the backward sweep (gathers counted once), v written
+    ilu = (info["lslots"] + info["uslots"]) * (8 * info["nvb"] + 4) + 8 * (N_local + 3 * n_loc)
+    blas = 192 * N_local  # ~24 vector passes per iteration (the contract's figure)
+    return {"asm": B_asm, "it_contract": B_it, "spmv_stored": spmv, "ilu_stored": ilu,
+            "blas": blas, "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}
+
+
+def make_context(mesh, cfg, rank, world, local, dist):
+    uid = None
+    if world > 1:
+        obj = [P.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+    ctx = P.Context(mesh, P.Params.from_config(cfg), device=local, rank=rank, size=world,
+                    unique_id=uid)
+    # Boltzmann initial state: PB Newton, then the BCExtension interpolation
+    t_setup = time.perf_counter()
+    ctx.set_operator(P.OP_PB)
+    pb_prec = P.PREC_ILU0 if "without_dna" in cfg.meshfile else P.PREC_SSOR
+    phi_pb, pb_res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=pb_prec,
+                                linear_maxit=20000)
+    phi_pb = ctx.sync_vector(phi_pb, 1)  # each rank returns its owned entries; combine
+    x0 = ctx.initial_state(phi_pb)
+    ctx.set_operator(P.OP_PNP)
+    ctx.state_set(x0)
+    return ctx, x0, pb_res, time.perf_counter() - t_setup
+
+
+def measure(ctx, mesh, args, prec, dist, world):
+    """Timed regions on one context: warm assembly (the metric), BiCGSTAB, then the event-timed
+    passes (warm, cache-cold) the rooflines are computed from."""
+    info = ctx.info()
+    ctx.assemble_state(args.warmup)
+    ctx.bicgstab_iterations(max(1, args.warmup), prec)
+    # ---- timed region 1: assembly --------------------------------------------------------------
+    ctx.assemble_state(1)
+    barrier_sync(dist, world)
+    t0 = time.perf_counter()
+    ctx.assemble_state(args.steps)
+    barrier_sync(dist, world)
+    t_asm = time.perf_counter() - t0
+    # ---- timed region 2: BiCGSTAB --------------------------------------------------------------
+    barrier_sync(dist, world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.bicgstab_iterations(args.bicg_iters, prec)
+    barrier_sync(dist, world)
+    t_bicg = time.perf_counter() - t0
+    # ---- event-timed passes (library stream) ---------------------------------------------------
+    ctx.timers(enable=True, reset=True)
+    ctx.assemble_state(args.steps)
+    ctx.bicgstab_iterations(args.bicg_iters, prec)
+    tm = ctx.timers(enable=False)
+    ctx.timers(reset=True)
+    for _ in range(args.steps):  # cache-cold: 1 GiB read between launches (untimed)
+        ctx.cache_scrub(SCRUB_BYTES)
+        ctx.timers(enable=True)
+        ctx.assemble_state(1)
+        ctx.timers(enable=False)
+    tm_cold = ctx.timers()
+    t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
+
+    nf = 3
+    N_global = 3 * mesh.nv
+    N_local = 3 * info["nv_owned"]
+    T_local = int(round(mesh.nt * info["nv_owned"] / mesh.nv))
+    B = byte_models(info, nf, N_local, T_local, prec)
+    asm_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
+    asm_cold_s = tm_cold["assemble_ms"] / max(1, tm_cold["assemble_launches"]) / 1e3
+    it_ev = (tm["spmv_ms"] + tm["prec_ms"] + tm["blas_ms"] + tm["halo_ms"] +
+             tm["allreduce_ms"]) / 1e3 / args.bicg_iters
+    spmv_s = tm["spmv_ms"] / max(1, tm["spmv_launches"]) / 1e3
+    prec_s = tm["prec_ms"] / max(1, tm["prec_launches"]) / 1e3
+    blas_s = tm["blas_ms"] / 1e3 / args.bicg_iters
+    rl = lambda b, t: {"bytes": b, "seconds": t, "achieved": b / t / 1e9,  # noqa: E731
+                       "frac": b / t / 1e9 / HBM_PEAK_GBS}
+    return {
+        "info": info, "N_global": N_global, "N_local": N_local, "t_asm": t_asm,
+        "t_bicg": t_bicg, "timers": tm, "timers_cold": tm_cold, "bytes": B,
+        "dofs_per_s": N_global * args.steps / t_asm,
+        "iters_per_s": args.steps * args.bicg_iters / t_bicg,
+        "asm_warm": rl(B["asm"], asm_s), "asm_cold": rl(B["asm"], asm_cold_s),
+        "it_contract": rl(B["it_contract"], it_ev), "it_stored": rl(B["it_stored"], it_ev),
+        "spmv_stored": rl(B["spmv_stored"], spmv_s),
+        "ilu_stored": rl(B["ilu_stored"], prec_s) if prec != P.PREC_NONE else None,
+        "blas": rl(B["blas"], blas_s),
+    }
+
+
+def strong_mesh(refine):
+    cfg = P.read_config(os.path.join(ROOT, "data", "pore_without_dna", "pore.cfg"))
+    return cfg, P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(refine)
+
+
+def primary_mesh(args, world):
+    if args.scaling == "strong":
+        return strong_mesh(args.strong_refine)
+    cfg = P.read_config(args.cfg)
+    return cfg, tile_mesh(P.Mesh.read_gmsh(cfg.meshfile).refine(args.refine), world)
 
 
 def main():
@@ -169,6 +325,13 @@ def main():
     ap.add_argument("--refine", type=int, default=4)
     ap.add_argument("--bicg-iters", type=int, default=20)
     ap.add_argument("--prec", default="ilu0", choices=["none", "jacobi", "ssor", "ilu0", "amg"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="primary line: weak (config 3 per GPU, default) or strong (config 5 "
+                         "split over the ranks)")
+    ap.add_argument("--strong-refine", type=int, default=6,
+                    help="refinement of the config-5 mesh (6: 8.87 M DOF)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the config-5 strong-scaling leg")
     ap.add_argument("--no-solve", action="store_true",
                     help="skip the time-to-solution PNP Newton after the timed regions")
     ap.add_argument("--no-amg", action="store_true",
@@ -176,7 +339,8 @@ def main():
     ap.add_argument("--amg-multi", action="store_true",
                     help="run the AMG time-to-solution leg at N>1 too (default: N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-refine", type=int, default=2)
+    ap.add_argument("--cpu-refine", type=int, default=4,
+                    help="refinement of the CPU sample (4: the config-3 mesh itself)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cfg", default=os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
     ap.add_argument("--newton-reduction", type=float, default=None,
@@ -189,73 +353,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", str(1)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    uid = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-        obj = [P.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
-
-    cfg = P.read_config(args.cfg)
-    base = P.Mesh.read_gmsh(cfg.meshfile).refine(args.refine)
-    mesh = tile_mesh(base, world)
-    par = P.Params.from_config(cfg)
     prec = P.PREC_BY_NAME[args.prec]
 
-    ctx = P.Context(mesh, par, device=local, rank=rank, size=world, unique_id=uid)
-    # Boltzmann initial state: PB Newton (SSOR BiCGSTAB, like ISTLBackend_NOVLP_BCGS_SSORk)
-    t_setup = time.perf_counter()
-    ctx.set_operator(P.OP_PB)
-    phi_pb, pb_res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=P.PREC_SSOR,
-                                linear_maxit=20000)
-    phi_pb = ctx.sync_vector(phi_pb, 1)  # each rank returns its owned entries; combine
-    x0 = ctx.initial_state(phi_pb)
-    ctx.set_operator(P.OP_PNP)
-    ctx.state_set(x0)
-    t_setup = time.perf_counter() - t_setup
-    info = ctx.info()
-    N_global = 3 * mesh.nv
-    N_local = 3 * info["nv_owned"]
-
-    # ---- warmup ------------------------------------------------------------------------------
-    ctx.assemble_state(args.warmup)
-    ctx.bicgstab_iterations(max(1, args.warmup), prec)
-
-    # ---- timed region 1: assembly --------------------------------------------------------------
-    ctx.assemble_state(1)
-    barrier_sync(dist, world)
-    t0 = time.perf_counter()
-    ctx.assemble_state(args.steps)
-    barrier_sync(dist, world)
-    t_asm = time.perf_counter() - t0
-
-    # ---- timed region 2: BiCGSTAB ---------------------------------------------------------------
-    barrier_sync(dist, world)
-    t0 = time.perf_counter()
-    sres = None
-    for _ in range(args.steps):
-        sres = ctx.bicgstab_iterations(args.bicg_iters, prec)
-    barrier_sync(dist, world)
-    t_bicg = time.perf_counter() - t0
-
-    # ---- event-timed pass (roofline) -------------------------------------------------------------
-    ctx.timers(enable=True, reset=True)
-    ctx.assemble_state(args.steps)
-    ctx.bicgstab_iterations(args.bicg_iters, prec)
-    tm = ctx.timers(enable=False)
+    copy_gbs = measured_copy_gbs(local)
+    cfg, mesh = primary_mesh(args, world)
+    ctx, x0, pb_res, t_setup = make_context(mesh, cfg, rank, world, local, dist)
+    M = measure(ctx, mesh, args, prec, dist, world)
+    info = M["info"]
 
     # ---- time to solution (reported beside the metric): PNP Newton from the Boltzmann state ----
     newton = None
-    # the config's Newton settings (pore.cfg: newtonReduction 1e-9, newtonMinLinearReduction
-    # 1e-8), overridable
     nt_red = args.newton_reduction or cfg.system["newtonReduction"]
     nt_linred = args.min_linear_reduction or cfg.system["newtonMinLinearReduction"]
     if not args.no_solve:
         barrier_sync(dist, world)
         t0 = time.perf_counter()
-        # bounded (10 Newton steps; 3 at N=1) so a block-Jacobi preconditioner that converges
-        # slowly at N>1 cannot stall the scaling runs; the metric does not include this leg
+        # bounded (10 Newton steps) so a block-Jacobi preconditioner that converges slowly at N>1
+        # cannot stall the scaling runs; the metric does not include this leg
         _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=prec,
                              linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
         barrier_sync(dist, world)
@@ -266,11 +383,8 @@ def main():
                   "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                   "reduction": nt_red, "min_linear_reduction": nt_linred,
                   "preconditioner": args.prec}
-
-    # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB:
-    # fewer, dearer iterations (reported beside the metric; the metric stays on --prec)
+    # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB
     newton_amg = None
-    # (N=1 only unless --amg-multi: the scaling runs time the metric, not this leg)
     if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
         ctx.amg_configure(smoother=P.PREC_ILU0)  # defaults: omega 0.8, 2 coarse sweeps
         # warm-up (untimed): first AMG setup loads rocSOLVER's getrf/getri kernels
@@ -285,29 +399,38 @@ def main():
         newton_amg = {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
                       "status": nres["status"], "iterations": nres["iterations"],
                       "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
+                      "linear_fallbacks": nres["linear_fallbacks"],
                       "preconditioner": "amg (ILU0 smoother, 2 block-Jacobi sweeps omega=0.8 "
                                         "on the coarse levels)",
                       "amg_rows": ctx.amg_info()["rows"]}
+    ctx.close()
 
-    t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
-    asm_avg_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
-    V, T = info["nv_owned"], None
-    # algorithmic bytes: B_asm = 8 nnz_red + 16 N + 12 T + 16 V, per rank
-    nnz_red = 7 * info["nblocks"]
-    T_local = int(round(mesh.nt * V / mesh.nv))
-    B_asm = 8 * nnz_red + 16 * N_local + 12 * T_local + 16 * V
-    B_it = (48 if prec != P.PREC_NONE else 24) * nnz_red + (304 if prec != P.PREC_NONE else 232) \
-        * N_local
-    achieved_asm = B_asm / asm_avg_s / 1e9
-    it_time_ev = (tm["spmv_ms"] + tm["prec_ms"] + tm["blas_ms"] + tm["halo_ms"] +
-                  tm["allreduce_ms"]) / 1e3 / args.bicg_iters
-
-    dofs_per_s = N_global * args.steps / t_asm
-    iters_per_s = args.steps * args.bicg_iters / t_bicg
+    # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
+    strong = None
+    if args.scaling == "weak" and not args.no_strong:
+        scfg, smesh = strong_mesh(args.strong_refine)
+        sctx, _, spb, s_setup = make_context(smesh, scfg, rank, world, local, dist)
+        S = measure(sctx, smesh, args, prec, dist, world)
+        sctx.close()
+        strong = {"workload": f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
+                              f"natively (scale 0.85), refined k={args.strong_refine}, one mesh "
+                              f"RCB-split over {world} GPU(s)",
+                  "scaling": "strong", "dofs": S["N_global"], "dofs_per_gpu": S["N_local"],
+                  "assembled_dofs_per_s": S["dofs_per_s"],
+                  "ms_per_step": 1e3 * S["t_asm"] / args.steps,
+                  "bicgstab_iters_per_s": S["iters_per_s"],
+                  "bicgstab_ms_per_iter": 1e3 * S["t_bicg"] / (args.steps * args.bicg_iters),
+                  "roofline_assembly_warm": S["asm_warm"], "roofline_assembly_cold": S["asm_cold"],
+                  "roofline_bicgstab_stored": S["it_stored"], "spmv_stored": S["spmv_stored"],
+                  "ilu0_apply_stored": S["ilu_stored"], "colors": S["info"]["ncolors"],
+                  "ghost_vertices": S["info"]["nv_ghost"], "setup_s": s_setup,
+                  "halo_ms_per_iter": S["timers"]["halo_ms"] / args.bicg_iters,
+                  "allreduce_ms_per_iter": S["timers"]["allreduce_ms"] / args.bicg_iters}
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the contract: rank 0 at N=1 only
-        cb = cpu_baseline(cfg, args.cpu_refine, args.cpu_seconds)
+        cb = cpu_baseline(cfg if args.scaling == "weak" else P.read_config(args.cfg),
+                          args.cpu_refine, args.cpu_seconds)
         cpu = {"value": cb["dofs_per_s"], "unit": "assembled DOFs/s", "cores": 1, "kind": "port",
                "sample": (f"oracle/pnp_oracle.c (C restatement of the reference: PnpOperator "
                           f"residual + PDELab forward-difference Jacobian + BCRS-style scatter) on "
@@ -322,42 +445,70 @@ def main():
                    "sample": (f"the same assembly on the same sample with OpenMP over element "
                               f"colours (orc_assemble_mt), {cb['mt_threads']} threads "
                               f"(OMP_NUM_THREADS / host), {cb['mt_assembly_s']:.4f} s per "
-                              f"assembly")}
+                              f"assembly; ISTL BiCGSTAB NOPREC row-parallel "
+                              f"{cb['bicgstab_nonprec_s_per_it_mt'] * 1e3:.2f} ms/it"),
+                   "bicgstab_nonprec_iters_per_s": 1.0 / cb["bicgstab_nonprec_s_per_it_mt"]}
 
     if rank == 0:
+        tm = M["timers"]
+        aw, ac = M["asm_warm"], M["asm_cold"]
+        if args.scaling == "weak":
+            workload = (f"config 3: stationary 3-ion PNP, test/pore_pnp/pore.msh refined "
+                        f"k={args.refine} x {world} mirrored copies")
+        else:
+            workload = (f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
+                        f"natively (scale 0.85), refined k={args.strong_refine}, one mesh "
+                        f"RCB-split over {world} GPU(s)")
         line = {
             "metric": "assembled DOFs/s + BiCGStab iters/s, 3-species PNP on pore.msh-refined",
-            "value": dofs_per_s,
+            "value": M["dofs_per_s"],
             "unit": "assembled DOFs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * t_asm / args.steps,
+            "ms_per_step": 1e3 * M["t_asm"] / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "reference inputs: test/pore_pnp mesh (refined) + pore.cfg; state = Boltzmann "
                     "initial state from a GPU PB Newton solve (no synthetic vectors)",
-            "config": {"workload": f"config 3: stationary 3-ion PNP, test/pore_pnp/pore.msh "
-                                   f"refined k={args.refine} x {world} mirrored copies",
-                       "dofs": N_global, "dofs_per_gpu": N_local, "mesh_vertices": mesh.nv,
-                       "triangles": mesh.nt, "parallelism": f"mesh partition (RCB) x{world}",
+            "config": {"workload": workload,
+                       "dofs": M["N_global"], "dofs_per_gpu": M["N_local"],
+                       "mesh_vertices": mesh.nv, "triangles": mesh.nt,
+                       "parallelism": f"mesh partition (RCB) x{world}",
                        "preconditioner": args.prec, "colors": info["ncolors"],
                        "sell_slots": info["nslots"], "blocks": info["nblocks"]},
-            "bicgstab_iters_per_s": iters_per_s,
-            "bicgstab_ms_per_iter": 1e3 * t_bicg / (args.steps * args.bicg_iters),
-            "roofline": {"bound": "hbm", "achieved": achieved_asm, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_asm / HBM_PEAK_GBS,
+            "bicgstab_iters_per_s": M["iters_per_s"],
+            "bicgstab_ms_per_iter": 1e3 * M["t_bicg"] / (args.steps * args.bicg_iters),
+            "roofline": {"bound": "hbm", "achieved": aw["achieved"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": aw["frac"],
                          "traffic": pmc_traffic("k_assemble_ga<0, 1, 3, 9, 6>"),
-                         "traffic_source": "profiles/r01/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
+                         "traffic_source": "profiles/r02/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
                                            "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
-                         "bytes_per_launch": B_asm, "avg_launch_us": asm_avg_s * 1e6},
-            "roofline_bicgstab": {"bound": "hbm", "bytes_per_iter": B_it,
-                                  "event_ms_per_iter": it_time_ev * 1e3,
-                                  "achieved": B_it / it_time_ev / 1e9, "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s", "frac": B_it / it_time_ev / 1e9 / HBM_PEAK_GBS},
+                         "bytes_per_launch": aw["bytes"], "avg_launch_us": aw["seconds"] * 1e6,
+                         "note": "warm: back-to-back launches, the matrix write stream stays in "
+                                 "the Infinity Cache at config 3; see roofline_cold"},
+            "roofline_cold": {"bound": "hbm", "achieved": ac["achieved"], "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": ac["frac"], "bytes_per_launch": ac["bytes"],
+                              "avg_launch_us": ac["seconds"] * 1e6,
+                              "frac_of_measured_copy": ac["achieved"] / copy_gbs,
+                              "scrub": f"{SCRUB_BYTES >> 20} MiB read between launches"},
+            "measured_copy_gbs": copy_gbs,
+            "roofline_bicgstab": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "event_ms_per_iter": M["it_stored"]["seconds"] * 1e3,
+                                  "bytes_per_iter": M["it_stored"]["bytes"],
+                                  "achieved": M["it_stored"]["achieved"],
+                                  "frac": M["it_stored"]["frac"],
+                                  "byte_model": "stored formats (k-form SELL + 4-B index per "
+                                                "slot, split ILU(0) factors, vectors)",
+                                  "contract_bytes_per_iter": M["it_contract"]["bytes"],
+                                  "contract_achieved": M["it_contract"]["achieved"],
+                                  "contract_frac": M["it_contract"]["frac"],
+                                  "kernels": {"spmv": M["spmv_stored"],
+                                              "ilu0_apply": M["ilu_stored"],
+                                              "blas_per_iter": M["blas"]}},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "setup_s": t_setup,
@@ -367,9 +518,9 @@ def main():
             "event_timers_ms": tm,
             "pnp_newton_time_to_solution": newton,
             "pnp_newton_time_to_solution_amg": newton_amg,
+            "strong_scaling": strong,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

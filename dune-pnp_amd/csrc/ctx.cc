@@ -118,6 +118,7 @@ struct pnp_ctx {
   DBuf<double> lvals, uvals, tsgs;
   int split_of = 0;
   DBuf<int> d_blkmap;
+  DBuf<double> scrub;  // pnp_cache_scrub (cache-cold benchmark timings)
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
   // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
   // global segment order
@@ -1335,6 +1336,10 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->nblocks = c->L.nblocks;
   info->nnz_reduced = c->L.nblocks * (c->nvb ? c->nvb : 1);
   info->nslots = c->L.nslots;
+  info->nks = c->nks;
+  info->nvb = c->nvb;
+  info->lslots = (int64_t)c->d_lsrc.n;
+  info->uslots = (int64_t)c->d_usrc.n;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->b.n + c->prevu.n + c->ext.n) * 8;
@@ -1816,6 +1821,16 @@ extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_
   int rc = c->bicgstab(c->b.p, c->z.p, o, *res, n);
   c->amg_symmetric = true;
   return rc;
+}
+
+extern "C" int pnp_cache_scrub(pnp_ctx *c, int64_t bytes) {
+  if (!c || bytes < 0) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  const size_t n = size_t(bytes) / 8;
+  if (c->scrub.n < n + 1) CK(c->scrub.alloc(n + 1), "scrub buffer");
+  CK(pnp::launch_scrub(c->scrub.p, (long long)n, c->scrub.p + n, c->stream), "scrub");
+  CK(hipStreamSynchronize(c->stream), "scrub");
+  return PNP_OK;
 }
 
 extern "C" int pnp_timers_enable(pnp_ctx *c, int32_t on) {

@@ -342,5 +342,7 @@ hipError_t launch_gather_ext(int n, int nf, int nv_global, const int *l2g, const
                              double *in, hipStream_t s);
 hipError_t launch_scatter_ext(int n, int nf, int nv_global, const int *l2g, const double *in,
                               double *ext, hipStream_t s);
+// read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
+hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 
 }  // namespace pnp

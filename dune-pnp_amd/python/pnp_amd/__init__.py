@@ -87,7 +87,9 @@ class _Info(C.Structure):
     _fields_ = [("nv_global", C.c_int32), ("nv_owned", C.c_int32), ("nv_ghost", C.c_int32),
                 ("nfields", C.c_int32), ("ncolors", C.c_int32), ("nchunks", C.c_int32),
                 ("max_slots", C.c_int32), ("nranks", C.c_int32), ("nblocks", C.c_int64),
-                ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64)]
+                ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
+                ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
+                ("uslots", C.c_int64)]
 
 
 class _OpArgs(C.Structure):
@@ -560,6 +562,10 @@ class Context:
         r = _SolveResult()
         self._ck(lib().pnp_bicgstab_iterations(self.h, int(n), int(prec), C.byref(r)))
         return {k: getattr(r, k) for k, _ in _SolveResult._fields_}
+
+    def cache_scrub(self, nbytes=1 << 30):
+        """Evict the caches (read nbytes of scratch on the context's stream) before a cold timing."""
+        self._ck(lib().pnp_cache_scrub(self.h, C.c_int64(int(nbytes))))
 
     def timers(self, enable=None, reset=False):
         if enable is not None:

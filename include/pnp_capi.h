@@ -148,6 +148,9 @@ typedef struct {
   int64_t nnz_reduced;   /* scalar nonzeros of the stored block pattern */
   int64_t nslots;        /* SELL slots incl. padding */
   int64_t device_bytes;
+  int32_t nks;           /* stored values per block of the current operator (k-form) */
+  int32_t nvb;           /* block-pattern values per block (expanded, e.g. 7 for PNP) */
+  int64_t lslots, uslots;/* slots of the strictly-lower / diagonal+upper split storage */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 
@@ -298,6 +301,11 @@ int pnp_state_get(pnp_ctx *ctx, double *x);
 int pnp_assemble_state(pnp_ctx *ctx, int32_t n);  /* n < 0: |n| residual-only assemblies */
 /* n BiCGSTAB iterations (no convergence stop) on J z = r of the last assembly */
 int pnp_bicgstab_iterations(pnp_ctx *ctx, int32_t n, int32_t prec, pnp_solve_result *res);
+
+/* read `bytes` of a context-owned scratch buffer on the context's stream, then synchronise:
+ * evicts the matrix and vectors from the L2s and the Infinity Cache before a cache-cold timing
+ * (dirty lines are written back here, outside the timed launch) */
+int pnp_cache_scrub(pnp_ctx *ctx, int64_t bytes);
 
 /* per-phase device time from HIP events recorded on the context's stream (enable first) */
 typedef struct {

@@ -908,7 +908,14 @@ int orc_num_threads(void) {
 /* ----------------------------------------------------------------------------------------
  * linear algebra: ISTL BiCGSTABSolver + preconditioners (a11)
  * ---------------------------------------------------------------------------------------- */
+/* all-core CPU baseline switch (bench cpu_baseline_all_cores): when on, the SpMV, the dots and
+ * the vector updates of orc_bicgstab run as OpenMP row-parallel loops (dots then sum in OpenMP's
+ * order, not ISTL's; the tests leave it off and keep the serial order) */
+static int g_par = 0;
+void orc_set_parallel(int on) { g_par = on; }
+
 void orc_spmv(const orc_csr *A, const double *x, double *y) {
+#pragma omp parallel for schedule(static) if (g_par)
   for (int i = 0; i < A->n; i++) {
     double s = 0;
     for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++) s += A->val[k] * x[A->col[k]];
@@ -918,6 +925,11 @@ void orc_spmv(const orc_csr *A, const double *x, double *y) {
 
 static double dot(int n, const double *a, const double *b) {
   double s = 0;
+  if (g_par) {
+#pragma omp parallel for schedule(static) reduction(+ : s)
+    for (int i = 0; i < n; i++) s += a[i] * b[i];
+    return s;
+  }
   for (int i = 0; i < n; i++) s += a[i] * b[i];
   return s;
 }
@@ -1044,6 +1056,7 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
       memcpy(p, r, sizeof(double) * n);
     } else {
       beta = (rho_new / rho) * (alpha / omega);
+#pragma omp parallel for schedule(static) if (g_par)
       for (int i = 0; i < n; i++) p[i] = beta * (p[i] - omega * v[i]) + r[i];
     }
     memset(y, 0, sizeof(double) * n);
@@ -1052,8 +1065,11 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
     h = dot(n, rt, v);
     if (fabs(h) < EPSILON) { res->breakdown = 3; break; }
     alpha = rho_new / h;
-    for (int i = 0; i < n; i++) x[i] += alpha * y[i];
-    for (int i = 0; i < n; i++) r[i] -= alpha * v[i];
+#pragma omp parallel for schedule(static) if (g_par)
+    for (int i = 0; i < n; i++) {
+      x[i] += alpha * y[i];
+      r[i] -= alpha * v[i];
+    }
     norm = sqrt(dot(n, r, r));
     if (norm < reduction * norm_0) { res->converged = 1; break; }
     it += .5;
@@ -1061,8 +1077,11 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
     prec_apply(&P, y, r);
     orc_spmv(A, y, t);
     omega = dot(n, t, r) / dot(n, t, t);
-    for (int i = 0; i < n; i++) x[i] += omega * y[i];
-    for (int i = 0; i < n; i++) r[i] -= omega * t[i];
+#pragma omp parallel for schedule(static) if (g_par)
+    for (int i = 0; i < n; i++) {
+      x[i] += omega * y[i];
+      r[i] -= omega * t[i];
+    }
     rho = rho_new;
     norm = sqrt(dot(n, r, r));
     if (norm < reduction * norm_0 || norm < 1e-30) { res->converged = 1; break; }

@@ -154,6 +154,8 @@ typedef struct {
 
 void orc_spmv(const orc_csr *A, const double *x, double *y);
 /* ISTL BiCGSTABSolver::apply(x, b, res): x overwritten (start value = x), b overwritten. */
+/* 1: OpenMP row-parallel SpMV / dots / updates in orc_bicgstab (all-core CPU baseline) */
+void orc_set_parallel(int on);
 void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
                   orc_solve_result *res);
 /* ISTL CGSolver (LINEARSOLVER CG_NOPREC / CG_Jacobi), see pnp_oracle.c */

@@ -15,8 +15,8 @@ for step in "$@"; do
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$? ;;
     bench)  timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1; rc=$? ;;
     benchq) timeout -k 10 600 python bench.py --no-cpu --steps 10 > "$OUT/bench.log" 2>&1; rc=$? ;;
-    trace)  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --no-cpu --no-solve --steps 3 --warmup 1 > "$OUT/trace.log" 2>&1; rc=$? ;;
-    prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-solve --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
+    trace)  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --no-cpu --no-solve --no-strong --steps 3 --warmup 1 > "$OUT/trace.log" 2>&1; rc=$? ;;
+    prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-solve --no-strong --steps 10 > "$OUT/prof.log" 2>&1; rc=$? ;;
     pmcf)   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcf.log" 2>&1; rc=$? ;;
     pmcw)   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcw.log" 2>&1; rc=$? ;;
     pmcsq)  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_sq" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcsq.log" 2>&1; rc=$? ;;
