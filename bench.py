@@ -217,7 +217,9 @@ def byte_models(info, nf, N_local, T_local, prec):
     spmv = info["nslots"] * (8 * info["nks"] + 4) + 8 * n_loc + 16 * N_local
     # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
     # written, re-read by the backward sweep (gathers counted once), v written
-    ilu = (info["lslots"] + info["uslots"]) * (8 * info["nvb"] + 4) + 8 * (N_local + 3 * n_loc)
+    vb = 4 * ((info["nvb"] + 3) // 4 * 4 if info["nvb"] > 1 else 1) if info["ilu_f32"] else \
+        8 * info["nvb"]  # bytes per block of the stored factors (float: quads)
+    ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
     blas = 192 * N_local  # ~24 vector passes per iteration (the contract's figure)
     return {"asm": B_asm, "it_contract": B_it, "spmv_stored": spmv, "ilu_stored": ilu,
             "blas": blas, "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}
@@ -503,6 +505,7 @@ def main():
                                   "frac": M["it_stored"]["frac"],
                                   "byte_model": "stored formats (k-form SELL + 4-B index per "
                                                 "slot, split ILU(0) factors, vectors)",
+                                  "ilu_factor_precision": "f32" if info["ilu_f32"] else "f64",
                                   "contract_bytes_per_iter": M["it_contract"]["bytes"],
                                   "contract_achieved": M["it_contract"]["achieved"],
                                   "contract_frac": M["it_contract"]["frac"],

@@ -117,6 +117,16 @@ struct pnp_ctx {
       d_usrc;
   DBuf<double> lvals, uvals, tsgs;
   int split_of = 0;
+  // ILU(0) factors in the split storage in single precision (PNP_OPT_ILU_F32, default 1; the
+  // sweeps compute in fp64, the matrix, SpMV, SSOR and every vector stay fp64).  Measured at
+  // config 3: ILU(0) apply 119 -> 95 us, BiCGSTAB 428 -> 389 us/it, Newton 9,295 -> 9,177
+  // iterations (profiles/r02/ab_ilu_f32.log)
+  int ilu_f32 = [] {
+    const char *e = std::getenv("PNP_ILU_F32");
+    return (e && std::atoi(e) == 0) ? 0 : 1;
+  }();
+  int f32_now() const { return split_of == 2 ? ilu_f32 : 0; }
+  int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
   DBuf<int> d_blkmap;
   DBuf<double> scrub;  // pnp_cache_scrub (cache-cold benchmark timings)
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
@@ -412,16 +422,25 @@ struct pnp_ctx {
     return PNP_OK;
   }
 
-  // ILU(0) factors of the current matrix (once per assembly)
+  // ILU(0) factors of the current matrix (once per assembly).  Default: the fused factorisation
+  // (expand and split folded in, neighbour-row work hoisted; PNP_OPT_ILU_FUSED_FACTOR = 0 runs the
+  // three-pass path, the same bits)
   int ilu_factor() {
     if (lu_valid) return PNP_OK;
     hipEvent_t t0 = tb(T_FACT);
-    hipError_t e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
-    if (e == hipSuccess) e = pnp::launch_ilu0_factor(dl, L.color_ptr.data(), nf, pat, lu.p, stream);
+    hipError_t e;
+    if (ilu_fused) {
+      e = pnp::launch_ilu0_factor_fused(dl, L.color_ptr.data(), nf, pat, vals.p, lu.p, lvals.p,
+                                        uvals.p, ilu_f32, stream);
+    } else {
+      e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
+      if (e == hipSuccess)
+        e = pnp::launch_ilu0_factor(dl, L.color_ptr.data(), nf, pat, lu.p, stream);
+    }
     if (e != hipSuccess) return hipfail(e, "ilu0 factorisation");
     te(T_FACT, t0);
     lu_valid = true;
-    split_of = 0;
+    split_of = ilu_fused ? 2 : 0;
     return PNP_OK;
   }
 
@@ -431,7 +450,7 @@ struct pnp_ctx {
     hipEvent_t t0 = tb(T_FACT);
     hipError_t e = pnp::launch_split(dl, nf, pat, which == 1 ? 1 : 0, which == 2 ? lu.p : vals.p,
                                      d_lsrc.p, (long long)d_lsrc.n, d_usrc.p, (long long)d_usrc.n,
-                                     lvals.p, uvals.p, stream);
+                                     lvals.p, uvals.p, stream, which == 2 ? ilu_f32 : 0);
     if (e != hipSuccess) return hipfail(e, "split");
     te(T_FACT, t0);
     split_of = which;
@@ -602,7 +621,7 @@ struct pnp_ctx {
     if (e != hipSuccess) return hipfail(e, "amg v-cycle");
     if (sm == PNP_PREC_ILU0) {  // vout = y + M^-1 r, written by the backward sweep
       e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, amg_r.p,
-                                 amg_z.p, stream, 0, amg_y.p, vout);
+                                 amg_z.p, stream, 0, amg_y.p, vout, f32_now());
       return e == hipSuccess ? PNP_OK : hipfail(e, "amg v-cycle");
     }
     if ((rc = smoother(sm, amg_r.p, amg_z.p))) return rc;
@@ -620,7 +639,7 @@ struct pnp_ctx {
                           stream);
     } else if (prec == PNP_PREC_ILU0) {
       e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout,
-                                 stream);
+                                 stream, 0, nullptr, nullptr, f32_now());
     } else {
       e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
     }
@@ -697,7 +716,7 @@ struct pnp_ctx {
     auto ilu_from1 = [&](const double *d, double *out) -> int {
       hipEvent_t tp = tb(T_PREC);
       hipError_t ee = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p,
-                                             d, out, stream, 1);
+                                             d, out, stream, 1, nullptr, nullptr, f32_now());
       if (ee != hipSuccess) return hipfail(ee, "preconditioner");
       te(T_PREC, tp);
       return PNP_OK;
@@ -707,7 +726,8 @@ struct pnp_ctx {
       t0 = tb(T_BLAS);
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 0, k == 0 ? 1 : 0, nullptr, nullptr,
-                                    rs.p, v.p, p.p, uvals.p, y.p, nullptr, nullptr, stream);
+                                    rs.p, v.p, p.p, uvals.p, y.p, nullptr, nullptr, stream,
+                                    f32_now());
       else
         e = pnp::launch_update_p(n, S.p, rs.p, v.p, p.p, k == 0 ? 1 : 0, stream);
       if (e != hipSuccess) return hipfail(e, "update_p");
@@ -733,7 +753,7 @@ struct pnp_ctx {
       t0 = tb(T_BLAS);
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, zout, yin, rs.p, v.p, nullptr,
-                                    uvals.p, y.p, partials2.p, &npu, stream);
+                                    uvals.p, y.p, partials2.p, &npu, stream, f32_now());
       else
         e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials2.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (1)");
@@ -1340,6 +1360,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->nvb = c->nvb;
   info->lslots = (int64_t)c->d_lsrc.n;
   info->uslots = (int64_t)c->d_usrc.n;
+  info->ilu_f32 = c->ilu_f32;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->b.n + c->prevu.n + c->ext.n) * 8;
@@ -1552,6 +1573,39 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
   if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
   if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
   return c->download_ext(c->z.p, c->nf, v);
+}
+
+extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
+  if (!c) return PNP_E_ARG;
+  if (option == PNP_OPT_ILU_F32) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0 or 1");
+    if (c->ilu_f32 != int(value)) {
+      c->ilu_f32 = int(value);
+      if (c->split_of == 2) c->split_of = 0;  // re-split the factors in the new precision
+    }
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_ILU_FUSED_FACTOR) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_FUSED_FACTOR takes 0 or 1");
+    c->ilu_fused = int(value);
+    c->lu_valid = false;
+    if (c->split_of == 2) c->split_of = 0;
+    return PNP_OK;
+  }
+  return c->fail(PNP_E_ARG, "unknown option");
+}
+
+extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
+  if (!c || !value) return PNP_E_ARG;
+  if (option == PNP_OPT_ILU_F32) {
+    *value = c->ilu_f32;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_ILU_FUSED_FACTOR) {
+    *value = c->ilu_fused;
+    return PNP_OK;
+  }
+  return c->fail(PNP_E_ARG, "unknown option");
 }
 
 extern "C" int pnp_amg_configure(pnp_ctx *c, const pnp_amg_opts *o) {

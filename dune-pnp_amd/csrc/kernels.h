@@ -278,9 +278,11 @@ hipError_t launch_sgs(const DevLayout &L, const int *color_ptr_host, int nf, int
 // fill the L / U split storage (NV values per block) from the k-form matrix (from_k = 1: expand
 // and mask) or from the ILU factors (from_k = 0: copy).  lsrc/usrc: (row << 6 | slot) of the
 // source block in the full SELL, -1 for padding
+// f32 (from_k = 0 only): store the factors in single precision (quad-interleaved, see
+// linalg.hip vinf); the sweeps then read float values and compute in fp64
 hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,
-                        const int *lsrc, long long ln, const int *usrc, long long un, double *lv,
-                        double *uv, hipStream_t s);
+                        const int *lsrc, long long ln, const int *usrc, long long un, void *lv,
+                        void *uv, hipStream_t s, int f32 = 0);
 // lu = the k-form matrix expanded and masked to NV values per block (ILU input)
 hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals, double *lu,
                          hipStream_t s);
@@ -289,19 +291,25 @@ hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals
 // factors on exit (unit-lower L strictly below, U on/above the diagonal, diagonal inverted)
 hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                               double *lu, hipStream_t s);
+// the same factors from the k-form matrix in one launch per colour, expand and split folded in:
+// lu = scratch (NV values per block, the factors on exit), lv / uv = the split storage (float when
+// f32); bitwise the factors of launch_expand + launch_ilu0_factor + launch_split
+hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
+                                    const double *kvals, double *lu, void *lv, void *uv, int f32,
+                                    hipStream_t s);
 // c_first = 1: colour 0's forward step was already applied (launch_update_fwd0); add != null:
 // also out = add + v (written row by row as the backward sweep finishes them)
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
-                             const double *lv, const double *uv, const double *d, double *v,
+                             const void *lv, const void *uv, const double *d, double *v,
                              hipStream_t s, int c_first = 0, const double *add = nullptr,
-                             double *out = nullptr);
+                             double *out = nullptr, int f32 = 0);
 // BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
 // p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
 // r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
-                              const double *v, double *p, const double *uv, double *yout,
-                              double *partials, int *nparts, hipStream_t s);
+                              const double *v, double *p, const void *uv, double *yout,
+                              double *partials, int *nparts, hipStream_t s, int f32 = 0);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);

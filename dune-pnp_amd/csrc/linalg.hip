@@ -184,25 +184,64 @@ __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__
 // forward, descending backward).  The forward sweep starts from v = 0 (ISTL SeqSSOR applies to y = 0): rows of
 // later colours are still zero and are skipped, the row's own value is not read.
 // Row setup shared by the split sweeps: the row's slots in the L (FWD) or U (!FWD) storage.
+// Value type of the split storage: double, or float for the ILU(0) factors when the context
+// stores them in single precision (PNP_ILU_F32; the arithmetic stays fp64).  float slots hold NVP
+// = NV rounded up to 4 values per row, quad-interleaved (one dwordx4 per lane moves 4 values):
+// value q of lane l at (q >> 2) * 4 * kRows + 4 l + (q & 3); NV == 1 is row-contiguous.
+template <int NV>
+__host__ __device__ constexpr int nvp_f() { return NV == 1 ? 1 : ((NV + 3) & ~3); }
+__host__ __device__ constexpr int vinf(int nv, int q, int lane) {
+  return nv == 1 ? lane : (q >> 2) * 4 * kRows + 4 * lane + (q & 3);
+}
+template <int NV, typename VT>
+__host__ __device__ constexpr int slot_vals() {
+  return std::is_same<VT, float>::value ? nvp_f<NV>() : NV;
+}
+
+template <int NV, int NT, typename VT>
+__device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int lane, double *B) {
+  if constexpr (std::is_same<VT, double>::value) {
+    if (NT)
+      load_vals_nt<NV>(sb, lane, B);
+    else
+      load_vals<NV>(sb, lane, B);
+  } else if constexpr (NV == 1) {
+    B[0] = NT ? __builtin_nontemporal_load(sb + lane) : sb[lane];
+  } else {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int k = 0; k < nvp_f<NV>() / 4; k++) {
+      const f4v *pp = reinterpret_cast<const f4v *>(sb + k * 4 * kRows) + lane;
+      const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (4 * k + i < NV) B[4 * k + i] = double(t[i]);
+    }
+  }
+}
+
+// Row setup shared by the split sweeps: the row's slots in the L (FWD) or U (!FWD) storage.
+template <typename VT>
 struct SplitRow {
   const int *cix;
-  const double *vc;  // chunk base of the L or U values: slot s at vc + s * NV * kRows (vin())
-  const double *dg;  // U chunk base: slot 0 = diagonal block
+  const VT *vc;  // chunk base of the L or U values: slot s at vc + s * slot_vals * kRows
+  const VT *dg;  // U chunk base: slot 0 = diagonal block
   int len, lane;
 };
 
-template <int NV, int FWD>
-__device__ __forceinline__ SplitRow split_row(const DevLayout &L, const double *lv,
-                                              const double *uv, int row, bool live) {
+template <int NV, int FWD, typename VT = double>
+__device__ __forceinline__ SplitRow<VT> split_row(const DevLayout &L, const VT *lv, const VT *uv,
+                                                  int row, bool live) {
+  constexpr int NS = slot_vals<NV, VT>();
   const int chunk = row / kRows, lane = row % kRows;
   const int uoff = L.uchunk_off[chunk];
-  SplitRow r;
+  SplitRow<VT> r;
   r.lane = lane;
-  r.dg = uv + size_t(uoff) * NV;
+  r.dg = uv + size_t(uoff) * NS;
   if (FWD) {
     const int off = L.lchunk_off[chunk];
     r.cix = L.lcolidx + off + lane;
-    r.vc = lv + size_t(off) * NV;
+    r.vc = lv + size_t(off) * NS;
     r.len = live ? L.lchunk_len[chunk] : 0;
   } else {
     r.cix = L.ucolidx + uoff + lane;
@@ -216,10 +255,10 @@ __device__ __forceinline__ SplitRow split_row(const DevLayout &L, const double *
 // lanes, slots interleaved), partial sums combined across the row's lanes.  A colour holds ~1/6
 // of the rows (~2 waves per SIMD at config 3), so latency is hidden inside the thread: the
 // column indices of B slots are loaded together, then their gathers and values together.
-template <int NF, int PAT, int LPR, int B, int NT = 0>
-__device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, int row,
+template <int NF, int PAT, int LPR, int B, int NT = 0, typename VT = double>
+__device__ __forceinline__ void split_row_dot(const SplitRow<VT> &R, int s0, int q, int row,
                                               const double *__restrict__ v, double (&acc)[NF]) {
-  constexpr int NV = popc9(PAT);
+  constexpr int NV = popc9(PAT), NS = slot_vals<NV, VT>();
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] = 0.0;
   for (int sb = s0 + q; sb < R.len; sb += B * LPR) {
@@ -240,10 +279,7 @@ __device__ __forceinline__ void split_row_dot(const SplitRow &R, int s0, int q, 
         for (int g = 0; g < NF; g++) vj[b][g] = 0.0;
       }
       if (use) {
-        if (NT)
-          load_vals_nt<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
-        else
-          load_vals<NV>(R.vc + size_t(s) * NV * kRows, R.lane, a[b]);
+        load_split_vals<NV, NT>(R.vc + size_t(s) * NS * kRows, R.lane, a[b]);
       } else {
 #pragma unroll
         for (int qq = 0; qq < NV; qq++) a[b][qq] = 0.0;
@@ -285,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   const int k = gt / LPR, q = gt % LPR;
   const bool live = k < nk;
   const int row = k0 + (live ? k : 0);  // colour-major order: the colour's rows are [k0, k0+nk)
-  const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
+  const SplitRow<double> R = split_row<NV, FWD>(L, lv, uv, row, live);
   // the row's own data and diagonal block do not depend on the neighbours: issued before the
   // neighbour loop so that they share its memory round trips (after the loop they cost one more)
   double rhs[NF], vi[NF], Dg[NV];
@@ -408,6 +444,163 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
   }
 }
 
+// The same factorisation with the neighbour-row work hoisted and the expand / split passes folded
+// in (one launch per colour, no k_expand / k_split passes):
+//   0) the row expands its own k-form blocks (masked) into lu;
+//   1) per lower neighbour j (ascending): the L block L_ij = A_ij U_jj^-1 is finished in registers
+//      from row j's diagonal block (loaded once), then every block A_im with m > j in both rows is
+//      updated from row j's block U_jm, each loaded once per j (the column match of the two rows
+//      is computed once per j, not once per field pair);
+//   2) inside the vertex, as in k_ilu0_factor;
+//   3) the row's blocks are written to the split L / U storage (VT: double or float).
+// Per block entry the subtraction order (j ascending, then g ascending) is that of
+// k_ilu0_factor, so the factors are bitwise the same.
+template <int NF, int PAT, typename VT>
+__global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r0, int r1,
+                                                              const double *__restrict__ kvals,
+                                                              double *__restrict__ lu,
+                                                              VT *__restrict__ lv,
+                                                              VT *__restrict__ uv) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT), NS = slot_vals<NV, VT>();
+  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  if (row >= r1) return;
+  const int ci = row / kRows, li = row % kRows;
+  const int offi = L.chunk_off[ci], leni = int(L.rowmeta[row] & 63);
+  const int *__restrict__ cixi = L.colidx + offi + li;
+  double *__restrict__ vi = lu + size_t(offi) * NV;  // chunk base, see vin()
+  auto ld = [&](const double *base, int t, int lane, double (&B)[NV]) {
+#pragma unroll
+    for (int q = 0; q < NV; q++) B[q] = base[size_t(t) * NV * kRows + vin(NV, q, lane)];
+  };
+  auto st = [&](double *base, int t, int lane, const double (&B)[NV]) {
+#pragma unroll
+    for (int q = 0; q < NV; q++) base[size_t(t) * NV * kRows + vin(NV, q, lane)] = B[q];
+  };
+  // 0) expand + mask the row's blocks into lu
+  {
+    const unsigned dm = row_mask<NF>(L, row);
+    const double *kb = kvals + size_t(offi) * NK;
+    for (int t = 0; t < leni; t++) {
+      double K[NK], B[NV];
+#pragma unroll
+      for (int q = 0; q < NK; q++) K[q] = kb[size_t(t) * NK * kRows + vin(NK, q, li)];
+      expand_k<PAT>(K, B);
+      mask_rows<NF, PAT>(B, dm, t == 0);
+      st(vi, t, li, B);
+    }
+  }
+  // 1) lower neighbours in increasing index order
+  int prev = -1;
+  for (;;) {
+    int j = 0x7fffffff, s = -1;
+    for (int t = 1; t < leni; t++) {
+      const int c = cixi[t * kRows];
+      if (c < row && c > prev && c < j) {
+        j = c;
+        s = t;
+      }
+    }
+    if (s < 0) break;
+    prev = j;
+    const int cj = j / kRows, lj = j % kRows;
+    const int offj = L.chunk_off[cj], lenj = int(L.rowmeta[j] & 63);
+    const int *__restrict__ cixj = L.colidx + offj + lj;
+    const double *__restrict__ vj = lu + size_t(offj) * NV;
+    double Ujj[NV], Lb[NV];
+    ld(vj, 0, lj, Ujj);
+    ld(vi, s, li, Lb);
+#pragma unroll
+    for (int g = 0; g < NF; g++) {
+      const double dinv = Ujj[pat_index(PAT, g, g)];  // stored inverted
+#pragma unroll
+      for (int f = 0; f < NF; f++) {
+        if (pat_index(PAT, f, g) < 0) continue;
+        const double l = Lb[pat_index(PAT, f, g)] * dinv;
+        Lb[pat_index(PAT, f, g)] = l;
+        if (l == 0.0) continue;
+#pragma unroll
+        for (int h = g + 1; h < NF; h++)
+          if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
+            Lb[pat_index(PAT, f, h)] -= l * Ujj[pat_index(PAT, g, h)];
+      }
+    }
+    st(vi, s, li, Lb);
+    for (int t = 0; t < leni; t++) {
+      const int m = cixi[t * kRows];
+      if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;  // padding -> m == row
+      int u = 1;
+      while (u < lenj && cixj[u * kRows] != m) u++;
+      if (u == lenj) continue;
+      double U[NV], A[NV];
+      ld(vj, u, lj, U);
+      ld(vi, t, li, A);
+#pragma unroll
+      for (int g = 0; g < NF; g++)
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+          if (pat_index(PAT, f, g) < 0) continue;
+          const double l = Lb[pat_index(PAT, f, g)];
+          if (l == 0.0) continue;
+#pragma unroll
+          for (int h = 0; h < NF; h++)
+            if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
+              A[pat_index(PAT, f, h)] -= l * U[pat_index(PAT, g, h)];
+        }
+      st(vi, t, li, A);
+    }
+  }
+  // 2) inside the vertex: rows (i,f) eliminated by (i,g<f); invert the pivots
+  double D[NV];
+  ld(vi, 0, li, D);
+  for (int f = 0; f < NF; f++) {
+    for (int g = 0; g < f; g++) {
+      if (pat_index(PAT, f, g) < 0) continue;
+      const double l = D[pat_index(PAT, f, g)] * D[pat_index(PAT, g, g)];
+      D[pat_index(PAT, f, g)] = l;
+      for (int h = g + 1; h < NF; h++)
+        if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
+          D[pat_index(PAT, f, h)] -= l * D[pat_index(PAT, g, h)];
+      for (int t = 1; t < leni; t++) {
+        const int m = cixi[t * kRows];
+        if (m <= row || m >= L.n_owned) continue;
+        double A[NV];
+        ld(vi, t, li, A);
+        for (int h = 0; h < NF; h++)
+          if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
+            A[pat_index(PAT, f, h)] -= l * A[pat_index(PAT, g, h)];
+        st(vi, t, li, A);
+      }
+    }
+    D[pat_index(PAT, f, f)] = 1.0 / D[pat_index(PAT, f, f)];
+  }
+  st(vi, 0, li, D);
+  // 3) the split storage: slot 0 and the owned upper columns (slot order) to U, the lower
+  // columns (slot order) to L, ghost columns dropped -- the order ctx.cc builds lsrc / usrc in
+  auto put = [&](VT *base, int off, int k, const double (&B)[NV]) {
+    VT *sb = base + (size_t(off) + size_t(k) * kRows) * NS;
+    if constexpr (std::is_same<VT, double>::value) {
+#pragma unroll
+      for (int q = 0; q < NV; q++) sb[vin(NV, q, li)] = B[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < NS; q++) sb[vinf(NV, q, li)] = q < NV ? float(B[q]) : 0.0f;
+    }
+  };
+  const int loff = L.lchunk_off[ci], uoff = L.uchunk_off[ci];
+  put(uv, uoff, 0, D);
+  int kl = 0, ku = 1;
+  for (int t = 1; t < leni; t++) {
+    const int c = cixi[t * kRows];
+    if (c >= L.n_owned || c == row) continue;
+    double B[NV];
+    ld(vi, t, li, B);
+    if (c < row)
+      put(lv, loff, kl++, B);
+    else
+      put(uv, uoff, ku++, B);
+  }
+}
+
 // y <- Ld^-1 y (unit lower part of the factored diagonal block, fields ascending)
 template <int NF, int PAT, int NV>
 __device__ __forceinline__ void diag_lower_solve(const double (&Dg)[NV], double (&y)[NF]) {
@@ -446,10 +639,10 @@ enum { kIluFwd = 0, kIluBwd = 1, kIluLast = 2 };
 
 // ADD = 1 (backward / last-colour launches): also out_i = add_i + v_i for the finished rows (the
 // AMG's post-smoothing update y + M^-1 r without a separate pass)
-template <int NF, int PAT, int KIND, int LPR, int B, int NT, int ADD = 0>
+template <int NF, int PAT, int KIND, int LPR, int B, int NT, int ADD = 0, typename VT = double>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
-                                                       const double *__restrict__ lv,
-                                                       const double *__restrict__ uv,
+                                                       const VT *__restrict__ lv,
+                                                       const VT *__restrict__ uv,
                                                        const double *__restrict__ d,
                                                        double *__restrict__ v,
                                                        const double *__restrict__ add = nullptr,
@@ -460,13 +653,13 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   const int k = gt / LPR, q = gt % LPR;
   const bool live = r0 + k < r1;
   const int row = live ? r0 + k : r0;
-  const SplitRow R = split_row<NV, FWD>(L, lv, uv, row, live);
+  const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, row, live);
   // own data and diagonal block first: they share the neighbour loop's round trips
   double own[NF], Dg[NV];
   load_nf<NF>(FWD ? d : v, size_t(row), own);
-  load_vals<NV>(R.dg, R.lane, Dg);
+  load_split_vals<NV, 0>(R.dg, R.lane, Dg);
   double acc[NF];
-  split_row_dot<NF, PAT, LPR, B, NT>(R, FWD ? 0 : 1, q, row, v, acc);
+  split_row_dot<NF, PAT, LPR, B, NT, VT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] += own[f];
@@ -485,16 +678,15 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
 // split storage position p takes the block (row, slot) = (src >> 6, src & 63) of the full SELL:
 // FROMK: expanded and masked from the k-form matrix, else copied from the NV-form ILU factors;
 // padding (src < 0) gets zeros
-template <int NF, int PAT, int FROMK>
+template <int NF, int PAT, int FROMK, typename VT = double>
 __global__ __launch_bounds__(kBlock) void k_split(DevLayout L, const double *__restrict__ src,
                                                   const int *__restrict__ lsrc, long long ln,
                                                   const int *__restrict__ usrc, long long un,
-                                                  double *__restrict__ lv,
-                                                  double *__restrict__ uv) {
-  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
+                                                  VT *__restrict__ lv, VT *__restrict__ uv) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT), NS = slot_vals<NV, VT>();
   long long p = blockIdx.x * (long long)kBlock + threadIdx.x;
   const int *ps = lsrc;
-  double *dst = lv;
+  VT *dst = lv;
   if (p >= ln) {
     p -= ln;
     if (p >= un) return;
@@ -502,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void k_split(DevLayout L, const double *__r
     dst = uv;
   }
   const int lane = int(p & (kRows - 1));
-  double *sb = dst + (p - lane) * NV;  // slot base (position p - lane is lane 0 of the slot)
+  VT *sb = dst + (p - lane) * NS;  // slot base (position p - lane is lane 0 of the slot)
   const int code = ps[p];
   double B[NV];
   if (code < 0) {
@@ -521,8 +713,13 @@ __global__ __launch_bounds__(kBlock) void k_split(DevLayout L, const double *__r
     }
   }
   // the split position's lane equals the row's lane (same row)
+  if constexpr (std::is_same<VT, double>::value) {
 #pragma unroll
-  for (int q = 0; q < NV; q++) sb[vin(NV, q, lane)] = B[q];
+    for (int q = 0; q < NV; q++) sb[vin(NV, q, lane)] = B[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < NS; q++) sb[vinf(NV, q, lane)] = q < NV ? float(B[q]) : 0.0f;
+  }
 }
 
 // lu = expand_k + mask_rows of every block of the k-form matrix (NV values per block)
@@ -604,14 +801,14 @@ __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars
 // in the same pass, one row per thread, and the sweep starts at colour 1: one launch and one
 // re-read of d fewer per preconditioner application.  yin may alias yout (x += alpha y reads a
 // row's y before the row's new y is written, by the same thread).
-template <int NF, int PAT, int WHICH>
+template <int NF, int PAT, int WHICH, typename VT = double>
 __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
                                                         const Scalars *__restrict__ S, int first,
                                                         double *__restrict__ x, const double *yin,
                                                         double *__restrict__ r,
                                                         const double *__restrict__ v,
                                                         double *__restrict__ p,
-                                                        const double *__restrict__ uv,
+                                                        const VT *__restrict__ uv,
                                                         double *yout,
                                                         double *__restrict__ partials) {
   constexpr int NV = popc9(PAT);
@@ -649,7 +846,8 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     }
     if (row < c0_end) {
       double Dg[NV];
-      load_vals<NV>(uv + size_t(L.uchunk_off[row / kRows]) * NV, row % kRows, Dg);
+      load_split_vals<NV, 0>(uv + size_t(L.uchunk_off[row / kRows]) * slot_vals<NV, VT>(),
+                             row % kRows, Dg);
       diag_lower_solve<NF, PAT>(Dg, d);
       store_nf<NF>(yout, size_t(row), d);
     }
@@ -1054,64 +1252,97 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
   return hipGetLastError();
 }
 
-hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const double *lv,
-                             const double *uv, const double *d, double *v, hipStream_t s,
-                             int c_first, const double *add, double *out) {
+hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *cp, int nf, int pat,
+                                    const double *kvals, double *lu, void *lv, void *uv, int f32,
+                                    hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  auto run = [&](auto vt) -> hipError_t {
+    using VT = decltype(vt);
+    PNP_PAT_DISPATCH(nf, pat, {
+      for (int c = 0; c < L.ncolors; c++) {
+        int n = cp[c + 1] - cp[c];
+        if (n > 0)
+          hipLaunchKernelGGL((k_ilu0_factor_fused<NFc, PATc, VT>), rows_grid(n), dim3(kBlock), 0, s,
+                             L, cp[c], cp[c + 1], kvals, lu, static_cast<VT *>(lv),
+                             static_cast<VT *>(uv));
+      }
+    });
+    return hipGetLastError();
+  };
+  return f32 ? run(float()) : run(double());
+}
+
+hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const void *lvp,
+                             const void *uvp, const double *d, double *v, hipStream_t s,
+                             int c_first, const double *add, double *out, int f32) {
   if (L.n_owned == 0) return hipSuccess;
   const int nc = L.ncolors;
-  PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
-    auto go = [&](auto kind, int c) {
-      const int n = cp[c + 1] - cp[c];
-      if (n <= 0) return;
-      if (add && decltype(kind)::value != kIluFwd)
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 1>),
-                           rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
-                           d, v, add, out);
-      else
-        hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 0>),
-                           rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
-                           d, v, nullptr, nullptr);
-    };
-    // the last colour's backward step runs in its forward launch (kIluLast); c_first = 1: colour
-    // 0's forward step was done by launch_update_fwd0
-    for (int c = c_first; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
-    go(std::integral_constant<int, kIluLast>(), nc - 1);
-    for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
-  }));
-  return hipGetLastError();
+  auto run = [&](auto vt) -> hipError_t {
+    using VT = decltype(vt);
+    const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
+    PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
+      auto go = [&](auto kind, int c) {
+        const int n = cp[c + 1] - cp[c];
+        if (n <= 0) return;
+        if (add && decltype(kind)::value != kIluFwd)
+          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 1, VT>),
+                             rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
+                             d, v, add, out);
+        else
+          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 0, VT>),
+                             rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
+                             d, v, nullptr, nullptr);
+      };
+      // the last colour's backward step runs in its forward launch (kIluLast); c_first = 1:
+      // colour 0's forward step was done by launch_update_fwd0
+      for (int c = c_first; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
+      go(std::integral_constant<int, kIluLast>(), nc - 1);
+      for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
+    }));
+    return hipGetLastError();
+  };
+  return f32 ? run(float()) : run(double());
 }
 
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
-                              const double *v, double *p, const double *uv, double *yout,
-                              double *partials, int *nparts, hipStream_t s) {
+                              const double *v, double *p, const void *uvp, double *yout,
+                              double *partials, int *nparts, hipStream_t s, int f32) {
   const dim3 g = rows_grid(L.n_owned);
   if (nparts) *nparts = int(g.x);
   if (L.n_owned == 0) return hipSuccess;
-  PNP_PAT_DISPATCH(nf, pat, {
-    if (which == 0)
-      hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, c0_end, S, first,
-                         x, yin, r, v, p, uv, yout, partials);
-    else
-      hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, c0_end, S, first,
-                         x, yin, r, v, p, uv, yout, partials);
-  });
-  return hipGetLastError();
+  auto run = [&](auto vt) -> hipError_t {
+    using VT = decltype(vt);
+    const VT *uv = static_cast<const VT *>(uvp);
+    PNP_PAT_DISPATCH(nf, pat, {
+      if (which == 0)
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
+                           first, x, yin, r, v, p, uv, yout, partials);
+      else
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
+                           first, x, yin, r, v, p, uv, yout, partials);
+    });
+    return hipGetLastError();
+  };
+  return f32 ? run(float()) : run(double());
 }
 
 hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,
-                        const int *lsrc, long long ln, const int *usrc, long long un, double *lv,
-                        double *uv, hipStream_t s) {
+                        const int *lsrc, long long ln, const int *usrc, long long un, void *lv,
+                        void *uv, hipStream_t s, int f32) {
   const long long n = ln + un;
   if (n == 0) return hipSuccess;
   const dim3 g(unsigned((n + kBlock - 1) / kBlock));
   PNP_PAT_DISPATCH(nf, pat, {
     if (from_k)
       hipLaunchKernelGGL((k_split<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, src, lsrc, ln, usrc,
-                         un, lv, uv);
+                         un, static_cast<double *>(lv), static_cast<double *>(uv));
+    else if (f32)
+      hipLaunchKernelGGL((k_split<NFc, PATc, 0, float>), g, dim3(kBlock), 0, s, L, src, lsrc, ln,
+                         usrc, un, static_cast<float *>(lv), static_cast<float *>(uv));
     else
       hipLaunchKernelGGL((k_split<NFc, PATc, 0>), g, dim3(kBlock), 0, s, L, src, lsrc, ln, usrc,
-                         un, lv, uv);
+                         un, static_cast<double *>(lv), static_cast<double *>(uv));
   });
   return hipGetLastError();
 }

@@ -33,6 +33,7 @@ OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = 
 OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG = range(5)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
+OPT_ILU_F32, OPT_ILU_FUSED_FACTOR = 1, 2
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
                 "jacobi": PREC_JACOBI, "amg": PREC_AMG}
 MAX_SURFACES = 64
@@ -89,7 +90,7 @@ class _Info(C.Structure):
                 ("max_slots", C.c_int32), ("nranks", C.c_int32), ("nblocks", C.c_int64),
                 ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
                 ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
-                ("uslots", C.c_int64)]
+                ("uslots", C.c_int64), ("ilu_f32", C.c_int32)]
 
 
 class _OpArgs(C.Structure):
@@ -562,6 +563,14 @@ class Context:
         r = _SolveResult()
         self._ck(lib().pnp_bicgstab_iterations(self.h, int(n), int(prec), C.byref(r)))
         return {k: getattr(r, k) for k, _ in _SolveResult._fields_}
+
+    def set_option(self, option, value):
+        self._ck(lib().pnp_set_option(self.h, int(option), C.c_int64(int(value))))
+
+    def get_option(self, option):
+        v = C.c_int64()
+        self._ck(lib().pnp_get_option(self.h, int(option), C.byref(v)))
+        return v.value
 
     def cache_scrub(self, nbytes=1 << 30):
         """Evict the caches (read nbytes of scratch on the context's stream) before a cold timing."""

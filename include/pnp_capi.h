@@ -151,6 +151,7 @@ typedef struct {
   int32_t nks;           /* stored values per block of the current operator (k-form) */
   int32_t nvb;           /* block-pattern values per block (expanded, e.g. 7 for PNP) */
   int64_t lslots, uslots;/* slots of the strictly-lower / diagonal+upper split storage */
+  int32_t ilu_f32;       /* PNP_OPT_ILU_F32 */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 
@@ -255,6 +256,23 @@ int pnp_amg_info(pnp_ctx *ctx, pnp_amg_stats *stats);
 /* aggregate map of level -> level+1 (test hook): level 0 indexed by global vertex (-1: not owned
  * by this rank, agg sized nv), coarser levels by row */
 int pnp_amg_aggregates(pnp_ctx *ctx, int32_t level, int32_t *agg);
+
+/* ---- context options ------------------------------------------------------------------------ */
+enum {
+  /* 1 (default): the ILU(0) factors (PNP_PREC_ILU0 and the AMG's ILU(0) smoother) are stored in
+   * single precision; the sweeps read them as float and compute in fp64.  The matrix, the SpMV,
+   * SSOR/Jacobi and every vector stay fp64, so the operator and the converged solutions are those
+   * of the fp64 path; only the preconditioner is a rounded ILU(0) (config 3: apply 119 -> 95 us,
+   * Newton BiCGSTAB iterations 9,295 -> 9,177).  0: fp64 factors (the environment variable
+   * PNP_ILU_F32=0 sets the default to 0). */
+  PNP_OPT_ILU_F32 = 1,
+  /* 1 (default): ILU(0) factorisation in one launch per colour with the k-form expansion and the
+   * split into L / U storage folded in; 0: the three-pass path (expand, factor, split).  Both
+   * give the same factors bit for bit. */
+  PNP_OPT_ILU_FUSED_FACTOR = 2
+};
+int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
+int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
 
 /* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */
 int pnp_linear_solve(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,

@@ -328,14 +328,20 @@ def _ilu0_dense(A, M):
     return A
 
 
+@pytest.mark.parametrize("f32", [0, 1])
 @pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
                                        ("pore_small_k0", "pb"), ("cylinder_k0", "pnp")])
-def test_ilu0_application_matches_textbook_ilu0(name, kind):
+def test_ilu0_application_matches_textbook_ilu0(name, kind, f32):
     """pnp_prec_apply(ILU0) = (LU)^{-1} d with L, U the ILU(0) factors of the Jacobian on the
-    stored block pattern, ordered colour-major by vertex with fields ascending."""
+    stored block pattern, ordered colour-major by vertex with fields ascending.
+    f32 = 0: fp64 factors, to rounding (1e-10); f32 = 1 (PNP_OPT_ILU_F32, the default): the
+    factors stored in single precision, fp64 sweeps -- the same operator to float rounding of
+    the factors (2e-5 of max|v| on these well-conditioned small systems)."""
     import scipy.linalg as sla
     z, mesh, par, orc = golden(name)
     ctx = P.Context(mesh, par)
+    ctx.set_option(P.OPT_ILU_F32, f32)
+    assert ctx.get_option(P.OPT_ILU_F32) == f32
     set_ops(z, ctx, orc, kind)
     nf = 3 if kind.startswith("pnp") else 1
     A = ctx.jacobian(z[kind + "_x"]).toarray()
@@ -355,7 +361,7 @@ def test_ilu0_application_matches_textbook_ilu0(name, kind):
     y = sla.solve_triangular(np.tril(F, -1) + np.eye(len(F)), d[perm], lower=True)
     v_ref = sla.solve_triangular(np.triu(F), y, lower=False)
     v = ctx.prec_apply(d, P.PREC_ILU0)[perm]
-    assert np.max(np.abs(v - v_ref)) <= 1e-10 * np.max(np.abs(v_ref))
+    assert np.max(np.abs(v - v_ref)) <= (2e-5 if f32 else 1e-10) * np.max(np.abs(v_ref))
 
 
 def test_pb_then_pnp_on_refined_pore_converges_with_ilu0():
@@ -551,3 +557,26 @@ def test_cg_matches_oracle_cg(prec):
     assert ro.converged
     assert abs(res["iterations"] - ro.iterations) <= 1
     assert np.max(np.abs(sol - xo)) <= 1e-8 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+@pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
+                                       ("pore_small_k0", "pb")])
+def test_fused_ilu0_factorisation_is_bitwise_the_three_pass_one(name, kind, f32):
+    """PNP_OPT_ILU_FUSED_FACTOR (expand + factor + split in one launch per colour, the default)
+    gives the factors of the three-pass path bit for bit: same preconditioner output."""
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    set_ops(z, ctx, orc, kind)
+    ctx.set_option(P.OPT_ILU_F32, f32)
+    nf = 3 if kind.startswith("pnp") else 1
+    ctx.jacobian(z[kind + "_x"], export=False)
+    d = np.random.default_rng(7).standard_normal(nf * mesh.nv)
+    out = {}
+    for fused in (0, 1):
+        ctx.set_option(P.OPT_ILU_FUSED_FACTOR, fused)
+        out[fused] = ctx.prec_apply(d, P.PREC_ILU0)
+    assert np.array_equal(out[0], out[1])
+    # and a re-split after a switch to SSOR (the split storage reused) still gives the factors
+    ctx.prec_apply(d, P.PREC_SSOR)
+    assert np.array_equal(ctx.prec_apply(d, P.PREC_ILU0), out[1])
