@@ -409,6 +409,10 @@ hipError_t launch_amg_galerkin0(const DevLayout &L, int nf, int pat, const doubl
     hipLaunchKernelGGL((k_galerkin0<3, kPatPnp>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
   else if (nf == 3 && pat == kPatPnpIE)
     hipLaunchKernelGGL((k_galerkin0<3, kPatPnpIE>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
+  else if (nf == 3 && pat == kPatPnpFD)
+    hipLaunchKernelGGL((k_galerkin0<3, kPatPnpFD>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
+  else if (nf == 3 && pat == kPatPnpIEFD)
+    hipLaunchKernelGGL((k_galerkin0<3, kPatPnpIEFD>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
   else if (nf == 1)
     hipLaunchKernelGGL((k_galerkin0<1, kPatScalar>), g1(nq), dim3(kB), 0, s, L, kvals, nq, cptr, csrc, cv);
   else

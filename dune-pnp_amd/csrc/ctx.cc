@@ -129,6 +129,20 @@ struct pnp_ctx {
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
   DBuf<int> d_blkmap;
   DBuf<double> scrub;  // pnp_cache_scrub (cache-cold benchmark timings)
+  // forward-difference Jacobian (PNP_JAC_FD, fd_jacobian.hip): local elements, per-row block
+  // contribution lists, element matrices; built on first use
+  bool fd_built = false, fd_mode = false;
+  int fd_opt = 0;  // PNP_OPT_JAC_FD: every Jacobian assembly (Newton's too) by forward differences
+  int fd_ne = 0;
+  DBuf<int> fd_etri, fd_cdata;
+  DBuf<long long> fd_rptr;
+  DBuf<double> fd_jel;
+  // device CSR view (pnp_jacobian_csr_device): structure per block pattern, values per request
+  int csr_pat = -1, csr_nf = 0;
+  long long csr_nnz = 0;
+  DBuf<int> csr_rowptr, csr_col, csr_src;
+  DBuf<unsigned char> csr_vidx;
+  DBuf<double> csr_val;
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
   // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
   // global segment order
@@ -379,17 +393,28 @@ struct pnp_ctx {
     return PNP_OK;
   }
 
-  int upload_ext(const double *host, int nfv, double *dev, bool with_ghosts) {
+  // external (lexicographic, global) vector -> the internal layout; devptr: `host` is a device
+  // pointer (PNP_DEVICE_PTRS), gathered from directly
+  int upload_ext(const double *host, int nfv, double *dev, bool with_ghosts, bool devptr = false) {
     size_t ne = size_t(mesh.nv) * nfv;
-    hipError_t e = hipMemcpyAsync(ext.p, host, sizeof(double) * ne, hipMemcpyHostToDevice, stream);
+    hipError_t e = hipSuccess;
+    if (!devptr)
+      e = hipMemcpyAsync(ext.p, host, sizeof(double) * ne, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess)
       e = pnp::launch_gather_ext(with_ghosts ? L.n_owned + L.n_ghost : L.n_owned, nfv, mesh.nv,
-                                 d_l2g.p, ext.p, dev, stream);
+                                 d_l2g.p, devptr ? host : ext.p, dev, stream);
     if (e != hipSuccess) return hipfail(e, "upload");
     return PNP_OK;
   }
 
-  int download_ext(const double *dev, int nfv, double *host) {
+  // internal -> external; this rank's owned entries are written (devptr: into device memory,
+  // synchronised before return)
+  int download_ext(const double *dev, int nfv, double *host, bool devptr = false) {
+    if (devptr) {
+      hipError_t e = pnp::launch_scatter_ext(L.n_owned, nfv, mesh.nv, d_l2g.p, dev, host, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "download");
+    }
     size_t ne = size_t(mesh.nv) * nfv;
     hipError_t e = pnp::launch_scatter_ext(L.n_owned, nfv, mesh.nv, d_l2g.p, dev, ext.p, stream);
     std::vector<double> tmp(ne);
@@ -406,11 +431,16 @@ struct pnp_ctx {
 
   int assemble(const double *xdev, int jac) {
     if (kind < 0) return fail(PNP_E_STATE, "no operator set (pnp_set_operator)");
+    int rc;
+    if (jac && (rc = set_fd(fd_opt != 0))) return rc;
     aa.x = xdev;
-    aa.jac = jac;
+    aa.jac = fd_mode ? 0 : jac;
     aa.r = r.p;
     hipEvent_t t0 = tb(T_ASM);
     hipError_t e = pnp::launch_assemble(dl, aa, stream);
+    if (e == hipSuccess && jac && fd_mode)
+      e = pnp::launch_fd_jacobian(dl, aa, nf, pat, fd_ne, fd_etri.p, fd_rptr.p, fd_cdata.p,
+                                  fd_jel.p, stream);
     if (e != hipSuccess) return hipfail(e, "assemble");
     te(T_ASM, t0);
     if (jac) {
@@ -419,6 +449,108 @@ struct pnp_ctx {
       split_of = 0;
       amg_valid = false;
     }
+    return PNP_OK;
+  }
+
+  // analytic (k-form) or forward-difference (expanded, kPat*FD) storage of the next Jacobian
+  int set_fd(bool on) {
+    if (on == fd_mode) return PNP_OK;
+    int rc;
+    if (on && !fd_built && (rc = fd_build())) return rc;
+    const int base = kind == PNP_OP_PNP ? pnp::kPatPnp
+                                        : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE
+                                                                            : pnp::kPatScalar);
+    pat = (on && nf == 3) ? (base | pnp::kPatFD) : base;
+    nks = pnp::nks_of(pat);
+    fd_mode = on;
+    assembled = false;
+    lu_valid = false;
+    split_of = 0;
+    amg_valid = false;
+    if (on) {
+      const size_t need = size_t(fd_ne) * 9 * nf * nf;
+      if (fd_jel.n < need) {
+        hipError_t e = fd_jel.alloc(need);
+        if (e != hipSuccess) return hipfail(e, "fd element matrices");
+      }
+    }
+    // padding slots must read as zeros in the new value layout (the SpMV multiplies them)
+    hipError_t e = hipMemsetAsync(vals.p, 0, sizeof(double) * size_t(L.nslots) * nks, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "clear matrix");
+  }
+
+  // local elements (ascending global id, vertices in mesh order) and, per owned row and slot, the
+  // element entries summed into that block, in ascending element order
+  int fd_build() {
+    const pnp::Mesh &m = mesh;
+    std::vector<int> et;
+    for (int e = 0; e < m.nt; e++) {
+      const int *t = &m.tri[3 * size_t(e)];
+      const int l0 = L.g2l[t[0]], l1 = L.g2l[t[1]], l2 = L.g2l[t[2]];
+      const bool mine = (l0 >= 0 && l0 < L.n_owned) || (l1 >= 0 && l1 < L.n_owned) ||
+                        (l2 >= 0 && l2 < L.n_owned);
+      if (!mine) continue;
+      if (l0 < 0 || l1 < 0 || l2 < 0) return fail(PNP_E_MESH, "FD Jacobian: element not local");
+      et.push_back(l0);
+      et.push_back(l1);
+      et.push_back(l2);
+    }
+    const int ne = int(et.size() / 3);
+    auto pos_of = [&](int row, int col) -> long long {
+      const int ch = row / pnp::kRows, ln = row % pnp::kRows, len = pnp::meta_len(L.rowmeta[row]);
+      if (col == row) return L.chunk_off[ch] + ln;
+      for (int sl = 1; sl < len; sl++) {
+        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
+        if (L.colidx[p] == col) return p;
+      }
+      return -1;
+    };
+    std::vector<int> cnt(size_t(L.nslots) + 1, 0);
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < 3; a++) {
+        const int va = et[3 * size_t(e) + a];
+        if (va >= L.n_owned) continue;
+        for (int b = 0; b < 3; b++) {
+          const long long p = pos_of(va, et[3 * size_t(e) + b]);
+          if (p < 0) return fail(PNP_E_MESH, "FD Jacobian: element pair outside the pattern");
+          cnt[p]++;
+        }
+      }
+    // per row: for each slot, the count then its codes
+    std::vector<long long> rptr(L.n_owned + 1, 0);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      long long n = 0;
+      for (int sl = 0; sl < len; sl++) n += 1 + cnt[L.chunk_off[ch] + 64LL * sl + ln];
+      rptr[i + 1] = rptr[i] + n;
+    }
+    std::vector<long long> at((size_t)L.nslots, -1LL);  // next free code position of each block
+    std::vector<int> data((size_t)rptr[L.n_owned]);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      long long q = rptr[i];
+      for (int sl = 0; sl < len; sl++) {
+        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
+        data[q] = cnt[p];
+        at[p] = q + 1;
+        q += 1 + cnt[p];
+      }
+    }
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < 3; a++) {
+        const int va = et[3 * size_t(e) + a];
+        if (va >= L.n_owned) continue;
+        for (int b = 0; b < 3; b++) {
+          const long long p = pos_of(va, et[3 * size_t(e) + b]);
+          data[at[p]++] = e * 9 + a * 3 + b;
+        }
+      }
+    int rc;
+    if ((rc = upv(fd_etri, et, "fd elements")) || (rc = upv(fd_rptr, rptr, "fd rptr")) ||
+        (rc = upv(fd_cdata, data, "fd contributions")))
+      return rc;
+    fd_ne = ne;
+    fd_built = true;
     return PNP_OK;
   }
 
@@ -897,7 +1029,13 @@ using pnp_ctx_t = pnp_ctx;
 
 // host copy of kernels.h expand_k + mask_rows for the CSR export
 static void expand_host(int pat, const double *K, unsigned dm, bool diag, double *B) {
-  if (pat == pnp::kPatPnp) {
+  if (pat == pnp::kPatPnpFD) {
+    pnp::expand_k<pnp::kPatPnpFD>(K, B);
+    pnp::mask_rows<3, pnp::kPatPnpFD>(B, dm, diag);
+  } else if (pat == pnp::kPatPnpIEFD) {
+    pnp::expand_k<pnp::kPatPnpIEFD>(K, B);
+    pnp::mask_rows<3, pnp::kPatPnpIEFD>(B, dm, diag);
+  } else if (pat == pnp::kPatPnp) {
     pnp::expand_k<pnp::kPatPnp>(K, B);
     pnp::mask_rows<3, pnp::kPatPnp>(B, dm, diag);
   } else if (pat == pnp::kPatPnpIE) {
@@ -1389,6 +1527,7 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   if (kind == PNP_OP_POISSON && (!a->cp || !a->cm))
     return c->fail(PNP_E_ARG, "Poisson operator needs cp and cm");
   c->kind = kind;
+  c->fd_mode = false;  // the next Jacobian picks its form (set_fd)
   c->nf = (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER) ? 3 : 1;
   c->pat = kind == PNP_OP_PNP ? pnp::kPatPnp
                               : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE : pnp::kPatScalar);
@@ -1526,7 +1665,7 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
       for (int g = 0; g < nf; g++) dm |= unsigned(c->hmask[size_t(i) * nf + g] != 0) << g;
       for (int s = 0; s < len; s++) {
         int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows + lane];
-        double K[8], B[9];
+        double K[9], B[9];
         for (int q = 0; q < NKS; q++)
           K[q] = hv[(size_t(L.chunk_off[chunk]) + size_t(s) * pnp::kRows) * NKS +
                     pnp::vin(NKS, q, lane)];
@@ -1546,6 +1685,146 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
     }
   }
   for (int i = 0; i <= n; i++) rowptr[i] = cnt[i];
+  return PNP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// flags / device pointers / FD Jacobian / jacobian_apply / device CSR view
+// ---------------------------------------------------------------------------------------------
+static int check_flags(pnp_ctx *c, int32_t flags, int32_t allowed) {
+  if (flags & ~allowed) return c->fail(PNP_E_ARG, "unsupported flags for this call");
+  return PNP_OK;
+}
+
+extern "C" int pnp_residual_ex(pnp_ctx *c, const double *x, double *r, int32_t flags) {
+  if (!c || !x || !r) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  int rc;
+  if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS))) return rc;
+  hipSetDevice(c->device);
+  const bool dev = flags & PNP_DEVICE_PTRS;
+  if ((rc = c->upload_ext(x, c->nf, c->x.p, true, dev))) return rc;
+  if ((rc = c->assemble(c->x.p, 0))) return rc;
+  return c->download_ext(c->r.p, c->nf, r, dev);
+}
+
+extern "C" int pnp_jacobian_ex(pnp_ctx *c, const double *x, int32_t flags) {
+  if (!c || !x) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  int rc;
+  if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS | PNP_JAC_FD))) return rc;
+  hipSetDevice(c->device);
+  if ((rc = c->upload_ext(x, c->nf, c->x.p, true, flags & PNP_DEVICE_PTRS))) return rc;
+  const int keep = c->fd_opt;
+  if (flags & PNP_JAC_FD) c->fd_opt = 1;
+  rc = c->assemble(c->x.p, 1);
+  c->fd_opt = keep;
+  if (rc) return rc;
+  CK(hipStreamSynchronize(c->stream), "jacobian");
+  return PNP_OK;
+}
+
+extern "C" int pnp_jacobian_apply(pnp_ctx *c, const double *x, const double *z, double *y,
+                                  int32_t flags) {
+  if (!c || !z || !y) return PNP_E_ARG;
+  if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
+  int rc;
+  if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS | PNP_JAC_FD))) return rc;
+  hipSetDevice(c->device);
+  const bool dev = flags & PNP_DEVICE_PTRS;
+  if (x) {
+    if ((rc = pnp_jacobian_ex(c, x, flags))) return rc;
+  } else if (!c->assembled) {
+    return c->fail(PNP_E_STATE, "no Jacobian assembled (pass x)");
+  }
+  // z with ghosts (the halo of a global vector is local: every rank holds it), y = A z
+  if ((rc = c->upload_ext(z, c->nf, c->y.p, true, dev))) return rc;
+  int nsp = 0;
+  CK(pnp::launch_spmv(c->dl, c->nf, c->pat, c->vals.p, c->y.p, c->t.p, 0, nullptr, c->partials.p,
+                      &nsp, c->stream),
+     "jacobian apply");
+  return c->download_ext(c->t.p, c->nf, y, dev);
+}
+
+extern "C" int pnp_linear_solve_ex(pnp_ctx *c, const double *rhs, double *z,
+                                   const pnp_solve_opts *o, pnp_solve_result *res, int32_t flags) {
+  if (!c || !rhs || !z || !o || !res) return PNP_E_ARG;
+  int rc;
+  if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS))) return rc;
+  hipSetDevice(c->device);
+  std::memset(res, 0, sizeof *res);
+  const bool dev = flags & PNP_DEVICE_PTRS;
+  if ((rc = c->upload_ext(rhs, c->nf, c->b.p, false, dev))) return rc;
+  if ((rc = c->krylov(c->b.p, c->z.p, *o, *res))) return rc;
+  if ((rc = c->download_ext(c->z.p, c->nf, z, dev))) return rc;
+  return res->breakdown ? PNP_E_BREAKDOWN : PNP_OK;
+}
+
+extern "C" int pnp_jacobian_csr_device(pnp_ctx *c, pnp_csr_view *out) {
+  if (!c || !out) return PNP_E_ARG;
+  if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
+  hipSetDevice(c->device);
+  const pnp::LocalLayout &L = c->L;
+  const int nf = c->nf, nv = c->mesh.nv, mask = c->pat & 0x1FF;
+  if (c->csr_pat != mask || c->csr_nf != nf) {  // structure of this block pattern (host, once)
+    const int n = nf * nv;
+    std::vector<int> cnt(n + 1, 0);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int len = pnp::meta_len(L.rowmeta[i]);
+      for (int f = 0; f < nf; f++) {
+        int k = 0;
+        for (int g = 0; g < nf; g++) k += pnp::pat_index(mask, f, g) >= 0;
+        cnt[f * nv + L.l2g[i] + 1] += k * len;
+      }
+    }
+    for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+    const long long nnz = cnt[n];
+    std::vector<int> col(nnz), src(nnz);
+    std::vector<unsigned char> vid(nnz);
+    struct E {
+      int col, src;
+      unsigned char v;
+    };
+    std::vector<E> tmp;
+    for (int i = 0; i < L.n_owned; i++) {
+      const int chunk = i / pnp::kRows, lane = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      for (int f = 0; f < nf; f++) {
+        tmp.clear();
+        for (int sl = 0; sl < len; sl++) {
+          const int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(sl) * pnp::kRows + lane];
+          for (int g = 0; g < nf; g++) {
+            const int v = pnp::pat_index(mask, f, g);
+            if (v >= 0) tmp.push_back({g * nv + L.l2g[j], i << 6 | sl, (unsigned char)v});
+          }
+        }
+        std::sort(tmp.begin(), tmp.end(), [](const E &a, const E &b) { return a.col < b.col; });
+        long long q = cnt[f * nv + L.l2g[i]];
+        for (const E &e : tmp) {
+          col[q] = e.col;
+          src[q] = e.src;
+          vid[q] = e.v;
+          q++;
+        }
+      }
+    }
+    int rc;
+    if ((rc = c->upv(c->csr_rowptr, cnt, "csr rowptr")) || (rc = c->upv(c->csr_col, col, "csr col")) ||
+        (rc = c->upv(c->csr_src, src, "csr src")) || (rc = c->upv(c->csr_vidx, vid, "csr vidx")))
+      return rc;
+    CK(c->csr_val.alloc(std::max<long long>(1, nnz)), "csr values");
+    c->csr_nnz = nnz;
+    c->csr_pat = mask;
+    c->csr_nf = nf;
+  }
+  CK(pnp::launch_csr_fill(c->dl, nf, c->pat, c->vals.p, c->csr_nnz, c->csr_src.p, c->csr_vidx.p,
+                          c->csr_val.p, c->stream),
+     "csr fill");
+  CK(hipStreamSynchronize(c->stream), "csr fill");
+  out->n = nf * nv;
+  out->nnz = c->csr_nnz;
+  out->rowptr = c->csr_rowptr.p;
+  out->col = c->csr_col.p;
+  out->val = c->csr_val.p;
   return PNP_OK;
 }
 
@@ -1585,6 +1864,11 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     }
     return PNP_OK;
   }
+  if (option == PNP_OPT_JAC_FD) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_JAC_FD takes 0 or 1");
+    c->fd_opt = int(value);
+    return PNP_OK;
+  }
   if (option == PNP_OPT_ILU_FUSED_FACTOR) {
     if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_FUSED_FACTOR takes 0 or 1");
     c->ilu_fused = int(value);
@@ -1603,6 +1887,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_ILU_FUSED_FACTOR) {
     *value = c->ilu_fused;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_JAC_FD) {
+    *value = c->fd_opt;
     return PNP_OK;
   }
   return c->fail(PNP_E_ARG, "unknown option");

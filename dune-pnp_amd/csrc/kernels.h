@@ -138,6 +138,12 @@ enum OpKind : int {
 constexpr int kPatPnp = 0x1FF & ~((1 << 5) | (1 << 7));
 constexpr int kPatPnpIE = 0x1FF & ~(1 << 7);
 constexpr int kPatScalar = 1;
+// bit 9: the block's pattern values are stored as they are (no k-form) -- the forward-difference
+// Jacobian (PNP_JAC_FD), whose entries do not satisfy the analytic block's identities.  Scalar
+// operators need no FD variant (their k-form is the value itself).
+constexpr int kPatFD = 1 << 9;
+constexpr int kPatPnpFD = kPatPnp | kPatFD;
+constexpr int kPatPnpIEFD = kPatPnpIE | kPatFD;
 
 __host__ __device__ constexpr int popc9(int m) {
   int c = 0;
@@ -160,12 +166,15 @@ __host__ __device__ constexpr int pat_index(int mask, int f, int g) {
 // value itself.  expand_k gives the block pattern's values exactly (each is one coefficient, its
 // negation, or k0 -+ k4 (+ k5)); Dirichlet rows (mask_rows) become identity rows.
 __host__ __device__ constexpr int nks_of(int pat) {
-  return pat == kPatPnp ? 5 : (pat == kPatPnpIE ? 6 : 1);
+  return (pat & kPatFD) ? popc9(pat) : (pat == kPatPnp ? 5 : (pat == kPatPnpIE ? 6 : 1));
 }
 
 template <int PAT>
 __host__ __device__ __forceinline__ void expand_k(const double *K, double *B) {
-  if constexpr (PAT == kPatPnp || PAT == kPatPnpIE) {
+  if constexpr ((PAT & kPatFD) != 0) {
+#pragma unroll
+    for (int q = 0; q < popc9(PAT); q++) B[q] = K[q];
+  } else if constexpr (PAT == kPatPnp || PAT == kPatPnpIE) {
     B[pat_index(PAT, 0, 0)] = K[0];
     B[pat_index(PAT, 0, 1)] = K[1];
     B[pat_index(PAT, 0, 2)] = -K[1];
@@ -350,6 +359,17 @@ hipError_t launch_gather_ext(int n, int nf, int nv_global, const int *l2g, const
                              double *in, hipStream_t s);
 hipError_t launch_scatter_ext(int n, int nf, int nv_global, const int *l2g, const double *in,
                               double *ext, hipStream_t s);
+// forward-difference Jacobian (fd_jacobian.hip, PNP_JAC_FD): element matrices of the ne local
+// elements (etri: local vertex ids in mesh order, ascending global element id) into jel
+// [ne][3nf][3nf], then every SELL block of the owned rows summed from them (rptr / cdata: per row,
+// per slot a count and the codes e*9 + a*3 + b) into aa.vals in the FD pattern `pat`
+hipError_t launch_fd_jacobian(const DevLayout &L, const AsmArgs &aa, int nf, int pat, int ne,
+                              const int *etri, const long long *rptr, const int *cdata,
+                              double *jel, hipStream_t s);
+// device CSR values of the assembled Jacobian: out[k] = value vidx[k] of block src[k] (row << 6 |
+// slot), expanded and row-masked (pnp_jacobian_csr_device)
+hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *vals, long long nnz,
+                           const int *src, const unsigned char *vidx, double *out, hipStream_t s);
 // read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
 hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 

@@ -1065,6 +1065,12 @@ int blas_nparts(long long n) {
     } else if ((NF_) == 3 && (PAT_) == kPatPnpIE) {                       \
       constexpr int NFc = 3, PATc = kPatPnpIE;                            \
       CALL;                                                               \
+    } else if ((NF_) == 3 && (PAT_) == kPatPnpFD) {                       \
+      constexpr int NFc = 3, PATc = kPatPnpFD;                            \
+      CALL;                                                               \
+    } else if ((NF_) == 3 && (PAT_) == kPatPnpIEFD) {                     \
+      constexpr int NFc = 3, PATc = kPatPnpIEFD;                          \
+      CALL;                                                               \
     } else if ((NF_) == 1) {                                              \
       constexpr int NFc = 1, PATc = kPatScalar;                           \
       CALL;                                                               \
@@ -1472,6 +1478,40 @@ hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_
   if (n < 2) return hipSuccess;
   hipLaunchKernelGGL(k_scrub, dim3(4096), dim3(256), 0, s, reinterpret_cast<const double2 *>(buf),
                      n / 2, sink);
+  return hipGetLastError();
+}
+}  // namespace pnp
+
+namespace pnp {
+namespace {
+// device CSR view of the assembled Jacobian: entry k takes value v of block (row, slot) =
+// (src[k] >> 6, src[k] & 63), expanded from the stored form and row-masked
+template <int NF, int PAT>
+__global__ __launch_bounds__(kBlock) void k_csr_fill(DevLayout L, const double *__restrict__ vals,
+                                                     long long nnz, const int *__restrict__ src,
+                                                     const unsigned char *__restrict__ vidx,
+                                                     double *__restrict__ out) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
+  const long long k = blockIdx.x * (long long)kBlock + threadIdx.x;
+  if (k >= nnz) return;
+  const int code = src[k], row = code >> 6, slot = code & 63;
+  const int chunk = row / kRows, lane = row % kRows;
+  double K[NK], B[NV];
+  load_vals<NK>(vals + (size_t(L.chunk_off[chunk]) + size_t(slot) * kRows) * NK, lane, K);
+  expand_k<PAT>(K, B);
+  mask_rows<NF, PAT>(B, row_mask<NF>(L, row), slot == 0);
+  out[k] = B[vidx[k]];
+}
+}  // namespace
+
+hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *vals, long long nnz,
+                           const int *src, const unsigned char *vidx, double *out, hipStream_t s) {
+  if (nnz == 0) return hipSuccess;
+  const dim3 g(unsigned((nnz + kBlock - 1) / kBlock));
+  PNP_PAT_DISPATCH(nf, pat, {
+    hipLaunchKernelGGL((k_csr_fill<NFc, PATc>), g, dim3(kBlock), 0, s, L, vals, nnz, src, vidx,
+                       out);
+  });
   return hipGetLastError();
 }
 }  // namespace pnp

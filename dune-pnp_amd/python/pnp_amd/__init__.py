@@ -33,7 +33,8 @@ OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = 
 OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG = range(5)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
-OPT_ILU_F32, OPT_ILU_FUSED_FACTOR = 1, 2
+OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD = 1, 2, 3
+DEVICE_PTRS, JAC_FD = 1, 2
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
                 "jacobi": PREC_JACOBI, "amg": PREC_AMG}
 MAX_SURFACES = 64
@@ -141,6 +142,11 @@ class _Timers(C.Structure):
                 ("assemble_launches", C.c_int64), ("spmv_launches", C.c_int64),
                 ("prec_launches", C.c_int64), ("blas_launches", C.c_int64),
                 ("factor_ms", C.c_double), ("factor_launches", C.c_int64)]
+
+
+class _CsrView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("nnz", C.c_int64), ("rowptr", C.c_void_p), ("col", C.c_void_p),
+                ("val", C.c_void_p)]
 
 
 class _Layout(C.Structure):
@@ -455,11 +461,15 @@ class Context:
         self._ck(lib().pnp_residual(self.h, _ptr(x), _ptr(r)))
         return r
 
-    def jacobian(self, x, export=True):
+    def jacobian(self, x, export=True, fd=False):
+        """Assemble J(x) (fd: the reference's forward-difference Jacobian, PNP_JAC_FD)."""
         x = self._vec(x)
-        self._ck(lib().pnp_jacobian(self.h, _ptr(x)))
+        self._ck(lib().pnp_jacobian_ex(self.h, _ptr(x), JAC_FD if fd else 0))
         if not export:
             return None
+        return self.jacobian_export()
+
+    def jacobian_export(self):
         import scipy.sparse as sp
         nnz = C.c_int64()
         self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), None, None, None))
@@ -469,6 +479,44 @@ class Context:
         val = np.zeros(nnz.value, dtype=np.float64)
         self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), _ptr(rp), _ptr(col), _ptr(val)))
         return sp.csr_matrix((val, col, rp), shape=(n, n))
+
+    def jacobian_apply(self, z, x=None, fd=False):
+        """GridOperator::jacobian_apply: J(x) z (x None: the last assembled Jacobian)."""
+        z = self._vec(z)
+        xv = None if x is None else self._vec(x)
+        y = np.zeros_like(z)
+        self._ck(lib().pnp_jacobian_apply(self.h, _ptr(xv), _ptr(z), _ptr(y), JAC_FD if fd else 0))
+        return y
+
+    # raw device-pointer calls (PNP_DEVICE_PTRS): integer addresses of device buffers, e.g. a
+    # torch tensor's data_ptr()
+    def residual_dev(self, x_ptr, r_ptr):
+        self._ck(lib().pnp_residual_ex(self.h, C.c_void_p(x_ptr), C.c_void_p(r_ptr), DEVICE_PTRS))
+
+    def jacobian_dev(self, x_ptr, fd=False):
+        self._ck(lib().pnp_jacobian_ex(self.h, C.c_void_p(x_ptr),
+                                       DEVICE_PTRS | (JAC_FD if fd else 0)))
+
+    def jacobian_apply_dev(self, x_ptr, z_ptr, y_ptr, fd=False):
+        self._ck(lib().pnp_jacobian_apply(self.h, C.c_void_p(x_ptr) if x_ptr else None,
+                                          C.c_void_p(z_ptr), C.c_void_p(y_ptr),
+                                          DEVICE_PTRS | (JAC_FD if fd else 0)))
+
+    def linear_solve_dev(self, rhs_ptr, z_ptr, prec=PREC_NONE, reduction=1e-8, maxit=20000,
+                         check_every=8, method=0):
+        o = _SolveOpts(prec, reduction, maxit, check_every, method)
+        r = _SolveResult()
+        rc = lib().pnp_linear_solve_ex(self.h, C.c_void_p(rhs_ptr), C.c_void_p(z_ptr), C.byref(o),
+                                       C.byref(r), DEVICE_PTRS)
+        if rc not in (OK, E_BREAKDOWN):
+            self._ck(rc)
+        return {k: getattr(r, k) for k, _ in _SolveResult._fields_}
+
+    def jacobian_csr_device(self):
+        """Device CSR view of the last assembled Jacobian: dict of n, nnz and device addresses."""
+        v = _CsrView()
+        self._ck(lib().pnp_jacobian_csr_device(self.h, C.byref(v)))
+        return {"n": v.n, "nnz": v.nnz, "rowptr": v.rowptr, "col": v.col, "val": v.val}
 
     def linear_solve(self, rhs, prec=PREC_NONE, reduction=1e-8, maxit=20000, check_every=8,
                      method=0):

@@ -195,6 +195,41 @@ int pnp_jacobian(pnp_ctx *ctx, const double *x);
  * Pass NULL arrays to query nnz first. */
 int pnp_jacobian_export(pnp_ctx *ctx, int64_t *nnz, int32_t *rowptr, int32_t *col, double *val);
 
+/* ---- call flags, device pointers, FD Jacobian, jacobian_apply, device CSR view ---------------- */
+enum {
+  /* vectors passed to the call are DEVICE pointers (same device as the context), external
+   * layout; results are written to device memory (this rank's owned entries) and the call is
+   * synchronous on return */
+  PNP_DEVICE_PTRS = 1,
+  /* the Jacobian is PDELab's NumericalJacobianVolume (src/pnp_operator.hh:24-27 and the other
+   * LOPs' mixins): per element the local residual at u and at u + delta_j e_j, delta_j =
+   * 1e-7 (1 + |u_j|), columns (r(u + delta_j e_j) - r(u)) / delta_j, accumulated element by element
+   * in mesh order.  Computed on the GPU in the reference's operand order (no FMA contraction):
+   * for the polynomial operators it is the oracle's FD matrix to the last bits. */
+  PNP_JAC_FD = 2
+};
+/* pnp_residual with flags (PNP_DEVICE_PTRS) */
+int pnp_residual_ex(pnp_ctx *ctx, const double *x, double *r, int32_t flags);
+/* pnp_jacobian with flags (PNP_DEVICE_PTRS, PNP_JAC_FD) */
+int pnp_jacobian_ex(pnp_ctx *ctx, const double *x, int32_t flags);
+/* GridOperator::jacobian_apply (the LOPs' NumericalJacobianApplyVolume, src/pnp_operator.hh:22-25):
+ * y = J(x) z with J the matrix pnp_jacobian assembles (constrained rows identity).  x != NULL
+ * assembles J(x) first (PNP_JAC_FD: by forward differences); x == NULL applies the last
+ * assembled Jacobian.  z, y: external layout, nfields*nv; PNP_DEVICE_PTRS for device vectors. */
+int pnp_jacobian_apply(pnp_ctx *ctx, const double *x, const double *z, double *y, int32_t flags);
+/* device CSR view of the last assembled Jacobian (the ISTL BCRSMatrix<1x1> the reference's
+ * solvers take): external layout, sorted columns, the stored block pattern (structurally zero
+ * c+/c- couplings omitted), constrained rows identity.  The arrays are DEVICE memory owned by the
+ * context, valid until the next Jacobian assembly, pnp_set_operator or pnp_destroy. */
+typedef struct {
+  int32_t n;            /* rows = nfields * nv (rows owned by other ranks are empty) */
+  int64_t nnz;
+  const int32_t *rowptr;/* n + 1 */
+  const int32_t *col;
+  const double *val;
+} pnp_csr_view;
+int pnp_jacobian_csr_device(pnp_ctx *ctx, pnp_csr_view *view);
+
 /* ---- linear solve (ISTL BiCGSTABSolver semantics) ----------------------------------------- */
 enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3,
        PNP_PREC_AMG = 4 /* aggregation AMG V-cycle (ISTL Amg::AMG of LINEARSOLVER CG_AMG_SSOR,
@@ -269,7 +304,10 @@ enum {
   /* 1 (default): ILU(0) factorisation in one launch per colour with the k-form expansion and the
    * split into L / U storage folded in; 0: the three-pass path (expand, factor, split).  Both
    * give the same factors bit for bit. */
-  PNP_OPT_ILU_FUSED_FACTOR = 2
+  PNP_OPT_ILU_FUSED_FACTOR = 2,
+  /* 1: every Jacobian assembly of the context (pnp_jacobian, Newton, pnp_assemble_state) is the
+   * reference's forward-difference Jacobian (as PNP_JAC_FD); 0 (default): analytic */
+  PNP_OPT_JAC_FD = 3
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
@@ -277,6 +315,9 @@ int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
 /* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */
 int pnp_linear_solve(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,
                      pnp_solve_result *res);
+/* pnp_linear_solve with flags (PNP_DEVICE_PTRS) */
+int pnp_linear_solve_ex(pnp_ctx *ctx, const double *rhs, double *z, const pnp_solve_opts *opts,
+                        pnp_solve_result *res, int32_t flags);
 
 /* ---- Newton (PDELab Newton with hackbuschReuskenAcceptBest) -------------------------------- */
 typedef struct {

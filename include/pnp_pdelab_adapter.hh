@@ -165,14 +165,29 @@ class GridOperator {
     for (size_t i = 0; i < tmp.size(); i++) rp[i] += tmp[i];
   }
   void jacobian(const V &x, Matrix &m) const {
-    check(pnp_jacobian(ctx_.get(), data(x)), ctx_.get());
+    check(pnp_jacobian_ex(ctx_.get(), data(x), numerical_ ? PNP_JAC_FD : 0), ctx_.get());
     m.assembled = true;
+  }
+  // PDELab semantics: y += J(x) z (the LOPs' NumericalJacobianApplyVolume/Boundary mixins)
+  void jacobian_apply(const V &x, const V &z, V &y) const {
+    std::vector<double> tmp(size());
+    check(pnp_jacobian_apply(ctx_.get(), data(x), data(z), tmp.data(), numerical_ ? PNP_JAC_FD : 0),
+          ctx_.get());
+    double *yp = data(y);
+    for (size_t i = 0; i < tmp.size(); i++) yp[i] += tmp[i];
+  }
+  // the reference's NumericalJacobianVolume (forward differences, eps 1e-7) instead of the analytic
+  // Jacobian, for this operator's jacobian / jacobian_apply and for Newton on this context
+  void setNumericalJacobian(bool on) {
+    numerical_ = on;
+    check(pnp_set_option(ctx_.get(), PNP_OPT_JAC_FD, on ? 1 : 0), ctx_.get());
   }
   Context &context() const { return ctx_; }
 
  private:
   Context &ctx_;
   Operator lop_;
+  bool numerical_ = false;
 };
 
 struct InverseOperatorResult {  // Dune::InverseOperatorResult
