@@ -127,7 +127,25 @@ struct pnp_ctx {
   }();
   int f32_now() const { return split_of == 2 ? ilu_f32 : 0; }
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
+  int twored_opt = [] {  // PNP_OPT_BICG_TWORED: -1 auto (on with more than one rank), 0, 1
+    const char *ev = std::getenv("PNP_BICG_TWORED");
+    return ev ? (std::atoi(ev) != 0 ? 1 : 0) : -1;
+  }();
   DBuf<int> d_blkmap;
+  // halo-overlapped SpMV (multi-GPU): 256-row blocks without / with ghost columns, each in the
+  // spatial order of blkmap; the halo runs on cstream while the interior blocks compute
+  DBuf<int> d_blk_int, d_blk_bnd;
+  int n_blk_int = 0, n_blk_bnd = 0;
+  bool split_spmv = false;
+  pnp::DevLayout sub_layout(bool interior) const {
+    pnp::DevLayout d = dl;
+    d.blkmap = interior ? d_blk_int.p : d_blk_bnd.p;
+    const int n = interior ? n_blk_int : n_blk_bnd;
+    d.blkcount = n > 0 ? n : -1;  // -1: no block (launch nothing)
+    return d;
+  }
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
   DBuf<double> scrub;  // pnp_cache_scrub (cache-cold benchmark timings)
   // forward-difference Jacobian (PNP_JAC_FD, fd_jacobian.hip): local elements, per-row block
   // contribution lists, element matrices; built on first use
@@ -199,6 +217,9 @@ struct pnp_ctx {
     if (hS) hipHostFree(hS);
     if (comm) ncclCommDestroy(comm);
     if (blas) rocblas_destroy_handle(blas);
+    if (ev_ready) hipEventDestroy(ev_ready);
+    if (ev_halo) hipEventDestroy(ev_halo);
+    if (cstream) hipStreamDestroy(cstream);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -253,28 +274,75 @@ struct pnp_ctx {
   // ---- helpers ------------------------------------------------------------------------------
   long long nown() const { return (long long)L.n_owned * nf; }
 
-  int halo(double *vec, int nfv) {
+  int halo(double *vec, int nfv) { return halo_on(vec, nfv, stream); }
+
+  int halo_on(double *vec, int nfv, hipStream_t hs) {
     if (nranks == 1) return PNP_OK;
     if (lg) return halo_local(vec, nfv);
     if (L.nbr_ranks.empty()) return PNP_OK;
-    hipEvent_t t0 = tb(T_HALO);
+    hipEvent_t t0 = hs == stream ? tb(T_HALO) : nullptr;
     int ns = int(L.send_idx.size());
-    hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, stream);
+    hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, hs);
     if (e != hipSuccess) return hipfail(e, "halo pack");
     if (ncclGroupStart() != ncclSuccess) return fail(PNP_E_RCCL, "ncclGroupStart");
     for (size_t q = 0; q < L.nbr_ranks.size(); q++) {
       int peer = L.nbr_ranks[q];
       size_t sc = size_t(L.send_ptr[q + 1] - L.send_ptr[q]) * nfv;
       size_t rc = size_t(L.recv_ptr[q + 1] - L.recv_ptr[q]) * nfv;
-      if (ncclSend(sendbuf.p + size_t(L.send_ptr[q]) * nfv, sc, ncclDouble, peer, comm, stream) !=
+      if (ncclSend(sendbuf.p + size_t(L.send_ptr[q]) * nfv, sc, ncclDouble, peer, comm, hs) !=
           ncclSuccess)
         return fail(PNP_E_RCCL, "ncclSend");
       if (ncclRecv(vec + (size_t(L.n_owned) + L.recv_ptr[q]) * nfv, rc, ncclDouble, peer, comm,
-                   stream) != ncclSuccess)
+                   hs) != ncclSuccess)
         return fail(PNP_E_RCCL, "ncclRecv");
     }
     if (ncclGroupEnd() != ncclSuccess) return fail(PNP_E_RCCL, "ncclGroupEnd");
-    te(T_HALO, t0);
+    if (t0) te(T_HALO, t0);
+    return PNP_OK;
+  }
+
+  // halo exchange of vin's ghosts + y = A vin (mode / dots as launch_spmv).  Multi-GPU with the
+  // split layout: the interior blocks (no ghost columns) run while the halo is in flight on
+  // cstream, then the boundary blocks; their partials follow each other, *nsp counts both.
+  int halo_spmv(double *vin, double *yout, int mode, const double *w, const double *w2, int *nsp) {
+    hipError_t e;
+    if (!split_spmv) {
+      int rc = halo(vin, nf);
+      if (rc) return rc;
+      hipEvent_t t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, vin, yout, mode, w, partials.p, nsp, stream, w2);
+      if (e != hipSuccess) return hipfail(e, "spmv");
+      te(T_SPMV, t0);
+      return PNP_OK;
+    }
+    const int kd = mode == 4 ? 3 : (mode == 2 ? 2 : 1);
+    const pnp::DevLayout dl_int = sub_layout(true), dl_bnd = sub_layout(false);
+    int n1 = 0, n2 = 0, rc;
+    if (lg) {  // in-process transport: synchronous halo between the two halves
+      hipEvent_t t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl_int, nf, pat, vals.p, vin, yout, mode, w, partials.p, &n1, stream, w2);
+      if (e != hipSuccess) return hipfail(e, "spmv interior");
+      te(T_SPMV, t0);
+      if ((rc = halo(vin, nf))) return rc;
+    } else {
+      if ((e = hipEventRecord(ev_ready, stream)) != hipSuccess ||
+          (e = hipStreamWaitEvent(cstream, ev_ready, 0)) != hipSuccess)
+        return hipfail(e, "halo stream order");
+      if ((rc = halo_on(vin, nf, cstream))) return rc;
+      if ((e = hipEventRecord(ev_halo, cstream)) != hipSuccess) return hipfail(e, "halo event");
+      hipEvent_t t0 = tb(T_SPMV);
+      e = pnp::launch_spmv(dl_int, nf, pat, vals.p, vin, yout, mode, w, partials.p, &n1, stream, w2);
+      if (e != hipSuccess) return hipfail(e, "spmv interior");
+      te(T_SPMV, t0);
+      if ((e = hipStreamWaitEvent(stream, ev_halo, 0)) != hipSuccess)
+        return hipfail(e, "halo wait");
+    }
+    hipEvent_t t1 = tb(T_SPMV);
+    e = pnp::launch_spmv(dl_bnd, nf, pat, vals.p, vin, yout, mode, w, partials.p + size_t(n1) * kd,
+                         &n2, stream, w2);
+    if (e != hipSuccess) return hipfail(e, "spmv boundary");
+    te(T_SPMV, t1);
+    *nsp = n1 + n2;
     return PNP_OK;
   }
 
@@ -340,13 +408,14 @@ struct pnp_ctx {
   }
 
   // S->red = sum of partials (all ranks), then the derive step of BiCGSTAB stage `stage`
-  int reduce_derive(int np, int k, int stage) {
+  int reduce_derive(int np, int k, int stage, bool from2 = false) {
     hipError_t e;
+    const double *src = from2 ? partials2.p : partials.p;
     if (nranks == 1) {
-      e = pnp::launch_reduce(partials.p, np, k, S.p, stream, stage);
+      e = pnp::launch_reduce(src, np, k, S.p, stream, stage);
       return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
     }
-    e = pnp::launch_reduce(partials.p, np, k, S.p, stream);
+    e = pnp::launch_reduce(src, np, k, S.p, stream);
     if (e != hipSuccess) return hipfail(e, "reduce");
     int rc = allreduce_red(k);
     if (rc) return rc;
@@ -853,6 +922,13 @@ struct pnp_ctx {
       te(T_PREC, tp);
       return PNP_OK;
     };
+    // two-reduction iteration (two allreduces per iteration instead of three: rho_new from the
+    // same reduction as omega, the second half step's test lagged into the next h reduction):
+    // on by default with more than one rank, where each reduction is an allreduce round trip;
+    // PNP_OPT_BICG_TWORED (or PNP_BICG_TWORED) 0/1 forces it off/on.  Half-step counts keep
+    // ISTL's semantics.
+    const bool twored = twored_opt >= 0 ? twored_opt == 1 : nranks > 1;
+    int pending_np = 0;
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
       t0 = tb(T_BLAS);
@@ -873,24 +949,27 @@ struct pnp_ctx {
         if ((rc = precond(prec, p.p, y.p))) return rc;
         yin = y.p;
       }
-      if ((rc = halo(const_cast<double *>(yin), nf))) return rc;
-      t0 = tb(T_SPMV);
-      e = pnp::launch_spmv(dl, nf, pat, vals.p, yin, v.p, 1, rt.p, partials.p, &nsp, stream);
-      if (e != hipSuccess) return hipfail(e, "spmv h");
-      te(T_SPMV, t0);
-      if ((rc = reduce_derive(nsp, 1, 1))) return rc;
+      if ((rc = halo_spmv(const_cast<double *>(yin), v.p, 1, rt.p, nullptr, &nsp))) return rc;
+      if (twored)  // h, with the previous iteration's second-half test (||r||^2 in partials2)
+        rc = pending_np > 0 ? reduce_derive2(nsp, 1, pending_np, 1, 31) : reduce_derive(nsp, 1, 31);
+      else
+        rc = reduce_derive(nsp, 1, 1);
+      if (rc) return rc;
       // x += alpha y ; r -= alpha v ; ||r|| (partials2: its half-step test is derived together
       // with omega below -- one reduction and one allreduce fewer per iteration; the second
-      // half's kernels ignore a converged first half, update_xr skips on S->done)
+      // half's kernels ignore a converged first half, update_xr skips on S->done).  Two-reduction
+      // iteration (twored): also <rt, s> into partials2, for rho_new without a third reduction.
       t0 = tb(T_BLAS);
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, zout, yin, rs.p, v.p, nullptr,
-                                    uvals.p, y.p, partials2.p, &npu, stream, f32_now());
+                                    uvals.p, y.p, partials2.p, &npu, stream, f32_now(),
+                                    twored ? rt.p : nullptr);
       else
-        e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, nullptr, partials2.p, stream);
+        e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, twored ? rt.p : nullptr,
+                                  partials2.p, stream);
       if (e != hipSuccess) return hipfail(e, "update x r (1)");
       te(T_BLAS, t0);
-      // y = M^{-1} r ; t = A y ; <t,r>, <t,t>
+      // y = M^{-1} r ; t = A y ; <t,r>, <t,t> (twored: and <t,rt>)
       const double *yin2 = rs.p;
       if (fuse) {
         if ((rc = ilu_from1(rs.p, y.p))) return rc;
@@ -899,18 +978,25 @@ struct pnp_ctx {
         if ((rc = precond(prec, rs.p, y.p))) return rc;
         yin2 = y.p;
       }
-      if ((rc = halo(const_cast<double *>(yin2), nf))) return rc;
-      t0 = tb(T_SPMV);
-      e = pnp::launch_spmv(dl, nf, pat, vals.p, yin2, t.p, 2, rs.p, partials.p, &nsp, stream);
-      if (e != hipSuccess) return hipfail(e, "spmv t");
-      te(T_SPMV, t0);
-      if ((rc = reduce_derive2(nsp, 2, fuse ? npu : np, 1, 23))) return rc;
-      // x += omega y ; r -= omega t ; ||r||, <rt, r>
-      t0 = tb(T_BLAS);
-      e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
-      if (e != hipSuccess) return hipfail(e, "update x r (2)");
-      if ((rc = reduce_derive(np, 2, 4))) return rc;
-      te(T_BLAS, t0);
+      if ((rc = halo_spmv(const_cast<double *>(yin2), t.p, twored ? 4 : 2, rs.p, rt.p, &nsp)))
+        return rc;
+      if (twored) {
+        if ((rc = reduce_derive2(nsp, 3, fuse ? npu : np, 2, 32))) return rc;
+        // x += omega y ; r -= omega t ; ||r||^2 into partials2, tested at the next h (stage 31)
+        t0 = tb(T_BLAS);
+        e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, nullptr, partials2.p, stream);
+        if (e != hipSuccess) return hipfail(e, "update x r (2)");
+        te(T_BLAS, t0);
+        pending_np = np;
+      } else {
+        if ((rc = reduce_derive2(nsp, 2, fuse ? npu : np, 1, 23))) return rc;
+        // x += omega y ; r -= omega t ; ||r||, <rt, r>
+        t0 = tb(T_BLAS);
+        e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
+        if (e != hipSuccess) return hipfail(e, "update x r (2)");
+        if ((rc = reduce_derive(np, 2, 4))) return rc;
+        te(T_BLAS, t0);
+      }
       if (debug_trace) {
         e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipStreamSynchronize(stream);
@@ -927,6 +1013,7 @@ struct pnp_ctx {
         if (hS->done) break;
       }
     }
+    if (twored && pending_np > 0 && (rc = reduce_derive(pending_np, 1, 33, true))) return rc;
     e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "bicgstab result");
@@ -968,11 +1055,8 @@ struct pnp_ctx {
     if ((rc = reduce_derive(np, 1, 11))) return rc;
     int check = o.check_every > 0 ? o.check_every : 8;
     for (int k = 0; k < o.maxit; k++) {
-      if ((rc = halo(p.p, nf))) return rc;
-      hipEvent_t t0 = tb(T_SPMV);
-      e = pnp::launch_spmv(dl, nf, pat, vals.p, p.p, v.p, 1, p.p, partials.p, &nsp, stream);
-      if (e != hipSuccess) return hipfail(e, "cg spmv");
-      te(T_SPMV, t0);
+      if ((rc = halo_spmv(p.p, v.p, 1, p.p, nullptr, &nsp))) return rc;
+      hipEvent_t t0 = nullptr;
       if ((rc = reduce_derive(nsp, 1, 12))) return rc;
       t0 = tb(T_BLAS);
       e = pnp::launch_update_xr(n, S.p, 0, zout, p.p, rs.p, v.p, nullptr, partials.p, stream);
@@ -1425,13 +1509,14 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
       (rc = al(c->ext, 3 * size_t(c->mesh.nv), "ext")) ||
       (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
+      // up to 3 partials per workgroup (SpMV mode 4) / 2 (updates with <rt, s>)
       (rc = al(c->partials,
-               2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
+               3 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
                                     size_t(pnp::spmv_parts(L.n_owned))) + 64,
                "partials")) ||
       (rc = al(c->partials2,
-               std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
-                                size_t(pnp::spmv_parts(L.n_owned))) + 64,
+               2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
+                                    size_t(pnp::spmv_parts(L.n_owned))) + 64,
                "partials2")) ||
       (rc = al(c->S, 2, "scalars")) ||
       (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
@@ -1443,6 +1528,44 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
   if ((e = hipHostMalloc(&c->hS, 3 * sizeof(pnp::Scalars))) != hipSuccess) {
     g_err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return PNP_E_HIP;
+  }
+  if (c->nranks > 1) {  // halo-overlapped SpMV: interior / boundary 256-row blocks
+    const char *ev = getenv("PNP_HALO_OVERLAP");
+    if (!(ev && atoi(ev) == 0) && L.n_owned > 0) {
+      const int nblk = (L.n_owned + 255) / 256;
+      std::vector<int> order(nblk);
+      if (c->d_blkmap.p) {
+        CK(hipMemcpy(order.data(), c->d_blkmap.p, sizeof(int) * nblk, hipMemcpyDeviceToHost),
+           "blkmap");
+      } else {
+        for (int b = 0; b < nblk; b++) order[b] = b;
+      }
+      std::vector<int> bi, bb;
+      for (int b : order) {
+        bool bnd = false;
+        for (int i = 256 * b; i < std::min(L.n_owned, 256 * b + 256) && !bnd; i++) {
+          const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+          for (int sl = 1; sl < len && !bnd; sl++)
+            bnd = L.colidx[size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln] >= L.n_owned;
+        }
+        (bnd ? bb : bi).push_back(b);
+      }
+      if ((rc = up(c->d_blk_int, bi, "interior blocks")) || (rc = up(c->d_blk_bnd, bb, "boundary blocks"))) {
+        g_err = c->err;
+        return rc;
+      }
+      c->n_blk_int = int(bi.size());
+      c->n_blk_bnd = int(bb.size());
+      c->split_spmv = true;
+      if (comm->rccl_unique_id) {
+        if ((e = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming)) != hipSuccess) {
+          g_err = std::string("halo stream: ") + hipGetErrorString(e);
+          return PNP_E_HIP;
+        }
+      }
+    }
   }
   if (c->nranks > 1 && !comm->rccl_unique_id) {  // join the in-process group
     std::shared_ptr<LocalGroup> g;
@@ -1864,6 +1987,11 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     }
     return PNP_OK;
   }
+  if (option == PNP_OPT_BICG_TWORED) {
+    if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_BICG_TWORED takes -1, 0 or 1");
+    c->twored_opt = int(value);
+    return PNP_OK;
+  }
   if (option == PNP_OPT_JAC_FD) {
     if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_JAC_FD takes 0 or 1");
     c->fd_opt = int(value);
@@ -1891,6 +2019,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_JAC_FD) {
     *value = c->fd_opt;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_BICG_TWORED) {
+    *value = c->twored_opt;
     return PNP_OK;
   }
   return c->fail(PNP_E_ARG, "unknown option");

@@ -220,6 +220,9 @@ struct DevLayout {
   // colour, so each XCD takes one spatial slice of the domain in every colour and the neighbour
   // gathers of its rows share its L2 (colour-major rows otherwise spread a region over all XCDs).
   const int *blkmap = nullptr;
+  // > 0: whole-matrix launches (SpMV) cover only the blkcount 256-row blocks listed in blkmap
+  // (the interior / boundary halves of a halo-overlapped SpMV, multi-GPU)
+  int blkcount = 0;
   // triangular split of the owned-column pattern, SELL-64 each (same row order and chunks):
   // L = strictly lower slots (columns of earlier colours), U = slot 0 diagonal + upper slots.
   // Padding slots point at the row itself with zero values.  The sweeps read only the half
@@ -256,11 +259,12 @@ struct AsmArgs {
 struct Scalars {
   double rho, rho_new, alpha, omega, h, norm0, norm, reduction;
   double it_half;        // ISTL half-step counter of the last completed half step
-  double red[4];         // reduction results (after allreduce)
+  double red[6];         // reduction results (after allreduce)
   int done;              // 0 running, 1 converged, 2 breakdown
   int breakdown;         // 1 rho, 2 omega, 3 h
   int iter;              // full iterations started
   int divguard;          // 1: stop with breakdown 4 once ||r|| > 1e10 ||r0|| (AMG solves)
+  int pending;           // two-reduction iteration: the second half step's test is still due
 };
 
 // ---- launchers (return hipError_t of the launch) ----------------------------------------------
@@ -272,10 +276,11 @@ hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi
                              const double *x_old, double *cvec, hipStream_t s);
 
 // y = A x over owned rows; optional fused dots: out partials[block*k + j]
-//   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2); 3: y = w - A x (no dots)
+//   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2); 3: y = w - A x (no dots);
+//   4: <y, w>, <y, y>, <y, w2> (k=3)
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
-                       hipStream_t s);
+                       hipStream_t s, const double *w2 = nullptr);
 
 // preconditioners: v = M^{-1} d (v over owned rows)
 hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
@@ -318,7 +323,8 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int 
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
                               const double *v, double *p, const void *uv, double *yout,
-                              double *partials, int *nparts, hipStream_t s, int f32 = 0);
+                              double *partials, int *nparts, hipStream_t s, int f32 = 0,
+                              const double *rt = nullptr);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);
@@ -341,12 +347,17 @@ hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, 
                          int derive_stage = -1);
 // partial-sum count of launch_spmv over nrows rows (allocation bound)
 int spmv_parts(int nrows);
-// sum partials pa[npa][ka] -> S->red[0..ka) and pb[npb][kb] -> S->red[ka..ka+kb), ka+kb <= 4
+// sum partials pa[npa][ka] -> S->red[0..ka) and pb[npb][kb] -> S->red[ka..ka+kb), ka+kb <= 5
 hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
                           Scalars *S, hipStream_t s, int derive_stage = -1);
 // derive scalars after a reduction; stage: 0 init (red: <r,r>), 1 after h, 2 after first half
 // norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>); 23 = 2 then 3 from one
-// reduction (red: <t,r>, <t,t>, ||s||^2), the first half step's test deferred to the second's
+// reduction (red: <t,r>, <t,t>, ||s||^2), the first half step's test deferred to the second's;
+// two-reduction iteration (multi-GPU: two allreduces per iteration instead of three):
+// 31 = h (red[0]) with the previous iteration's second-half test on red[1] = ||r||^2 (lagged),
+// 32 = the first half's test and omega from <t,s>, <t,t>, <t,rt>, ||s||^2, <rt,s>, then
+// rho_new = <rt,s> - omega <rt,t> and the second half's counters, its test left pending;
+// 33 = the pending test alone (red[0] = ||r||^2), after the last iteration
 hipError_t launch_derive(Scalars *S, int stage, hipStream_t s);
 
 // y = x - lambda*z (Newton line search), copy/scale helpers

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
                                                  const double *__restrict__ x,
                                                  double *__restrict__ y,
                                                  const double *__restrict__ w,
-                                                 double *__restrict__ partials) {
+                                                 double *__restrict__ partials,
+                                                 const double *__restrict__ w2) {
   constexpr int NV = popc9(PAT), NK = nks_of(PAT);
   // LPR lanes per row (slots interleaved): block b covers part b % LPR of the 256-row group the
   // spatial block map gives b / LPR
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
     q = threadIdx.x % LPR;
   }
   const bool live = row < L.n_owned;
-  double d[2] = {0, 0};
+  double d[3] = {0, 0, 0};
   double acc[NF];
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] = 0;
@@ -140,15 +141,21 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
       for (int f = 0; f < NF; f++) acc[f] = wr[f] - acc[f];
     }
     store_nf<NF>(y, size_t(row), acc);
-    if constexpr (MODE == 1 || MODE == 2) {
+    if constexpr (MODE == 1 || MODE == 2 || MODE == 4) {
       double wr[NF];
       load_nf<NF>(w, size_t(row), wr);
 #pragma unroll
       for (int f = 0; f < NF; f++) d[0] += acc[f] * wr[f];
     }
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 || MODE == 4) {
 #pragma unroll
       for (int f = 0; f < NF; f++) d[1] += acc[f] * acc[f];
+    }
+    if constexpr (MODE == 4) {
+      double wr[NF];
+      load_nf<NF>(w2, size_t(row), wr);
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[2] += acc[f] * wr[f];
     }
   }
   if constexpr (MODE == 1) {
@@ -157,6 +164,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
   } else if constexpr (MODE == 2) {
     double v2[2] = {d[0], d[1]};
     block_sum<2>(v2, partials + 2 * blockIdx.x);
+  } else if constexpr (MODE == 4) {
+    double v3[3] = {d[0], d[1], d[2]};
+    block_sum<3>(v3, partials + 3 * blockIdx.x);
   }
 }
 
@@ -810,12 +820,13 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
                                                         double *__restrict__ p,
                                                         const VT *__restrict__ uv,
                                                         double *yout,
-                                                        double *__restrict__ partials) {
+                                                        double *__restrict__ partials,
+                                                        const double *__restrict__ rt) {
   constexpr int NV = popc9(PAT);
   if (S->done) return;  // uniform over the grid
   const int row = blockIdx.x * kBlock + threadIdx.x;
   const bool live = row < L.n_owned;
-  double ss = 0;
+  double ss = 0, rs = 0;
   if (live) {
     double d[NF], vv[NF];
     load_nf<NF>(r, size_t(row), d);
@@ -841,6 +852,12 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
         d[f] -= a * vv[f];
         ss += d[f] * d[f];
       }
+      if (rt) {  // <rt, s> for the two-reduction iteration
+        double ti[NF];
+        load_nf<NF>(rt, size_t(row), ti);
+#pragma unroll
+        for (int f = 0; f < NF; f++) rs += ti[f] * d[f];
+      }
       store_nf<NF>(x, size_t(row), xi);
       store_nf<NF>(r, size_t(row), d);
     }
@@ -853,8 +870,13 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     }
   }
   if (WHICH == 1) {
-    double a1[1] = {ss};
-    block_sum<1>(a1, partials + blockIdx.x);
+    if (rt) {  // uniform over the grid
+      double a2[2] = {ss, rs};
+      block_sum<2>(a2, partials + 2 * blockIdx.x);
+    } else {
+      double a1[1] = {ss};
+      block_sum<1>(a1, partials + blockIdx.x);
+    }
   }
 }
 
@@ -964,6 +986,43 @@ __device__ void derive(Scalars *S, int stage) {
   if (stage == 14) {  // CG: beta = <q, r> / rho (kept in omega), rho = <q, r>
     S->omega = S->red[0] / S->rho;
     S->rho = S->red[0];
+    return;
+  }
+  if (stage == 31 || stage == 33) {  // the lagged second-half test (stage 4's checks)
+    if (S->pending) {
+      S->pending = 0;
+      const double nr = S->red[stage == 31 ? 1 : 0];
+      S->norm = sqrt(nr);
+      if (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) {
+        S->done = 1;
+      } else if (S->divguard && !(S->norm <= 1e10 * S->norm0)) {
+        S->done = 2;
+        S->breakdown = 4;
+      } else if (fabs(S->rho) <= kEps) {
+        S->done = 2;
+        S->breakdown = 1;
+      } else if (fabs(S->omega) <= kEps) {
+        S->done = 2;
+        S->breakdown = 2;
+      }
+      if (S->done) return;
+    }
+    if (stage == 33) return;
+    stage = 1;  // then h as in stage 1
+  }
+  if (stage == 32) {  // red: <t,s>, <t,t>, <t,rt>, ||s||^2, <rt,s>
+    S->norm = sqrt(S->red[3]);
+    S->it_half += 0.5;
+    if (S->norm < S->reduction * S->norm0) {
+      S->done = 1;
+      return;
+    }
+    S->omega = S->red[0] / S->red[1];
+    S->it_half += 0.5;
+    S->iter += 1;
+    S->rho = S->rho_new;
+    S->rho_new = S->red[4] - S->omega * S->red[2];
+    S->pending = 1;
     return;
   }
   if (stage == 1) {  // h = <rt, v>
@@ -1110,13 +1169,14 @@ static bool spmv_nt() {
 
 template <int NF, int PAT, int MODE>
 static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double *vals,
-                        const double *x, double *y, const double *w, double *partials) {
+                        const double *x, double *y, const double *w, double *partials,
+                        const double *w2) {
 #define PNP_SPMV_GO(SBc, LPRc)                                                                 \
   hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc>), dim3(g.x * LPRc), dim3(kBlock), 0, s, \
-                     L, vals, x, y, w, partials)
+                     L, vals, x, y, w, partials, w2)
 #define PNP_SPMV_GO2(SBc, LPRc, NTc)                                                        \
   hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc, NTc>), dim3(g.x * LPRc), dim3(kBlock), \
-                     0, s, L, vals, x, y, w, partials)
+                     0, s, L, vals, x, y, w, partials, w2)
   const int b = spmv_batch(), l = spmv_lpr();
   if (spmv_nt() && l == 2 && b == 2) {
     PNP_SPMV_GO2(2, 2, 1);
@@ -1141,19 +1201,25 @@ int spmv_parts(int nrows) { return int(rows_grid(nrows).x) * spmv_lpr(); }
 
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
-                       hipStream_t s) {
-  dim3 g = rows_grid(L.n_owned);
+                       hipStream_t s, const double *w2) {
+  if (L.blkcount < 0) {  // an empty block subset (e.g. a rank without interior blocks)
+    if (nparts) *nparts = 0;
+    return hipSuccess;
+  }
+  dim3 g = L.blkcount > 0 ? dim3(L.blkcount) : rows_grid(L.n_owned);
   if (nparts) *nparts = int(g.x) * spmv_lpr();
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
-      (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials);
+      (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials, w2);
     else if (mode == 1)
-      (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials);
+      (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials, w2);
     else if (mode == 2)
-      (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials);
+      (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials, w2);
+    else if (mode == 4)
+      (spmv_launch<NFc, PATc, 4>)(g, s, L, vals, x, y, w, partials, w2);
     else
-      (spmv_launch<NFc, PATc, 3>)(g, s, L, vals, x, y, w, partials);
+      (spmv_launch<NFc, PATc, 3>)(g, s, L, vals, x, y, w, partials, w2);
   });
   return hipGetLastError();
 }
@@ -1313,7 +1379,8 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
                               const double *v, double *p, const void *uvp, double *yout,
-                              double *partials, int *nparts, hipStream_t s, int f32) {
+                              double *partials, int *nparts, hipStream_t s, int f32,
+                              const double *rt) {
   const dim3 g = rows_grid(L.n_owned);
   if (nparts) *nparts = int(g.x);
   if (L.n_owned == 0) return hipSuccess;
@@ -1323,10 +1390,10 @@ hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, c
     PNP_PAT_DISPATCH(nf, pat, {
       if (which == 0)
         hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
-                           first, x, yin, r, v, p, uv, yout, partials);
+                           first, x, yin, r, v, p, uv, yout, partials, nullptr);
       else
         hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
-                           first, x, yin, r, v, p, uv, yout, partials);
+                           first, x, yin, r, v, p, uv, yout, partials, rt);
     });
     return hipGetLastError();
   };
@@ -1418,6 +1485,8 @@ hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, i
     hipLaunchKernelGGL((k_reduce<1, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
   else if (ka == 2 && kb == 2)
     hipLaunchKernelGGL((k_reduce<2, 2>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
+  else if (ka == 3 && kb == 2)
+    hipLaunchKernelGGL((k_reduce<3, 2>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

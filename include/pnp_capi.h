@@ -307,7 +307,14 @@ enum {
   PNP_OPT_ILU_FUSED_FACTOR = 2,
   /* 1: every Jacobian assembly of the context (pnp_jacobian, Newton, pnp_assemble_state) is the
    * reference's forward-difference Jacobian (as PNP_JAC_FD); 0 (default): analytic */
-  PNP_OPT_JAC_FD = 3
+  PNP_OPT_JAC_FD = 3,
+  /* BiCGSTAB with two global reductions per iteration instead of three: rho_new = <rt,s> -
+   * omega <rt,t> comes from omega's reduction, and the second half step's convergence test is
+   * folded into the next iteration's <rt,v> reduction (a converged solve runs the first kernels
+   * of one more iteration, whose updates are skipped).  ISTL half-step counting is unchanged.
+   * -1 (default): on when the context has more than one rank (each reduction is an allreduce
+   * round trip over xGMI); 0 off; 1 on. */
+  PNP_OPT_BICG_TWORED = 4
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);

@@ -238,3 +238,84 @@ def test_amg_solve_partitioned(nranks, kind):
         assert info["levels"] >= 2
     assert len({o[1]["iterations"] for o in outs}) == 1
     assert sum(o[4]["rows"][0] for o in outs) == mesh.nv
+
+
+def _config5_mesh(k=1):
+    """BASELINE configs[4]'s geometry: test/pore_without_dna/pore_without_dna.geo meshed natively
+    (scale 0.85, as bench.py's strong-scaling leg), refined k times."""
+    cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
+    return cfg, P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(k)
+
+
+def test_config5_geometry_8_ranks_residual_jacobian():
+    """8 in-process ranks (the north star's GPU count) on the config-5 geometry: residual and
+    Jacobian (analytic and FD) = one rank's."""
+    cfg, mesh = _config5_mesh(1)
+    par = P.Params.from_config(cfg)
+    rng = np.random.default_rng(8)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PNP)
+        return ctx.residual(x), ctx.jacobian(x), ctx.jacobian(x, fd=True), ctx.info()
+    outs = run_ranks(8, mesh, par, fn)
+    assert sum(o[3]["nv_owned"] for o in outs) == nv
+    ctx1 = P.Context(mesh, par)
+    ctx1.set_operator(P.OP_PNP)
+    r1, J1, F1 = ctx1.residual(x), ctx1.jacobian(x), ctx1.jacobian(x, fd=True)
+    assert np.max(np.abs(sum(o[0] for o in outs) - r1)) <= 1e-13 * np.max(np.abs(r1))
+    assert abs(sum(o[1] for o in outs) - J1).max() <= 1e-13 * abs(J1).max()
+    assert abs(sum(o[2] for o in outs) - F1).max() <= 1e-13 * abs(F1).max()
+
+
+def test_config5_geometry_8_ranks_driver_sequence():
+    """PB Newton -> BCExtension -> PNP Newton (the config's reductions, block-Jacobi ILU(0)) on 8
+    in-process ranks vs one rank, config-5 geometry refined once."""
+    cfg, mesh = _config5_mesh(1)
+    par = P.Params.from_config(cfg)
+    s = cfg.system
+
+    def seq(ctx, r):
+        ctx.set_operator(P.OP_PB)
+        phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0, reduction=1e-10)
+        phi = ctx.sync_vector(phi, 1)
+        x0 = ctx.initial_state(phi)
+        ctx.set_operator(P.OP_PNP)
+        u, res = ctx.newton(x0, prec=P.PREC_ILU0, reduction=1e-10,
+                            min_linear_reduction=s["newtonMinLinearReduction"])
+        return ctx.sync_vector(u), res, rpb
+    outs = run_ranks(8, mesh, par, seq)
+    u1, res1, rpb1 = seq(P.Context(mesh, par), 0)
+    assert res1["converged"] == 1 and rpb1["converged"] == 1
+    for u, res, rpb in outs:
+        assert rpb["converged"] == 1 and res["converged"] == 1, (rpb, res)
+        assert np.max(np.abs(u - u1)) <= 1e-6 * np.max(np.abs(u1))
+
+
+def test_implicit_euler_8_ranks():
+    """Config 4's operator (PnpOperator + PnpTOperator, implicit Euler, dt = tau) for 3 steps on 8
+    in-process ranks vs one rank, config-5 geometry refined once."""
+    cfg, mesh = _config5_mesh(1)
+    par = P.Params.from_config(cfg)
+    dt = cfg.system["tau"]
+
+    def steps(ctx, r):
+        ctx.set_operator(P.OP_PB)
+        phi, _ = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0, reduction=1e-10)
+        x = ctx.initial_state(ctx.sync_vector(phi, 1))
+        out = []
+        for n in range(3):
+            ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=dt, x_old=x)
+            # abs_limit above the residual's rounding floor (~1e-12 on this mesh)
+            u, res = ctx.newton(x, prec=P.PREC_ILU0, reduction=1e-8, abs_limit=1e-10)
+            assert res["converged"] == 1, res
+            x = ctx.sync_vector(u)
+            out.append(x)
+        return out
+    outs = run_ranks(8, mesh, par, steps)
+    ref = steps(P.Context(mesh, par), 0)
+    for traj in outs:
+        for a, b in zip(traj, ref):
+            assert np.max(np.abs(a - b)) <= 1e-6 * np.max(np.abs(b))
