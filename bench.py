@@ -485,7 +485,7 @@ def main():
             "bicgstab_ms_per_iter": 1e3 * M["t_bicg"] / (args.steps * args.bicg_iters),
             "roofline": {"bound": "hbm", "achieved": aw["achieved"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": aw["frac"],
-                         "traffic": pmc_traffic("k_assemble_ga<0, 1, 3, 9, 6>"),
+                         "traffic": pmc_traffic("k_assemble_ga<0, 1, 3, 9, 6"),
                          "traffic_source": "profiles/r02/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
                                            "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",

@@ -132,6 +132,7 @@ struct pnp_ctx {
     return ev ? (std::atoi(ev) != 0 ? 1 : 0) : -1;
   }();
   DBuf<int> d_blkmap;
+  DBuf<int> d_rowoff, d_rowcol;  // row-contiguous block offsets / columns (fused ILU(0) factor)
   // halo-overlapped SpMV (multi-GPU): 256-row blocks without / with ghost columns, each in the
   // spatial order of blkmap; the halo runs on cstream while the interior blocks compute
   DBuf<int> d_blk_int, d_blk_bnd;
@@ -631,8 +632,8 @@ struct pnp_ctx {
     hipEvent_t t0 = tb(T_FACT);
     hipError_t e;
     if (ilu_fused) {
-      e = pnp::launch_ilu0_factor_fused(dl, L.color_ptr.data(), nf, pat, vals.p, lu.p, lvals.p,
-                                        uvals.p, ilu_f32, stream);
+      e = pnp::launch_ilu0_factor_fused(dl, L.color_ptr.data(), nf, pat, vals.p, d_rowoff.p,
+                                        d_rowcol.p, lu.p, lvals.p, uvals.p, ilu_f32, stream);
     } else {
       e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
       if (e == hipSuccess)
@@ -648,6 +649,10 @@ struct pnp_ctx {
   // bring the split storage up to date with the matrix (which = 1) or the factors (which = 2)
   int split(int which) {
     if (split_of == which) return PNP_OK;
+    if (which == 2 && ilu_fused) {  // the fused factorisation keeps no SELL copy: redo it
+      lu_valid = false;
+      return ilu_factor();
+    }
     hipEvent_t t0 = tb(T_FACT);
     hipError_t e = pnp::launch_split(dl, nf, pat, which == 1 ? 1 : 0, which == 2 ? lu.p : vals.p,
                                      d_lsrc.p, (long long)d_lsrc.n, d_usrc.p, (long long)d_usrc.n,
@@ -1401,6 +1406,20 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       (rc = up(c->d_ucolidx, ucol, "ucolidx")) || (rc = up(c->d_usrc, usrc, "usrc"))) {
     g_err = c->err;
     return rc;
+  }
+  {  // row-contiguous block offsets and columns of the owned rows (fused ILU(0) factorisation)
+    std::vector<int> ro(L.n_owned + 1, 0), rcol;
+    rcol.reserve(size_t(L.nblocks));
+    for (int i = 0; i < L.n_owned; i++) {
+      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      for (int sl = 0; sl < len; sl++)
+        rcol.push_back(L.colidx[size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln]);
+      ro[i + 1] = ro[i] + len;
+    }
+    if ((rc = up(c->d_rowoff, ro, "rowoff")) || (rc = up(c->d_rowcol, rcol, "rowcol"))) {
+      g_err = c->err;
+      return rc;
+    }
   }
   {  // spatial block order (DevLayout::blkmap) for the whole-matrix kernels (assembly, SpMV):
      // each XCD takes one spatial slice of every colour, so the neighbour gathers of its rows

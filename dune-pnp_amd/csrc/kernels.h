@@ -306,11 +306,12 @@ hipError_t launch_expand(const DevLayout &L, int nf, int pat, const double *vals
 hipError_t launch_ilu0_factor(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                               double *lu, hipStream_t s);
 // the same factors from the k-form matrix in one launch per colour, expand and split folded in:
-// lu = scratch (NV values per block, the factors on exit), lv / uv = the split storage (float when
-// f32); bitwise the factors of launch_expand + launch_ilu0_factor + launch_split
+// aos = row-contiguous scratch (row i's blocks at (rowoff[i] + slot) * NV, columns rowcol[rowoff[i]
+// + slot]), lv / uv = the split storage (float when f32); bitwise the factors of launch_expand +
+// launch_ilu0_factor + launch_split
 hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
-                                    const double *kvals, double *lu, void *lv, void *uv, int f32,
-                                    hipStream_t s);
+                                    const double *kvals, const int *rowoff, const int *rowcol,
+                                    double *aos, void *lv, void *uv, int f32, hipStream_t s);
 // c_first = 1: colour 0's forward step was already applied (launch_update_fwd0); add != null:
 // also out = add + v (written row by row as the backward sweep finishes them)
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,

@@ -455,8 +455,12 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
 }
 
 // The same factorisation with the neighbour-row work hoisted and the expand / split passes folded
-// in (one launch per colour, no k_expand / k_split passes):
-//   0) the row expands its own k-form blocks (masked) into lu;
+// in (one launch per colour, no k_expand / k_split passes), on a row-contiguous scratch copy:
+// row i's blocks are aos[(rowoff[i] + t) * NV + q] and its columns rowcol[rowoff[i] + t]
+// (t = fan slot), so reading a neighbour row's blocks and columns touches ~4 cache lines instead
+// of one line per (slot, value pair) of the SELL layout (the gathers of a factorisation are per
+// thread, not per wave, and were 8x over-fetched: profiles/r02/pmc_summary.json).
+//   0) the row expands its own k-form blocks (masked) into aos;
 //   1) per lower neighbour j (ascending): the L block L_ij = A_ij U_jj^-1 is finished in registers
 //      from row j's diagonal block (loaded once), then every block A_im with m > j in both rows is
 //      updated from row j's block U_jm, each loaded once per j (the column match of the two rows
@@ -465,28 +469,45 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
 //   3) the row's blocks are written to the split L / U storage (VT: double or float).
 // Per block entry the subtraction order (j ascending, then g ascending) is that of
 // k_ilu0_factor, so the factors are bitwise the same.
-template <int NF, int PAT, typename VT>
-__global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r0, int r1,
-                                                              const double *__restrict__ kvals,
-                                                              double *__restrict__ lu,
-                                                              VT *__restrict__ lv,
-                                                              VT *__restrict__ uv) {
+// KMAX > 0: the row's own blocks live in LDS during the elimination (KMAX >= the fan length +
+// 1 of every row) and reach the scratch once, when they are final: the per-row working set of a
+// wave does not fit the L2 otherwise, and every update of an own block was a write-back.
+template <int NF, int PAT, typename VT, int KMAX, int TB>
+__global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, int r1,
+                                                          const double *__restrict__ kvals,
+                                                          const int *__restrict__ rowoff,
+                                                          const int *__restrict__ rowcol,
+                                                          double *__restrict__ aos,
+                                                          VT *__restrict__ lv,
+                                                          VT *__restrict__ uv) {
   constexpr int NV = popc9(PAT), NK = nks_of(PAT), NS = slot_vals<NV, VT>();
-  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
+  __shared__ double own[KMAX > 0 ? KMAX * NV : 1][KMAX > 0 ? TB : 1];
+  const int row = r0 + xcd_block(blockIdx.x, gridDim.x, 1) * TB + threadIdx.x;
   if (row >= r1) return;
   const int ci = row / kRows, li = row % kRows;
   const int offi = L.chunk_off[ci], leni = int(L.rowmeta[row] & 63);
-  const int *__restrict__ cixi = L.colidx + offi + li;
-  double *__restrict__ vi = lu + size_t(offi) * NV;  // chunk base, see vin()
-  auto ld = [&](const double *base, int t, int lane, double (&B)[NV]) {
+  const int *__restrict__ cixi = rowcol + rowoff[row];
+  double *__restrict__ vi = aos + size_t(rowoff[row]) * NV;
+  const int tl = threadIdx.x;
+  auto ld = [&](const double *base, int t, double (&B)[NV]) {
+    if (KMAX > 0 && base == vi) {
 #pragma unroll
-    for (int q = 0; q < NV; q++) B[q] = base[size_t(t) * NV * kRows + vin(NV, q, lane)];
-  };
-  auto st = [&](double *base, int t, int lane, const double (&B)[NV]) {
+      for (int q = 0; q < NV; q++) B[q] = own[t * NV + q][tl];
+      return;
+    }
 #pragma unroll
-    for (int q = 0; q < NV; q++) base[size_t(t) * NV * kRows + vin(NV, q, lane)] = B[q];
+    for (int q = 0; q < NV; q++) B[q] = base[size_t(t) * NV + q];
   };
-  // 0) expand + mask the row's blocks into lu
+  auto st = [&](double *base, int t, const double (&B)[NV]) {
+    if (KMAX > 0 && base == vi) {
+#pragma unroll
+      for (int q = 0; q < NV; q++) own[t * NV + q][tl] = B[q];
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < NV; q++) base[size_t(t) * NV + q] = B[q];
+  };
+  // 0) expand + mask the row's blocks into its scratch rows
   {
     const unsigned dm = row_mask<NF>(L, row);
     const double *kb = kvals + size_t(offi) * NK;
@@ -496,7 +517,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
       for (int q = 0; q < NK; q++) K[q] = kb[size_t(t) * NK * kRows + vin(NK, q, li)];
       expand_k<PAT>(K, B);
       mask_rows<NF, PAT>(B, dm, t == 0);
-      st(vi, t, li, B);
+      st(vi, t, B);
     }
   }
   // 1) lower neighbours in increasing index order
@@ -504,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
   for (;;) {
     int j = 0x7fffffff, s = -1;
     for (int t = 1; t < leni; t++) {
-      const int c = cixi[t * kRows];
+      const int c = cixi[t];
       if (c < row && c > prev && c < j) {
         j = c;
         s = t;
@@ -512,13 +533,12 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
     }
     if (s < 0) break;
     prev = j;
-    const int cj = j / kRows, lj = j % kRows;
-    const int offj = L.chunk_off[cj], lenj = int(L.rowmeta[j] & 63);
-    const int *__restrict__ cixj = L.colidx + offj + lj;
-    const double *__restrict__ vj = lu + size_t(offj) * NV;
+    const int lenj = int(L.rowmeta[j] & 63);
+    const int *__restrict__ cixj = rowcol + rowoff[j];
+    const double *__restrict__ vj = aos + size_t(rowoff[j]) * NV;
     double Ujj[NV], Lb[NV];
-    ld(vj, 0, lj, Ujj);
-    ld(vi, s, li, Lb);
+    ld(vj, 0, Ujj);
+    ld(vi, s, Lb);
 #pragma unroll
     for (int g = 0; g < NF; g++) {
       const double dinv = Ujj[pat_index(PAT, g, g)];  // stored inverted
@@ -534,16 +554,16 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
             Lb[pat_index(PAT, f, h)] -= l * Ujj[pat_index(PAT, g, h)];
       }
     }
-    st(vi, s, li, Lb);
+    st(vi, s, Lb);
     for (int t = 0; t < leni; t++) {
-      const int m = cixi[t * kRows];
-      if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;  // padding -> m == row
+      const int m = cixi[t];
+      if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;
       int u = 1;
-      while (u < lenj && cixj[u * kRows] != m) u++;
+      while (u < lenj && cixj[u] != m) u++;
       if (u == lenj) continue;
       double U[NV], A[NV];
-      ld(vj, u, lj, U);
-      ld(vi, t, li, A);
+      ld(vj, u, U);
+      ld(vi, t, A);
 #pragma unroll
       for (int g = 0; g < NF; g++)
 #pragma unroll
@@ -556,12 +576,12 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
             if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
               A[pat_index(PAT, f, h)] -= l * U[pat_index(PAT, g, h)];
         }
-      st(vi, t, li, A);
+      st(vi, t, A);
     }
   }
   // 2) inside the vertex: rows (i,f) eliminated by (i,g<f); invert the pivots
   double D[NV];
-  ld(vi, 0, li, D);
+  ld(vi, 0, D);
   for (int f = 0; f < NF; f++) {
     for (int g = 0; g < f; g++) {
       if (pat_index(PAT, f, g) < 0) continue;
@@ -571,19 +591,24 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
         if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
           D[pat_index(PAT, f, h)] -= l * D[pat_index(PAT, g, h)];
       for (int t = 1; t < leni; t++) {
-        const int m = cixi[t * kRows];
+        const int m = cixi[t];
         if (m <= row || m >= L.n_owned) continue;
         double A[NV];
-        ld(vi, t, li, A);
+        ld(vi, t, A);
         for (int h = 0; h < NF; h++)
           if (pat_index(PAT, f, h) >= 0 && pat_index(PAT, g, h) >= 0)
             A[pat_index(PAT, f, h)] -= l * A[pat_index(PAT, g, h)];
-        st(vi, t, li, A);
+        st(vi, t, A);
       }
     }
     D[pat_index(PAT, f, f)] = 1.0 / D[pat_index(PAT, f, f)];
   }
-  st(vi, 0, li, D);
+  st(vi, 0, D);
+  if constexpr (KMAX > 0) {  // the finished row, for the rows of later colours
+    for (int t = 0; t < leni; t++)
+#pragma unroll
+      for (int q = 0; q < NV; q++) vi[size_t(t) * NV + q] = own[t * NV + q][tl];
+  }
   // 3) the split storage: slot 0 and the owned upper columns (slot order) to U, the lower
   // columns (slot order) to L, ghost columns dropped -- the order ctx.cc builds lsrc / usrc in
   auto put = [&](VT *base, int off, int k, const double (&B)[NV]) {
@@ -600,10 +625,10 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor_fused(DevLayout L, int r
   put(uv, uoff, 0, D);
   int kl = 0, ku = 1;
   for (int t = 1; t < leni; t++) {
-    const int c = cixi[t * kRows];
+    const int c = cixi[t];
     if (c >= L.n_owned || c == row) continue;
     double B[NV];
-    ld(vi, t, li, B);
+    ld(vi, t, B);
     if (c < row)
       put(lv, loff, kl++, B);
     else
@@ -1325,19 +1350,31 @@ hipError_t launch_ilu0_factor(const DevLayout &L, const int *cp, int nf, int pat
 }
 
 hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *cp, int nf, int pat,
-                                    const double *kvals, double *lu, void *lv, void *uv, int f32,
-                                    hipStream_t s) {
+                                    const double *kvals, const int *rowoff, const int *rowcol,
+                                    double *aos, void *lv, void *uv, int f32, hipStream_t s) {
   if (L.n_owned == 0) return hipSuccess;
+  // own rows in LDS (64 rows per workgroup) when every fan fits KMAX slots, else in the scratch
+  const int ms = L.max_slots;
   auto run = [&](auto vt) -> hipError_t {
     using VT = decltype(vt);
     PNP_PAT_DISPATCH(nf, pat, {
-      for (int c = 0; c < L.ncolors; c++) {
-        int n = cp[c + 1] - cp[c];
-        if (n > 0)
-          hipLaunchKernelGGL((k_ilu0_factor_fused<NFc, PATc, VT>), rows_grid(n), dim3(kBlock), 0, s,
-                             L, cp[c], cp[c + 1], kvals, lu, static_cast<VT *>(lv),
-                             static_cast<VT *>(uv));
-      }
+      auto go = [&](auto kmax) {
+        constexpr int K = decltype(kmax)::value;
+        constexpr int TB = K > 0 ? 64 : kBlock;
+        for (int c = 0; c < L.ncolors; c++) {
+          int n = cp[c + 1] - cp[c];
+          if (n > 0)
+            hipLaunchKernelGGL((k_ilu0_factor_fused<NFc, PATc, VT, K, TB>), dim3((n + TB - 1) / TB),
+                               dim3(TB), 0, s, L, cp[c], cp[c + 1], kvals, rowoff, rowcol, aos,
+                               static_cast<VT *>(lv), static_cast<VT *>(uv));
+        }
+      };
+      if (ms <= 10)
+        go(std::integral_constant<int, 10>());
+      else if (ms <= 16)
+        go(std::integral_constant<int, 16>());
+      else
+        go(std::integral_constant<int, 0>());
     });
     return hipGetLastError();
   };
