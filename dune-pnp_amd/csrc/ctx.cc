@@ -127,6 +127,7 @@ struct pnp_ctx {
   }();
   int f32_now() const { return split_of == 2 ? ilu_f32 : 0; }
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
+  int amg_fallback = 0;  // PNP_OPT_AMG_FALLBACK
   int twored_opt = [] {  // PNP_OPT_BICG_TWORED: -1 auto (on with more than one rank), 0, 1
     const char *ev = std::getenv("PNP_BICG_TWORED");
     return ev ? (std::atoi(ev) != 0 ? 1 : 0) : -1;
@@ -2006,6 +2007,11 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     }
     return PNP_OK;
   }
+  if (option == PNP_OPT_AMG_FALLBACK) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_AMG_FALLBACK takes 0 or 1");
+    c->amg_fallback = int(value);
+    return PNP_OK;
+  }
   if (option == PNP_OPT_BICG_TWORED) {
     if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_BICG_TWORED takes -1, 0 or 1");
     c->twored_opt = int(value);
@@ -2042,6 +2048,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_BICG_TWORED) {
     *value = c->twored_opt;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_AMG_FALLBACK) {
+    *value = c->amg_fallback;
     return PNP_OK;
   }
   return c->fail(PNP_E_ARG, "unknown option");
@@ -2181,7 +2191,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
     double ts = now_s();
     if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
     res->linear_iterations += sr.iterations;
-    if (lo.prec == PNP_PREC_AMG && (sr.breakdown || !sr.converged)) {
+    if (lo.prec == PNP_PREC_AMG && c->amg_fallback && (sr.breakdown || !sr.converged)) {
       // AMG fallback: the V-cycle of a non-symmetric system can fail where its level-0
       // smoother alone converges (a far-from-converged state); redo this step's solve with the
       // smoother as the preconditioner

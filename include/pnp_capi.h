@@ -314,7 +314,13 @@ enum {
    * of one more iteration, whose updates are skipped).  ISTL half-step counting is unchanged.
    * -1 (default): on when the context has more than one rank (each reduction is an allreduce
    * round trip over xGMI); 0 off; 1 on. */
-  PNP_OPT_BICG_TWORED = 4
+  PNP_OPT_BICG_TWORED = 4,
+  /* 1: pnp_newton re-solves a step whose AMG-preconditioned BiCGSTAB failed with the AMG's
+   * level-0 smoother alone (pnp_newton_result.linear_fallbacks).  0 (default).  The round-1
+   * divergence this guarded against came from a too-small coarsest level (<= 64 blocks): with
+   * the default (<= 1024 blocks, exact dense solve) config 4 runs 100 steps without a failed
+   * AMG solve (profiles/r02/amg_c4_*.log). */
+  PNP_OPT_AMG_FALLBACK = 5
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
@@ -337,9 +343,10 @@ typedef struct {
       PNP_E_NOT_CONVERGED (NewtonNotConverged / NewtonLinearSolverError / line search),
       PNP_E_BREAKDOWN */
   double first_defect, defect, elapsed, assemble_seconds, solve_seconds;
-  int32_t linear_fallbacks; /* PNP_PREC_AMG only: Newton steps whose AMG-preconditioned solve
-      failed (diverged: ||r|| > 1e10 ||r0||, breakdown or maxit) and were re-solved with the
-      AMG's level-0 smoother alone; linear_iterations counts both solves */
+  int32_t linear_fallbacks; /* PNP_PREC_AMG with PNP_OPT_AMG_FALLBACK = 1 only: Newton steps
+      whose AMG-preconditioned solve failed (diverged: ||r|| > 1e10 ||r0||, breakdown or maxit)
+      and were re-solved with the AMG's level-0 smoother alone; linear_iterations counts both
+      solves.  Off by default: a failed AMG solve ends Newton like any linear-solver failure. */
 } pnp_newton_result;
 int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
 

@@ -199,3 +199,26 @@ def test_cpp_driver_amg_matches_ilu0(tmp_path):
         outs[prec] = np.loadtxt(tmp_path / f"{prec}_pnp.dat")
     scale = np.max(np.abs(outs["ilu0"]))
     assert np.max(np.abs(outs["amg"] - outs["ilu0"])) <= 1e-6 * scale
+
+
+def test_config4_steps_with_amg_need_no_fallback():
+    """Config 4's systems (implicit Euler, dt = tau, pore_pnp refined twice) with BiCGSTAB +
+    AMG(ILU0) at the default options: 10 steps, every AMG-preconditioned solve converges (the
+    smoother fallback, PNP_OPT_AMG_FALLBACK, is off).  Round 1's divergence came from a coarsest
+    level of <= 64 blocks: the 215- and 1,928-block levels then only get damped block-Jacobi
+    sweeps (spectral radius 1 - 1.7e-7 on their smooth modes) and the preconditioned operator's
+    smallest eigenvalue drops from 0.0145 to 0.0057 (tools/amg_c4_analyse.py,
+    profiles/r02/amg_c4_analyse.log)."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(2)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    assert ctx.get_option(P.OPT_AMG_FALLBACK) == 0
+    ctx.set_operator(P.OP_PB)
+    phi, _ = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=P.PREC_SSOR)
+    u = ctx.initial_state(phi)
+    for i in range(10):
+        ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=cfg.system["tau"], x_old=u)
+        ctx.amg_configure(smoother=P.PREC_ILU0)
+        u, res = ctx.newton(u, reduction=1e-8, abs_limit=1e-9, prec=P.PREC_AMG)
+        assert res["converged"] == 1 and res["status"] == 0, (i, res)
+        assert res["linear_fallbacks"] == 0
