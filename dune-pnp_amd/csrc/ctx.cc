@@ -22,6 +22,7 @@
 #include "amg.h"
 #include "kernels.h"
 #include "mesh.h"
+#include "pk.h"
 
 namespace {
 
@@ -94,7 +95,15 @@ struct pnp_ctx {
   ncclComm_t comm = nullptr;
   std::shared_ptr<LocalGroup> lg;  // test transport instead of RCCL
 
-  pnp::Mesh mesh;
+  // P_k, k > 1 (pnp_create_pk): `mesh` is the node mesh (nv = Lagrange nodes, no elements) the
+  // partition, layout and external vectors are built on; tmesh the triangle mesh, pks the space
+  int degree = 1;
+  pnp::Mesh mesh, tmesh;
+  pnp::PkSpace pks;
+  pnp::PkDev pkd;
+  DBuf<int> pk_enode, pk_vdata, pk_cdata;
+  DBuf<long long> pk_vptr, pk_rptr;
+  DBuf<double> pk_rel, pk_jel;
   pnp::Params params;
   pnp::Fans fans;
   pnp::LocalLayout L;
@@ -508,8 +517,12 @@ struct pnp_ctx {
     aa.jac = fd_mode ? 0 : jac;
     aa.r = r.p;
     hipEvent_t t0 = tb(T_ASM);
-    hipError_t e = pnp::launch_assemble(dl, aa, stream);
-    if (e == hipSuccess && jac && fd_mode)
+    hipError_t e;
+    if (degree > 1)
+      e = pnp::launch_pk_assemble(dl, aa, pkd, jac ? (fd_mode ? 2 : 1) : 0, stream);
+    else
+      e = pnp::launch_assemble(dl, aa, stream);
+    if (e == hipSuccess && jac && fd_mode && degree == 1)
       e = pnp::launch_fd_jacobian(dl, aa, nf, pat, fd_ne, fd_etri.p, fd_rptr.p, fd_cdata.p,
                                   fd_jel.p, stream);
     if (e != hipSuccess) return hipfail(e, "assemble");
@@ -527,7 +540,8 @@ struct pnp_ctx {
   int set_fd(bool on) {
     if (on == fd_mode) return PNP_OK;
     int rc;
-    if (on && !fd_built && (rc = fd_build())) return rc;
+    // P_k: the element kernel differentiates by itself; scalar blocks need no FD value layout
+    if (on && !fd_built && degree == 1 && (rc = fd_build())) return rc;
     const int base = kind == PNP_OP_PNP ? pnp::kPatPnp
                                         : (kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::kPatPnpIE
                                                                             : pnp::kPatScalar);
@@ -538,7 +552,7 @@ struct pnp_ctx {
     lu_valid = false;
     split_of = 0;
     amg_valid = false;
-    if (on) {
+    if (on && degree == 1) {
       const size_t need = size_t(fd_ne) * 9 * nf * nf;
       if (fd_jel.n < need) {
         hipError_t e = fd_jel.alloc(need);
@@ -548,6 +562,123 @@ struct pnp_ctx {
     // padding slots must read as zeros in the new value layout (the SpMV multiplies them)
     hipError_t e = hipMemsetAsync(vals.p, 0, sizeof(double) * size_t(L.nslots) * nks, stream);
     return e == hipSuccess ? PNP_OK : hipfail(e, "clear matrix");
+  }
+
+  // P_k element lists (once per context): the local elements (every element with an owned node,
+  // ascending global id), their local nodes (SoA), and per owned row the residual codes and, per
+  // SELL slot, the element-matrix codes summed into that block, in ascending element order
+  int pk_build() {
+    const pnp::Mesh &m = tmesh;
+    const int nl = pks.nl;
+    std::vector<int> en;
+    std::vector<int> elist;
+    for (int e = 0; e < m.nt; e++) {
+      const int *g = &pks.enode[size_t(e) * nl];
+      bool mine = false, local = true;
+      for (int a = 0; a < nl; a++) {
+        const int l = L.g2l[g[a]];
+        mine = mine || (l >= 0 && l < L.n_owned);
+        local = local && l >= 0;
+      }
+      if (!mine) continue;
+      if (!local) return fail(PNP_E_MESH, "P_k: element not local");
+      elist.push_back(e);
+    }
+    const int ne = int(elist.size());
+    if ((long long)ne * nl * nl >= (1LL << 31)) return fail(PNP_E_MESH, "P_k: too many local elements");
+    en.resize(size_t(ne) * nl);
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < nl; a++) en[size_t(a) * ne + e] = L.g2l[pks.enode[size_t(elist[e]) * nl + a]];
+    auto pos_of = [&](int row, int col) -> long long {
+      const int ch = row / pnp::kRows, ln = row % pnp::kRows, len = pnp::meta_len(L.rowmeta[row]);
+      if (col == row) return L.chunk_off[ch] + ln;
+      for (int sl = 1; sl < len; sl++) {
+        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
+        if (L.colidx[p] == col) return p;
+      }
+      return -1;
+    };
+    std::vector<long long> vptr(L.n_owned + 1, 0);
+    std::vector<int> cnt(size_t(L.nslots) + 1, 0);
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < nl; a++) {
+        const int ra = en[size_t(a) * ne + e];
+        if (ra >= L.n_owned) continue;
+        vptr[ra + 1]++;
+        for (int b = 0; b < nl; b++) {
+          const long long p = pos_of(ra, en[size_t(b) * ne + e]);
+          if (p < 0) return fail(PNP_E_MESH, "P_k: element pair outside the pattern");
+          cnt[p]++;
+        }
+      }
+    for (int i = 0; i < L.n_owned; i++) vptr[i + 1] += vptr[i];
+    std::vector<int> vdata((size_t)vptr[L.n_owned]);
+    std::vector<long long> rptr(L.n_owned + 1, 0);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      long long n = 0;
+      for (int sl = 0; sl < len; sl++) n += 1 + cnt[L.chunk_off[ch] + 64LL * sl + ln];
+      rptr[i + 1] = rptr[i] + n;
+    }
+    std::vector<long long> at((size_t)L.nslots, -1LL), vat(vptr.begin(), vptr.end() - 1);
+    std::vector<int> data((size_t)rptr[L.n_owned]);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      long long q = rptr[i];
+      for (int sl = 0; sl < len; sl++) {
+        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
+        data[q] = cnt[p];
+        at[p] = q + 1;
+        q += 1 + cnt[p];
+      }
+    }
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < nl; a++) {
+        const int ra = en[size_t(a) * ne + e];
+        if (ra >= L.n_owned) continue;
+        vdata[vat[ra]++] = a * ne + e;
+        for (int b = 0; b < nl; b++)
+          data[at[pos_of(ra, en[size_t(b) * ne + e])]++] = (a * nl + b) * ne + e;
+      }
+    int rc;
+    if ((rc = upv(pk_enode, en, "P_k elements")) || (rc = upv(pk_vptr, vptr, "P_k vptr")) ||
+        (rc = upv(pk_vdata, vdata, "P_k residual codes")) || (rc = upv(pk_rptr, rptr, "P_k rptr")) ||
+        (rc = upv(pk_cdata, data, "P_k matrix codes")))
+      return rc;
+    hipError_t e = pk_rel.alloc(std::max<size_t>(1, size_t(ne) * nl));
+    if (e == hipSuccess) e = pk_jel.alloc(std::max<size_t>(1, size_t(ne) * nl * nl));
+    if (e == hipSuccess) e = pnp::pk_upload_tables(pks.k, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "P_k scratch");
+    pkd.k = pks.k;
+    pkd.nl = nl;
+    pkd.ne = ne;
+    pkd.enode = pk_enode.p;
+    pkd.vptr = pk_vptr.p;
+    pkd.vdata = pk_vdata.p;
+    pkd.rptr = pk_rptr.p;
+    pkd.cdata = pk_cdata.p;
+    pkd.rel = pk_rel.p;
+    pkd.jel = pk_jel.p;
+    // ion-flux segments handled by this rank: those whose element is local and whose lower
+    // global vertex is owned here, {local element, face, group}, in global segment order
+    std::vector<int> eloc(m.nt, -1);
+    for (int e2 = 0; e2 < ne; e2++) eloc[elist[e2]] = e2;
+    std::vector<int4> segs;
+    fseg_group.clear();
+    for (int sg = 0; sg < m.nb; sg++) {
+      const int a = m.bseg[2 * size_t(sg)], b = m.bseg[2 * size_t(sg) + 1];
+      const int lo = L.g2l[std::min(a, b)];
+      if (lo < 0 || lo >= L.n_owned) continue;
+      const int bf = pks.bface[sg];
+      if (bf < 0 || eloc[bf / 3] < 0) return fail(PNP_E_MESH, "ion flux: the element of a boundary segment is not local");
+      segs.push_back(make_int4(eloc[bf / 3], bf % 3, m.bgroup[sg], 0));
+      fseg_group.push_back(m.bgroup[sg]);
+    }
+    if ((rc = upv(d_fseg, segs, "P_k flux segments"))) return rc;
+    e = fluxout.alloc(2 * segs.size() + 2);
+    if (e != hipSuccess) return hipfail(e, "flux out");
+    return PNP_OK;
   }
 
   // local elements (ascending global id, vertices in mesh order) and, per owned row and slot, the
@@ -1277,6 +1408,15 @@ static void params_from(const pnp_params *pp, pnp::Params &P) {
 
 extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
                           const pnp_comm *comm, pnp_ctx **out) {
+  return pnp_create_pk(mesh, params, 1, device, comm, out);
+}
+
+extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int32_t degree,
+                             int32_t device, const pnp_comm *comm, pnp_ctx **out) {
+  if (degree < 1 || degree > 3) {
+    g_err = "pnp_create_pk: degree must be 1, 2 or 3 (PDEGREE)";
+    return PNP_E_ARG;
+  }
   if (!mesh || !params || !out) {
     g_err = "pnp_create: null argument";
     return PNP_E_ARG;
@@ -1308,7 +1448,19 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       return PNP_E_ARG;
     }
   }
-  if (!pnp::build_fans(c->mesh, c->fans, err)) {
+  c->degree = degree;
+  if (degree > 1) {  // the layout is built on the node graph of the P_k space
+    if (!pnp::validate(c->mesh, err) || !pnp::build_pk_space(c->mesh, degree, c->pks, err)) {
+      g_err = err;
+      return PNP_E_MESH;
+    }
+    c->tmesh = std::move(c->mesh);
+    c->mesh = pnp::pk_node_mesh(c->pks);
+    if (!pnp::pk_adjacency(c->tmesh, c->pks, c->fans, err)) {
+      g_err = err;
+      return PNP_E_MESH;
+    }
+  } else if (!pnp::build_fans(c->mesh, c->fans, err)) {
     g_err = err;
     return PNP_E_MESH;
   }
@@ -1587,6 +1739,10 @@ extern "C" int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_
       }
     }
   }
+  if (degree > 1 && (rc = c->pk_build())) {
+    g_err = c->err;
+    return rc;
+  }
   if (c->nranks > 1 && !comm->rccl_unique_id) {  // join the in-process group
     std::shared_ptr<LocalGroup> g;
     {
@@ -1642,6 +1798,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->lslots = (int64_t)c->d_lsrc.n;
   info->uslots = (int64_t)c->d_usrc.n;
   info->ilu_f32 = c->ilu_f32;
+  info->degree = c->degree;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->b.n + c->prevu.n + c->ext.n) * 8;
@@ -1669,6 +1826,10 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
     return c->fail(PNP_E_ARG, "diffusion operator needs phi and field 1 or 2");
   if (kind == PNP_OP_POISSON && (!a->cp || !a->cm))
     return c->fail(PNP_E_ARG, "Poisson operator needs cp and cm");
+  if (c->degree > 1 && (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER))
+    return c->fail(PNP_E_ARG,
+                   "PnpOperator / PnpTOperator are P1 in the reference (Pk2DLocalFiniteElementMap<..., 1>, "
+                   "src/stationary_pnp_from_pb.hh:206-208); P_k contexts take PB, Poisson and diffusion");
   c->kind = kind;
   c->fd_mode = false;  // the next Jacobian picks its form (set_fd)
   c->nf = (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER) ? 3 : 1;
@@ -1690,11 +1851,17 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   // Dirichlet mask and constant load (Neumann flux of alpha_boundary), owned rows
   int field0 = (kind == PNP_OP_DIFF || kind == PNP_OP_DIFF_IMPLICIT_EULER) ? a->field : 0;
   std::vector<uint8_t> mask;
-  pnp::dirichlet_mask(m, c->params, nf, field0, mask);
+  if (c->degree > 1)
+    pnp::pk_dirichlet_mask(c->tmesh, c->pks, c->params, nf, field0, mask);
+  else
+    pnp::dirichlet_mask(m, c->params, nf, field0, mask);
   std::vector<double> load(size_t(m.nv) * nf, 0.0);
   if (kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_PB ||
       kind == PNP_OP_POISSON) {
-    pnp::neumann_load(m, c->params, nf, 0, load);
+    if (c->degree > 1)
+      pnp::pk_neumann_load(c->tmesh, c->pks, c->params, nf, 0, load);
+    else
+      pnp::neumann_load(m, c->params, nf, 0, load);
     if (kind == PNP_OP_PNP_IMPLICIT_EULER)
       for (auto &v : load) v *= a->dt;
   }
@@ -1726,9 +1893,12 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   if (ie) {  // cvec -= M(x_old), rows of this rank (x_old with ghosts)
     if ((rc = c->upload_ext(a->x_old, nf, c->prevu.p, true))) return rc;
     int k = kind == PNP_OP_PNP_IMPLICIT_EULER ? pnp::OP_PNP_IE : pnp::OP_DIFF_IE;
-    CK(pnp::launch_mass_apply(c->dl, k, c->params.tau, c->params.pi, c->params.cylindrical,
-                              c->prevu.p, c->cvec.p, c->stream),
-       "mass apply");
+    if (c->degree > 1)
+      CK(pnp::launch_pk_mass_apply(c->dl, c->pkd, c->prevu.p, c->cvec.p, c->stream), "mass apply");
+    else
+      CK(pnp::launch_mass_apply(c->dl, k, c->params.tau, c->params.pi, c->params.cylindrical,
+                                c->prevu.p, c->cvec.p, c->stream),
+         "mass apply");
     CK(hipStreamSynchronize(c->stream), "mass apply");
   }
   pnp::AsmArgs &aa = c->aa;
@@ -2116,9 +2286,14 @@ extern "C" int pnp_ion_flux(pnp_ctx *c, const double *x, int32_t nsurf, double *
     return c->fail(PNP_E_STATE, "ion flux of the context state needs a 3-field (PNP) operator");
   }
   const int ns = int(c->fseg_group.size());
-  CK(pnp::launch_ion_flux(ns, c->d_fseg.p, c->d_xy.p, xd, c->params.cylindrical, c->params.pi,
-                          c->fluxout.p, c->stream),
-     "ion flux");
+  if (c->degree > 1)
+    CK(pnp::launch_pk_ion_flux(c->dl, c->pkd, ns, c->d_fseg.p, xd, c->params.cylindrical,
+                               c->params.pi, c->fluxout.p, c->stream),
+       "ion flux");
+  else
+    CK(pnp::launch_ion_flux(ns, c->d_fseg.p, c->d_xy.p, xd, c->params.cylindrical, c->params.pi,
+                            c->fluxout.p, c->stream),
+       "ion flux");
   std::vector<double> out(2 * size_t(ns)), acc(2 * size_t(nsurf), 0.0);
   if (ns) {
     CK(hipMemcpyAsync(out.data(), c->fluxout.p, sizeof(double) * out.size(),
@@ -2275,7 +2450,25 @@ extern "C" int pnp_sync_vector(pnp_ctx *c, double *v, int32_t nfields) {
 
 extern "C" int pnp_initial_state(pnp_ctx *c, const double *phi_pb, double *x0) {
   if (!c || !x0) return PNP_E_ARG;
-  pnp::initial_state(c->mesh, c->params, phi_pb, x0);
+  if (c->degree > 1)
+    pnp::pk_initial_state(c->tmesh, c->pks, c->params, phi_pb, x0);
+  else
+    pnp::initial_state(c->mesh, c->params, phi_pb, x0);
+  return PNP_OK;
+}
+
+extern "C" int pnp_space(pnp_ctx *c, pnp_space_info *info, double *xy, int32_t *enode) {
+  if (!c || !info) return PNP_E_ARG;
+  const bool pk = c->degree > 1;
+  info->degree = c->degree;
+  info->nnodes = c->mesh.nv;
+  info->nt = pk ? c->tmesh.nt : c->mesh.nt;
+  info->nlocal = pk ? c->pks.nl : 3;
+  if (xy) std::memcpy(xy, c->mesh.xy.data(), sizeof(double) * c->mesh.xy.size());
+  if (enode) {
+    const std::vector<int> &en = pk ? c->pks.enode : c->mesh.tri;
+    std::memcpy(enode, en.data(), sizeof(int) * en.size());
+  }
   return PNP_OK;
 }
 

@@ -385,4 +385,27 @@ hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *va
 // read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
 hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 
+// ---- P_k (k = 2, 3) scalar operators (pk_assemble.hip, pk.h) ----------------------------------
+// ne local elements (every element with an owned node; its nodes are all local), enode[a * ne + e]
+// the local node of local node a; per owned row: vdata[vptr[i] .. vptr[i+1]) the residual codes
+// a * ne + e, and cdata from rptr[i] for each slot the count then the codes (a * nl + b) * ne + e
+// into the element matrices; rel / jel the element scratch
+struct PkDev {
+  int k = 1, nl = 3, ne = 0;
+  const int *enode = nullptr;
+  const long long *vptr = nullptr, *rptr = nullptr;
+  const int *vdata = nullptr, *cdata = nullptr;
+  double *rel = nullptr, *jel = nullptr;
+};
+hipError_t pk_upload_tables(int k, hipStream_t s);
+// jac 0 residual, 1 analytic Jacobian, 2 forward-difference Jacobian (PNP_JAC_FD)
+hipError_t launch_pk_assemble(const DevLayout &L, const AsmArgs &aa, const PkDev &P, int jac,
+                              hipStream_t s);
+// cvec -= M(x_old): the DiffusionTOperator mass of the old time level
+hipError_t launch_pk_mass_apply(const DevLayout &L, const PkDev &P, const double *x_old,
+                                double *cvec, hipStream_t s);
+// calcIonFlux: seg = {local element, local face, group}; out[2s], out[2s+1]
+hipError_t launch_pk_ion_flux(const DevLayout &L, const PkDev &P, int ns, const int4 *seg,
+                              const double *x, int cyl, double pi, double *out, hipStream_t s);
+
 }  // namespace pnp

@@ -395,6 +395,13 @@ void neumann_load(const Mesh &m, const Params &p, int nf, int field0, std::vecto
 }
 
 void initial_state(const Mesh &m, const Params &p, const double *phi_pb, double *x0) {
+  initial_state_at(m, p, 3, m.tri.data(), m.xy.data(), m.nv, phi_pb, x0);
+}
+
+// the element loop of interpolate(BCExtension) over nl nodes per element (enode[e * nl + a], at
+// nxy), last write wins: P1 (the vertices) or the Lagrange nodes of a P_k space (pk.cc)
+void initial_state_at(const Mesh &m, const Params &p, int nl, const int *enode, const double *nxy,
+                      int nn, const double *phi_pb, double *x0) {
   // element neighbours and boundary faces (DUNE reference-triangle face order (0,1),(0,2),(1,2))
   static const int F[3][2] = {{0, 1}, {0, 2}, {1, 2}};
   std::unordered_map<uint64_t, int> seg, first;
@@ -430,11 +437,11 @@ void initial_state(const Mesh &m, const Params &p, const double *phi_pb, double 
     double ex = vx * proj - dx, ey = vy * proj - dy;
     return std::sqrt(ex * ex + ey * ey) < 1e-9;
   };
-  int nv = m.nv;
+  const int nv = nn;
   for (int e = 0; e < m.nt; e++) {
-    for (int a = 0; a < 3; a++) {
-      int v = m.tri[3 * e + a];
-      double px = m.xy[2 * size_t(v)], py = m.xy[2 * size_t(v) + 1];
+    for (int a = 0; a < nl; a++) {
+      int v = enode[size_t(nl) * e + a];
+      double px = nxy[2 * size_t(v)], py = nxy[2 * size_t(v) + 1];
       int pgi = -1;
       auto consider = [&](int s) {
         if (s < 0 || !on_line(s, px, py)) return;

@@ -82,6 +82,9 @@ void dirichlet_mask(const Mesh &m, const Params &p, int nf, int field0, std::vec
 void neumann_load(const Mesh &m, const Params &p, int nf, int field0, std::vector<double> &load);
 // BCExtension + interpolate (src/dirichlet_bc.hh:54-123): lexicographic x0[3nv] from phi_pb[nv]
 void initial_state(const Mesh &m, const Params &p, const double *phi_pb, double *x0);
+// the same over nl nodes per element (enode [nt][nl], node coordinates nxy [nn][2]); x0[3 nn]
+void initial_state_at(const Mesh &m, const Params &p, int nl, const int *enode, const double *nxy,
+                      int nn, const double *phi_pb, double *x0);
 
 // ---- distribution and local layout -----------------------------------------------------------
 // RCB on vertex coordinates into nparts (deterministic); part[v] in [0, nparts)

@@ -1,0 +1,503 @@
+// P_k (k = 2, 3) residual + Jacobian assembly on gfx950: the scalar LocalOperators of the
+// reference's operator-split driver with its compile-time PDEGREE (src/instationary_pnp_from_pb_md.hh
+// :26-28, 125, 245-247): PBOperator (src/pb_operator.hh:46-122), PoissonOperator
+// (src/poisson_operator.hh:46-127), DiffusionOperator (src/diffusion_operator.hh:42-112) and
+// DiffusionTOperator (src/diffusion_toperator.hh:38-73), each with its own quadrature order
+// (PB / Poisson 3, Diffusion 2 -- the default of its constructor, :36 --, DiffusionT 5, the
+// `cptop(5)` of src/instationary_pnp_from_pb_md.hh:363).
+//
+// Two launches, no atomics, deterministic:
+//   k_pk_element  one thread per local element: the element residual (nl values) and the element
+//                 matrix (nl x nl; analytic, or PDELab's forward differences for PNP_JAC_FD) into
+//                 SoA scratch rel[a][e], jel[a*nl+b][e] (coalesced stores across the wave);
+//   k_pk_gather   one thread per owned node row (SELL lane order): the row's residual and every
+//                 SELL block summed from its element contributions in ascending element order
+//                 (the order PDELab's element loop accumulates them), blocks stored slot by slot,
+//                 i.e. one coalesced 512-byte line per slot and wave.
+// The P1 path keeps its fan-walk kernels (assemble.hip); the element work of P_k is small next to
+// its matrix traffic (P2: 36, P3: 100 entries per element) and the two-pass form keeps every
+// store whole-line and every sum in a fixed order.
+#include <cmath>
+#include <vector>
+
+#include "kernels.h"
+#include "pk.h"
+
+namespace pnp {
+
+namespace {
+
+constexpr int kB = 256;
+
+template <int NL>
+struct PkPoint {
+  double xi, eta, w;
+  double phi[NL];
+  double dphi[NL][2];
+};
+// the quadrature rules of the reference's intorders on the reference triangle (weights sum to
+// 1/2; dune-geometry SimplexQuadraturePoints<2>, restated: order 2 the 3-point rule, order 3 the
+// Strang-Fix 4-point rule, order 5 Radon's 7-point rule) and the three face centres (ion flux)
+template <int NL>
+struct PkTab {
+  PkPoint<NL> q2[3], q3[4], q5[7], fc[3];
+};
+__constant__ PkTab<6> c_tab2;
+__constant__ PkTab<10> c_tab3;
+
+template <int K>
+struct PkK {
+  static constexpr int NL = (K + 1) * (K + 2) / 2;
+};
+
+template <int K>
+__device__ __forceinline__ const PkTab<PkK<K>::NL> &tab() {
+  if constexpr (K == 2)
+    return c_tab2;
+  else
+    return c_tab3;
+}
+
+struct PkGeo {
+  double y0, J10, J11, adet;
+  double it00, it01, it10, it11;  // jacobianInverseTransposed
+};
+
+__device__ __forceinline__ PkGeo pk_geometry(double2 p0, double2 p1, double2 p2) {
+  PkGeo G;
+  const double J00 = p1.x - p0.x, J01 = p2.x - p0.x, J10 = p1.y - p0.y, J11 = p2.y - p0.y;
+  const double det = J00 * J11 - J01 * J10;
+  G.y0 = p0.y;
+  G.J10 = J10;
+  G.J11 = J11;
+  G.adet = fabs(det);
+  G.it00 = J11 / det;
+  G.it01 = -J10 / det;
+  G.it10 = -J01 / det;
+  G.it11 = J00 / det;
+  return G;
+}
+
+// physical gradient of local basis function b at a table point
+template <int NL>
+__device__ __forceinline__ void grad(const PkGeo &G, const PkPoint<NL> &P, int b, double &g0,
+                                     double &g1) {
+  g0 = G.it00 * P.dphi[b][0] + G.it01 * P.dphi[b][1];
+  g1 = G.it10 * P.dphi[b][0] + G.it11 * P.dphi[b][1];
+}
+
+struct PkArgs {
+  int kind, cyl, mass;  // mass: the DiffusionTOperator mass M(x) alone (old time level)
+  double l_b, c0, pi, dt, z;
+};
+
+// quadrature factor of the reference: weight * integrationElement (* 2 PI y when cylindrical)
+template <int NL>
+__device__ __forceinline__ double factor(const PkGeo &G, const PkPoint<NL> &P, int cyl, double pi) {
+  double f = P.w * G.adet;
+  if (cyl) f *= (G.y0 + G.J10 * P.xi + G.J11 * P.eta) * 2 * pi;
+  return f;
+}
+
+// element residual rl[NL] (zeroed here) of the operator at local values xl; f0 / f1 the frozen
+// fields (DIFF: phi; POISSON: c+, c-)
+template <int K>
+__device__ void pk_residual(const PkGeo &G, const PkArgs &a, const double *xl, const double *f0,
+                            const double *f1, double *rl) {
+  constexpr int NL = PkK<K>::NL;
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+#pragma unroll
+  for (int i = 0; i < NL; i++) rl[i] = 0.0;
+  if (a.mass || a.kind == OP_DIFF_IE) {  // DiffusionTOperator, order 5, u * phi_i
+    for (int q = 0; q < 7; q++) {
+      const auto &P = T.q5[q];
+      double u = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+      const double f = P.w * G.adet;
+#pragma unroll
+      for (int i = 0; i < NL; i++) rl[i] += u * P.phi[i] * f;
+    }
+    if (a.mass) return;
+  }
+  if (a.kind == OP_PB || a.kind == OP_POISSON) {  // order 3 (src/pb_operator.hh:114-120,
+    for (int q = 0; q < 4; q++) {                 //  src/poisson_operator.hh:119-125)
+      const auto &P = T.q3[q];
+      const double f = factor(G, P, a.cyl, PI);
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g0;
+        gu1 += xl[i] * g1;
+        if (a.kind == OP_POISSON) {
+          cp += f0[i] * P.phi[i];
+          cm += f1[i] * P.phi[i];
+        }
+      }
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        rl[i] += (gu0 * g0 + gu1 * g1 + s * P.phi[i]) * f;
+      }
+    }
+  } else {  // OP_DIFF / OP_DIFF_IE: order 2, no cylindrical weight (Q8), grad of the frozen phi
+    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+    for (int q = 0; q < 3; q++) {
+      const auto &P = T.q2[q];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g0;
+        gu1 += xl[i] * g1;
+        gP0 += f0[i] * g0;
+        gP1 += f0[i] * g1;
+      }
+      const double f = P.w * G.adet;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {  // src/diffusion_operator.hh:109-110, a = 0
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        rl[i] += sc * ((gu0 * g0 + gu1 * g1 + u * a.z * (gP0 * g0 + gP1 * g1) + 0.0 * u * P.phi[i]) * f);
+      }
+    }
+  }
+}
+
+// analytic element matrix row a: J[a][b] = d rl[a] / d xl[b]
+template <int K>
+__device__ void pk_jac_row(const PkGeo &G, const PkArgs &a, int ra, const double *xl,
+                           const double *f0, double *Jr) {
+  constexpr int NL = PkK<K>::NL;
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+#pragma unroll
+  for (int b = 0; b < NL; b++) Jr[b] = 0.0;
+  if (a.kind == OP_DIFF_IE) {
+    for (int q = 0; q < 7; q++) {
+      const auto &P = T.q5[q];
+      const double f = P.w * G.adet;
+#pragma unroll
+      for (int b = 0; b < NL; b++) Jr[b] += P.phi[ra] * P.phi[b] * f;
+    }
+  }
+  if (a.kind == OP_PB || a.kind == OP_POISSON) {
+    for (int q = 0; q < 4; q++) {
+      const auto &P = T.q3[q];
+      const double f = factor(G, P, a.cyl, PI);
+      double c = 0.0;
+      if (a.kind == OP_PB) {
+        double u = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+        c = 8 * PI * a.l_b * a.c0 * cosh(u) * P.phi[ra];
+      }
+      double ga0, ga1;
+      grad(G, P, ra, ga0, ga1);
+#pragma unroll
+      for (int b = 0; b < NL; b++) {
+        double g0, g1;
+        grad(G, P, b, g0, g1);
+        Jr[b] += (ga0 * g0 + ga1 * g1 + c * P.phi[b]) * f;
+      }
+    }
+  } else {
+    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+    for (int q = 0; q < 3; q++) {
+      const auto &P = T.q2[q];
+      double gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        gP0 += f0[i] * g0;
+        gP1 += f0[i] * g1;
+      }
+      double ga0, ga1;
+      grad(G, P, ra, ga0, ga1);
+      const double f = P.w * G.adet, drift = a.z * (gP0 * ga0 + gP1 * ga1);
+#pragma unroll
+      for (int b = 0; b < NL; b++) {
+        double g0, g1;
+        grad(G, P, b, g0, g1);
+        Jr[b] += sc * ((ga0 * g0 + ga1 * g1 + P.phi[b] * drift) * f);
+      }
+    }
+  }
+}
+
+// JAC 0: residual only, 1: analytic Jacobian, 2: forward differences (NumericalJacobianVolume,
+// eps 1e-7 (1 + |x_j|))
+template <int K, int JAC>
+__global__ __launch_bounds__(kB) void k_pk_element(int ne, const int *__restrict__ enode,
+                                                   const double *__restrict__ xy,
+                                                   const double *__restrict__ x,
+                                                   const double *__restrict__ aux0,
+                                                   const double *__restrict__ aux1, PkArgs a,
+                                                   double *__restrict__ rel,
+                                                   double *__restrict__ jel) {
+  constexpr int NL = PkK<K>::NL;
+  const int e = blockIdx.x * kB + threadIdx.x;
+  if (e >= ne) return;
+  int nd[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) nd[i] = enode[size_t(i) * ne + e];
+  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
+  const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
+  double xl[NL], f0[NL], f1[NL], rl[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    xl[i] = x[nd[i]];
+    f0[i] = aux0 ? aux0[nd[i]] : 0.0;
+    f1[i] = aux1 ? aux1[nd[i]] : 0.0;
+  }
+  pk_residual<K>(G, a, xl, f0, f1, rl);
+#pragma unroll
+  for (int i = 0; i < NL; i++) rel[size_t(i) * ne + e] = rl[i];
+  if constexpr (JAC == 1) {
+    for (int r = 0; r < NL; r++) {
+      double Jr[NL];
+      pk_jac_row<K>(G, a, r, xl, f0, Jr);
+#pragma unroll
+      for (int b = 0; b < NL; b++) jel[size_t(r * NL + b) * ne + e] = Jr[b];
+    }
+  } else if constexpr (JAC == 2) {
+    for (int j = 0; j < NL; j++) {
+      double up[NL];
+      const double xj = xl[j], delta = 1e-7 * (1.0 + fabs(xj));
+      xl[j] = xj + delta;
+      pk_residual<K>(G, a, xl, f0, f1, up);
+      xl[j] = xj;
+#pragma unroll
+      for (int i = 0; i < NL; i++) jel[size_t(i * NL + j) * ne + e] = (up[i] - rl[i]) / delta;
+    }
+  }
+}
+
+// residual rows: mode 0 r = (dmask ? 0 : cvec + sum), mode 1 cvec -= sum (old-time mass)
+__global__ __launch_bounds__(kB) void k_pk_gather_res(int n, const long long *__restrict__ vptr,
+                                                      const int *__restrict__ vdata,
+                                                      const double *__restrict__ rel, int mode,
+                                                      const uint8_t *__restrict__ dmask,
+                                                      double *__restrict__ cvec,
+                                                      double *__restrict__ r) {
+  const int row = blockIdx.x * kB + threadIdx.x;
+  if (row >= n) return;
+  double s = 0.0;
+  for (long long p = vptr[row]; p < vptr[row + 1]; p++) s += rel[vdata[p]];
+  if (mode == 1) {
+    cvec[row] -= s;
+  } else {
+    const double rv = s + cvec[row];
+    r[row] = dmask[row] != 0 ? 0.0 : rv;
+  }
+}
+
+// SELL blocks of the owned rows: cdata per row, for each slot the count then the codes into jel
+__global__ __launch_bounds__(kB) void k_pk_gather_jac(DevLayout L, const long long *__restrict__ rptr,
+                                                      const int *__restrict__ cdata,
+                                                      const double *__restrict__ jel,
+                                                      double *__restrict__ vals) {
+  const int row = blockIdx.x * kB + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk], len = int(L.rowmeta[row] & 63);
+  long long p = rptr[row];
+  for (int s = 0; s < len; s++) {
+    double acc = 0.0;
+    const int n = cdata[p++];
+    for (int k = 0; k < n; k++) acc += jel[cdata[p++]];
+    __builtin_nontemporal_store(acc, vals + size_t(off) + size_t(s) * kRows + lane);
+  }
+}
+
+// calcIonFlux (src/ionFlux.hh:50-91) on P_k: one thread per boundary segment of this rank;
+// seg = {element (local), local face, group}; the three fields at the face centre from the
+// element's nodes.  out[2s] / out[2s+1]: ip / im contributions (summed on the host in segment order)
+template <int K>
+__global__ __launch_bounds__(kB) void k_pk_ion_flux(int ns, const int4 *__restrict__ seg, int ne,
+                                                    const int *__restrict__ enode,
+                                                    const double *__restrict__ xy,
+                                                    const double *__restrict__ x, int cyl,
+                                                    double pi, double *__restrict__ out) {
+  constexpr int NL = PkK<K>::NL;
+  const int s = blockIdx.x * kB + threadIdx.x;
+  if (s >= ns) return;
+  const int4 sg = seg[s];
+  const int e = sg.x, f = sg.y;
+  int nd[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) nd[i] = enode[size_t(i) * ne + e];
+  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
+  const double2 p0 = xy2[nd[0]], p1 = xy2[nd[1]], p2 = xy2[nd[2]];
+  const PkGeo G = pk_geometry(p0, p1, p2);
+  const auto &P = tab<K>().fc[f];
+  double phi = 0, cp = 0, cm = 0, gph[2] = {0, 0}, gcp[2] = {0, 0}, gcm[2] = {0, 0};
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    double g0, g1;
+    grad(G, P, i, g0, g1);
+    const double u0 = x[3 * size_t(nd[i])], u1 = x[3 * size_t(nd[i]) + 1], u2 = x[3 * size_t(nd[i]) + 2];
+    phi += u0 * P.phi[i];
+    cp += u1 * P.phi[i];
+    cm += u2 * P.phi[i];
+    gph[0] += u0 * g0;
+    gph[1] += u0 * g1;
+    gcp[0] += u1 * g0;
+    gcp[1] += u1 * g1;
+    gcm[0] += u2 * g0;
+    gcm[1] += u2 * g1;
+  }
+  (void)phi;
+  // face f of the reference triangle: (0,1), (0,2), (1,2); outer normal of the element there
+  const int fa[3] = {0, 0, 1}, fb[3] = {1, 2, 2}, fo[3] = {2, 1, 0};
+  const double2 V[3] = {p0, p1, p2};
+  const double2 A = V[fa[f]], B = V[fb[f]], O = V[fo[f]];
+  const double tx = B.x - A.x, ty = B.y - A.y;
+  const double len = sqrt(tx * tx + ty * ty);
+  double nx = ty / len, ny = -tx / len;
+  if (nx * (O.x - A.x) + ny * (O.y - A.y) > 0) {
+    nx = -nx;
+    ny = -ny;
+  }
+  double factor = len;
+  if (cyl) factor *= 2 * pi * (G.y0 + G.J10 * P.xi + G.J11 * P.eta);
+  const double gC0 = -factor * gcp[0], gC1 = -factor * gcp[1];
+  const double gM0 = -factor * gcm[0], gM1 = -factor * gcm[1];
+  double gp0 = factor * gph[0] * cp, gp1 = factor * gph[1] * cp;
+  out[2 * size_t(s)] = (gC0 + gp0) * nx + (gC1 + gp1) * ny;
+  gp0 *= cm / cp;
+  gp1 *= cm / cp;
+  out[2 * size_t(s) + 1] = (gM0 - gp0) * nx + (gM1 - gp1) * ny;
+}
+
+template <int NL>
+void fill_tab(int k, PkTab<NL> &T) {
+  const double s15 = std::sqrt(15.0);
+  const double a1 = (6.0 - s15) / 21.0, a2 = (6.0 + s15) / 21.0;
+  const double w1 = (155.0 - s15) / 2400.0, w2 = (155.0 + s15) / 2400.0;
+  const double q2[3][3] = {{4.0 / 6.0, 1.0 / 6.0, 0.5 / 3.0},
+                           {1.0 / 6.0, 4.0 / 6.0, 0.5 / 3.0},
+                           {1.0 / 6.0, 1.0 / 6.0, 0.5 / 3.0}};
+  const double q3[4][3] = {{10.0 / 30.0, 10.0 / 30.0, 0.5 * -27.0 / 48.0},
+                           {18.0 / 30.0, 6.0 / 30.0, 0.5 * 25.0 / 48.0},
+                           {6.0 / 30.0, 18.0 / 30.0, 0.5 * 25.0 / 48.0},
+                           {6.0 / 30.0, 6.0 / 30.0, 0.5 * 25.0 / 48.0}};
+  const double q5[7][3] = {{1.0 / 3.0, 1.0 / 3.0, 9.0 / 80.0},
+                           {a1, a1, w1}, {1.0 - 2.0 * a1, a1, w1}, {a1, 1.0 - 2.0 * a1, w1},
+                           {a2, a2, w2}, {1.0 - 2.0 * a2, a2, w2}, {a2, 1.0 - 2.0 * a2, w2}};
+  const double fc[3][3] = {{0.5, 0.0, 0.0}, {0.0, 0.5, 0.0}, {0.5, 0.5, 0.0}};
+  auto set = [&](PkPoint<NL> &P, const double *r) {
+    P.xi = r[0];
+    P.eta = r[1];
+    P.w = r[2];
+    double phi[NL], dphi[2 * NL];
+    pk_basis(k, P.xi, P.eta, phi, dphi);
+    for (int i = 0; i < NL; i++) {
+      P.phi[i] = phi[i];
+      P.dphi[i][0] = dphi[2 * i];
+      P.dphi[i][1] = dphi[2 * i + 1];
+    }
+  };
+  for (int q = 0; q < 3; q++) set(T.q2[q], q2[q]);
+  for (int q = 0; q < 4; q++) set(T.q3[q], q3[q]);
+  for (int q = 0; q < 7; q++) set(T.q5[q], q5[q]);
+  for (int q = 0; q < 3; q++) set(T.fc[q], fc[q]);
+}
+
+template <int K>
+hipError_t upload_tab(hipStream_t s) {
+  static PkTab<PkK<K>::NL> T;  // the same for every context of degree K
+  static bool filled = false;
+  if (!filled) {
+    fill_tab<PkK<K>::NL>(K, T);
+    filled = true;
+  }
+  if constexpr (K == 2)
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_tab2), &T, sizeof T, 0, hipMemcpyHostToDevice, s);
+  else
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_tab3), &T, sizeof T, 0, hipMemcpyHostToDevice, s);
+}
+
+template <int K>
+hipError_t element_launch(int ne, const int *enode, const double *xy, const double *x,
+                          const double *aux0, const double *aux1, const PkArgs &a, int jac,
+                          double *rel, double *jel, hipStream_t s) {
+  const dim3 g((ne + kB - 1) / kB), b(kB);
+  if (jac == 0)
+    hipLaunchKernelGGL((k_pk_element<K, 0>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
+  else if (jac == 1)
+    hipLaunchKernelGGL((k_pk_element<K, 1>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
+  else
+    hipLaunchKernelGGL((k_pk_element<K, 2>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t pk_upload_tables(int k, hipStream_t s) {
+  if (k == 2) return upload_tab<2>(s);
+  if (k == 3) return upload_tab<3>(s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_pk_assemble(const DevLayout &L, const AsmArgs &aa, const PkDev &P, int jac,
+                              hipStream_t s) {
+  if (P.k != 2 && P.k != 3) return hipErrorInvalidValue;
+  const bool diff = aa.kind == OP_DIFF || aa.kind == OP_DIFF_IE;
+  const double *f0 = (diff || aa.kind == OP_POISSON) ? aa.aux0 : nullptr;
+  const double *f1 = aa.kind == OP_POISSON ? aa.aux1 : nullptr;
+  PkArgs a{aa.kind, aa.cylindrical, 0, aa.l_b, aa.c0, aa.pi, aa.dt, aa.z};
+  hipError_t e = hipSuccess;
+  if (P.ne > 0) {
+    e = P.k == 2 ? element_launch<2>(P.ne, P.enode, L.xy, aa.x, f0, f1, a, jac, P.rel, P.jel, s)
+                 : element_launch<3>(P.ne, P.enode, L.xy, aa.x, f0, f1, a, jac, P.rel, P.jel, s);
+    if (e != hipSuccess) return e;
+  }
+  if (L.n_owned == 0) return hipSuccess;
+  const dim3 gr((L.n_owned + kB - 1) / kB), b(kB);
+  hipLaunchKernelGGL(k_pk_gather_res, gr, b, 0, s, L.n_owned, P.vptr, P.vdata, P.rel, 0, aa.dmask,
+                     const_cast<double *>(aa.cvec), aa.r);
+  if (jac) hipLaunchKernelGGL(k_pk_gather_jac, gr, b, 0, s, L, P.rptr, P.cdata, P.jel, aa.vals);
+  return hipGetLastError();
+}
+
+hipError_t launch_pk_mass_apply(const DevLayout &L, const PkDev &P, const double *x_old,
+                                double *cvec, hipStream_t s) {
+  PkArgs a{OP_DIFF_IE, 0, 1, 0, 0, 0, 0, 0};
+  hipError_t e = hipSuccess;
+  if (P.ne > 0) {
+    e = P.k == 2 ? element_launch<2>(P.ne, P.enode, L.xy, x_old, nullptr, nullptr, a, 0, P.rel,
+                                     nullptr, s)
+                 : element_launch<3>(P.ne, P.enode, L.xy, x_old, nullptr, nullptr, a, 0, P.rel,
+                                     nullptr, s);
+    if (e != hipSuccess) return e;
+  }
+  if (L.n_owned == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pk_gather_res, dim3((L.n_owned + kB - 1) / kB), dim3(kB), 0, s, L.n_owned,
+                     P.vptr, P.vdata, P.rel, 1, nullptr, cvec, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_pk_ion_flux(const DevLayout &L, const PkDev &P, int ns, const int4 *seg,
+                              const double *x, int cyl, double pi, double *out, hipStream_t s) {
+  if (ns <= 0) return hipSuccess;
+  const dim3 g((ns + kB - 1) / kB), b(kB);
+  if (P.k == 2)
+    hipLaunchKernelGGL(k_pk_ion_flux<2>, g, b, 0, s, ns, seg, P.ne, P.enode, L.xy, x, cyl, pi, out);
+  else if (P.k == 3)
+    hipLaunchKernelGGL(k_pk_ion_flux<3>, g, b, 0, s, ns, seg, P.ne, P.enode, L.xy, x, cyl, pi, out);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace pnp

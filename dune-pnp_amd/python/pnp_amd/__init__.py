@@ -91,7 +91,12 @@ class _Info(C.Structure):
                 ("max_slots", C.c_int32), ("nranks", C.c_int32), ("nblocks", C.c_int64),
                 ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
                 ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
-                ("uslots", C.c_int64), ("ilu_f32", C.c_int32)]
+                ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32)]
+
+
+class _SpaceInfo(C.Structure):
+    _fields_ = [("degree", C.c_int32), ("nnodes", C.c_int32), ("nt", C.c_int32),
+                ("nlocal", C.c_int32)]
 
 
 class _OpArgs(C.Structure):
@@ -176,6 +181,8 @@ def lib():
         L.pnp_last_error.argtypes = [C.c_void_p]
         L.pnp_create.argtypes = [C.POINTER(_Mesh), C.POINTER(_Params), C.c_int32,
                                  C.POINTER(_Comm), C.POINTER(C.c_void_p)]
+        L.pnp_create_pk.argtypes = [C.POINTER(_Mesh), C.POINTER(_Params), C.c_int32, C.c_int32,
+                                    C.POINTER(_Comm), C.POINTER(C.c_void_p)]
         for name in ("pnp_destroy", "pnp_mesh_free", "pnp_layout_free"):
             getattr(L, name).restype = None
             getattr(L, name).argtypes = [C.c_void_p]
@@ -407,7 +414,9 @@ class Context:
     """One GPU (one rank): mesh + parameters resident in HBM, one operator at a time."""
 
     def __init__(self, mesh: Mesh, params: Params, device=0, rank=0, size=1, unique_id=None,
-                 local_group=None):
+                 local_group=None, degree=1):
+        """degree 2 / 3: the Lagrange P_k space (pnp_create_pk, the reference's PDEGREE); its
+        vectors have nfields x nn entries over the nodes of space()."""
         self.mesh, self.params = mesh, params
         self._uid = C.create_string_buffer(unique_id, 128) if unique_id else None
         self._grp = local_group.encode() if local_group else None
@@ -415,9 +424,11 @@ class Context:
                      self._grp)
         h = C.c_void_p()
         m = mesh.c()
-        _check(lib().pnp_create(C.byref(m), C.byref(params.c), int(device), C.byref(comm),
-                                C.byref(h)))
+        _check(lib().pnp_create_pk(C.byref(m), C.byref(params.c), int(degree), int(device),
+                                   C.byref(comm), C.byref(h)))
         self.h = h
+        self.degree = int(degree)
+        self.nn = self.info()["nv_global"]  # DOF nodes (= mesh.nv for degree 1)
         self.nf = 0
         self.rank, self.size = rank, size
 
@@ -440,6 +451,15 @@ class Context:
         self._ck(lib().pnp_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in _Info._fields_}
 
+    def space(self):
+        """(xy [nn, 2], enode [nt, nlocal]) of the context's Lagrange space (pnp_space)."""
+        si = _SpaceInfo()
+        self._ck(lib().pnp_space(self.h, C.byref(si), None, None))
+        xy = np.zeros((si.nnodes, 2))
+        en = np.zeros((si.nt, si.nlocal), dtype=np.int32)
+        self._ck(lib().pnp_space(self.h, C.byref(si), _ptr(xy), _ptr(en)))
+        return xy, en
+
     def set_operator(self, kind, dt=0.0, z=0.0, field=0, phi=None, cp=None, cm=None, x_old=None,
                      c_extra=None):
         keep = [np.ascontiguousarray(a, dtype=np.float64) if a is not None else None
@@ -451,8 +471,8 @@ class Context:
 
     def _vec(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
-        if x.size != self.nf * self.mesh.nv:
-            raise PnpError(E_ARG, f"vector of size {x.size}, expected {self.nf * self.mesh.nv}")
+        if x.size != self.nf * self.nn:
+            raise PnpError(E_ARG, f"vector of size {x.size}, expected {self.nf * self.nn}")
         return x
 
     def residual(self, x):
@@ -473,7 +493,7 @@ class Context:
         import scipy.sparse as sp
         nnz = C.c_int64()
         self._ck(lib().pnp_jacobian_export(self.h, C.byref(nnz), None, None, None))
-        n = self.nf * self.mesh.nv
+        n = self.nf * self.nn
         rp = np.zeros(n + 1, dtype=np.int32)
         col = np.zeros(nnz.value, dtype=np.int32)
         val = np.zeros(nnz.value, dtype=np.float64)
@@ -554,7 +574,7 @@ class Context:
     def amg_aggregates(self, level):
         """level 0: aggregate per global vertex (-1: not owned); level l: per level-l row."""
         info = self.amg_info()
-        n = self.mesh.nv if level == 0 else info["rows"][level]
+        n = self.nn if level == 0 else info["rows"][level]
         agg = np.zeros(n, dtype=np.int32)
         self._ck(lib().pnp_amg_aggregates(self.h, int(level), _ptr(agg)))
         return agg
@@ -566,7 +586,7 @@ class Context:
         ip = np.zeros(n)
         im = np.zeros(n)
         xv = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
-        if xv is not None and xv.size != 3 * self.mesh.nv:
+        if xv is not None and xv.size != 3 * self.nn:
             raise PnpError(E_ARG, "ion_flux needs a 3-field state")
         self._ck(lib().pnp_ion_flux(self.h, _ptr(xv), n, _ptr(ip), _ptr(im)))
         return ip, im
@@ -583,14 +603,14 @@ class Context:
 
     def sync_vector(self, v, nfields=None):
         """Collective: global vector from every rank's owned entries (no-op on one GPU)."""
-        nf = nfields or (v.size // self.mesh.nv)
+        nf = nfields or (v.size // self.nn)
         v = np.ascontiguousarray(v, dtype=np.float64).copy()
         self._ck(lib().pnp_sync_vector(self.h, _ptr(v), int(nf)))
         return v
 
     def initial_state(self, phi_pb):
         phi = np.ascontiguousarray(phi_pb, dtype=np.float64)
-        x0 = np.zeros(3 * self.mesh.nv)
+        x0 = np.zeros(3 * self.nn)
         self._ck(lib().pnp_initial_state(self.h, _ptr(phi), _ptr(x0)))
         return x0
 
@@ -600,7 +620,7 @@ class Context:
         self._ck(lib().pnp_state_set(self.h, _ptr(x)))
 
     def state_get(self):
-        x = np.zeros(self.nf * self.mesh.nv)
+        x = np.zeros(self.nf * self.nn)
         self._ck(lib().pnp_state_get(self.h, _ptr(x)))
         return x
 

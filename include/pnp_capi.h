@@ -135,6 +135,16 @@ typedef struct {
 
 int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
                const pnp_comm *comm, pnp_ctx **out);
+/* The same on the Lagrange P_k space of degree 1, 2 or 3: the reference's compile-time PDEGREE
+ * (Pk2DLocalFiniteElementMap<GV, Coord, Real, PDEGREE>, src/instationary_pnp_from_pb_md.hh:26-28,
+ * 125, 245-247; the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111).  pnp_create is
+ * degree 1.  For degree > 1 the DOFs are the Lagrange nodes (pnp_space): the mesh vertices first,
+ * then k-1 points per edge, then the interior points (k = 3: one per triangle); every vector at
+ * this boundary has nfields x nnodes entries, and the operators are the scalar ones of the
+ * operator-split driver (PB, Poisson, diffusion, diffusion + mass) -- PnpOperator is P1 in the
+ * reference (src/stationary_pnp_from_pb.hh:206-208) and is refused. */
+int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int32_t degree, int32_t device,
+                  const pnp_comm *comm, pnp_ctx **out);
 void pnp_destroy(pnp_ctx *ctx);
 /* message of the last failure on ctx (or of the last failed pnp_create / mesh call if ctx NULL) */
 const char *pnp_last_error(const pnp_ctx *ctx);
@@ -152,8 +162,18 @@ typedef struct {
   int32_t nvb;           /* block-pattern values per block (expanded, e.g. 7 for PNP) */
   int64_t lslots, uslots;/* slots of the strictly-lower / diagonal+upper split storage */
   int32_t ilu_f32;       /* PNP_OPT_ILU_F32 */
+  int32_t degree;        /* polynomial degree of the space (pnp_create_pk); nv_global = its nodes */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
+
+/* The DOF space of the context (GridFunctionSpace): nnodes Lagrange nodes (= nv_global), their
+ * coordinates xy[nnodes][2] and the nodes of each triangle enode[nt][nlocal] (local order:
+ * vertices 0, 1, 2; the k-1 points of the faces (0,1), (0,2), (1,2) from the face's first vertex to
+ * its second; interior points).  xy / enode may be NULL (query the sizes first). */
+typedef struct {
+  int32_t degree, nnodes, nt, nlocal;
+} pnp_space_info;
+int pnp_space(pnp_ctx *ctx, pnp_space_info *info, double *xy, int32_t *enode);
 
 /* ---- operators (LocalOperator + GridOperator) ---------------------------------------------- */
 enum {

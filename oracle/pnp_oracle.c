@@ -342,7 +342,13 @@ static int on_line(const orc_mesh *m, int b, double px, double py) {
 }
 
 void orc_initial_state(const orc_mesh *m, const orc_params *p, const double *phi_pb, double *x0) {
-  int nv = m->nv, nt = m->nt;
+  orc_initial_state_nodes(m, p, 3, m->tri, m->xy, m->nv, phi_pb, x0);
+}
+
+/* the same element loop over nl nodes per element (enode[e*nl+a] at nxy), x0[3 nn] */
+void orc_initial_state_nodes(const orc_mesh *m, const orc_params *p, int nl, const int *enode,
+                             const double *nxy, int nn, const double *phi_pb, double *x0) {
+  int nv = nn, nt = m->nt;
   /* boundary segments by edge, element neighbours by edge */
   ehash bh, eh;
   eh_init(&bh, m->nb);
@@ -376,10 +382,9 @@ void orc_initial_state(const orc_mesh *m, const orc_params *p, const double *phi
   }
   /* Q5: BCExtension::bctype() falls through every case -> minusDiffusionBtype */
   for (int e = 0; e < nt; e++) {
-    const int *t = m->tri + 3 * e;
-    for (int a = 0; a < 3; a++) {
-      int v = t[a];
-      double px = m->xy[2 * v], py = m->xy[2 * v + 1];
+    for (int a = 0; a < nl; a++) {
+      int v = enode[nl * e + a];
+      double px = nxy[2 * v], py = nxy[2 * v + 1];
       int pgi = -1;
       for (int k = 0; k < 3; k++) {
         if (bsi[3 * e + k] >= 0) { /* ii->boundary() */

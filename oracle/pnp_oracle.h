@@ -76,6 +76,10 @@ void orc_flux_container(const orc_mesh *m, const orc_params *p, double *flux);
 /* BCExtension::evaluate via PDELab interpolate (src/dirichlet_bc.hh:54-123): x0[3nv] from the PB
  * potential phi_pb[nv]; element loop in tri[] order, last write wins. */
 void orc_initial_state(const orc_mesh *m, const orc_params *p, const double *phi_pb, double *x0);
+/* the same element loop over nl nodes per element (enode[e*nl+a] at node coordinates nxy[nn][2]):
+ * x0[3 nn] (P_k: the Lagrange nodes) */
+void orc_initial_state_nodes(const orc_mesh *m, const orc_params *p, int nl, const int *enode,
+                             const double *nxy, int nn, const double *phi_pb, double *x0);
 
 /* ---- residuals (a1,a2,a4,a5,a6,a7,f1) -------------------------------------------------- */
 /* PnpOperator alpha_volume + alpha_boundary (src/pnp_operator.hh:46-315) + constraints. */
@@ -182,6 +186,32 @@ void orc_newton(const orc_mesh *m, const orc_params *p, const orc_operator *op, 
  * x = [phi | c+ | c-] (lexicographic, 3*nv).  ip, im: [nsurf], indexed by bgroup. */
 void orc_ion_flux(const orc_mesh *m, const orc_params *p, const double *x, double *ip,
                   double *im);
+
+/* ---- f4: P_k elements (PDEGREE 2, 3), pnp_oracle_pk.c --------------------------------------
+ * The scalar operators of the operator-split driver on the Lagrange space of degree k
+ * (src/instationary_pnp_from_pb_md.hh:26-28, 125, 245-247).  Vectors are over the space's nodes
+ * (S->nn); op->phi / cp / cm / x_old too.  PB and Poisson add their coulomb Neumann flux
+ * (op->flux [nb][3], or the surfaces' coulomb flux when NULL). */
+typedef struct {
+  int k, nl, nn, nedge;
+  double *xy; /* [nn][2] */
+  int *enode; /* [nt][nl]: vertices, face points (faces (0,1),(0,2),(1,2)), interior points */
+} orc_pk;
+int orc_pk_build(const orc_mesh *m, int k, orc_pk *S);
+void orc_pk_free(orc_pk *S);
+/* Lagrange basis of degree k on the local nodes at (xi, eta): phi[nl], dphi[nl][2] */
+void orc_pk_basis(int k, double xi, double eta, double *phi, double *dphi);
+void orc_pk_dirichlet_mask(const orc_mesh *m, const orc_pk *S, const orc_params *p, int field,
+                           uint8_t *mask);
+void orc_pk_residual(const orc_mesh *m, const orc_pk *S, const orc_params *p,
+                     const orc_operator *op, const double *x, double *r);
+void orc_pk_csr_pattern(const orc_mesh *m, const orc_pk *S, orc_csr *A);
+void orc_pk_jacobian(const orc_mesh *m, const orc_pk *S, const orc_params *p,
+                     const orc_operator *op, const double *x, int fd, orc_csr *A);
+void orc_pk_initial_state(const orc_mesh *m, const orc_pk *S, const orc_params *p,
+                          const double *phi_pb, double *x0);
+void orc_pk_ion_flux(const orc_mesh *m, const orc_pk *S, const orc_params *p, const double *x,
+                     double *ip, double *im);
 
 #ifdef __cplusplus
 }

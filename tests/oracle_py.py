@@ -45,6 +45,11 @@ class OrcOperator(C.Structure):
                 ("x_old", C.c_void_p)]
 
 
+class OrcPk(C.Structure):
+    _fields_ = [("k", C.c_int), ("nl", C.c_int), ("nn", C.c_int), ("nedge", C.c_int),
+                ("xy", C.POINTER(C.c_double)), ("enode", C.POINTER(C.c_int))]
+
+
 class OrcSolveResult(C.Structure):
     _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("it_half", C.c_double),
                 ("reduction", C.c_double), ("defect0", C.c_double), ("defect", C.c_double),
@@ -67,8 +72,10 @@ def lib():
     global _LIB
     if _LIB is None:
         so = os.path.join(ORACLE_DIR, "liboracle.so")
-        src = os.path.join(ORACLE_DIR, "pnp_oracle.c")
-        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("pnp_oracle.c", "pnp_oracle_pk.c",
+                                                       "pnp_oracle.h")]
+        if not os.path.exists(so) or any(os.path.getmtime(so) < os.path.getmtime(f)
+                                         for f in srcs):
             subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         _LIB = C.CDLL(so)
         _LIB.orc_operator_nfields.restype = C.c_int
@@ -226,6 +233,90 @@ class Problem:
         lib().orc_newton(C.byref(self.m), C.byref(self.p), C.byref(op), _p(u), C.byref(o),
                          C.byref(res))
         return u, res
+
+
+class PkSpace:
+    """The oracle's own Lagrange P_k space on a Problem's mesh (pnp_oracle_pk.c) and the scalar
+    operators of the operator-split driver on it.  Vectors are over the space's nn nodes."""
+
+    def __init__(self, prob: Problem, k):
+        self.prob, self.k = prob, int(k)
+        self.S = OrcPk()
+        rc = lib().orc_pk_build(C.byref(prob.m), self.k, C.byref(self.S))
+        assert rc == 0, rc
+        self.nn, self.nl = self.S.nn, self.S.nl
+        self.xy = np.ctypeslib.as_array(self.S.xy, shape=(self.nn, 2)).copy()
+        self.enode = np.ctypeslib.as_array(self.S.enode, shape=(prob.mesh.nt, self.nl)).copy()
+
+    def __del__(self):
+        try:
+            lib().orc_pk_free(C.byref(self.S))
+        except Exception:
+            pass
+
+    def mask(self, field=0):
+        out = np.zeros(self.nn, dtype=np.uint8)
+        lib().orc_pk_dirichlet_mask(C.byref(self.prob.m), C.byref(self.S), C.byref(self.prob.p),
+                                    int(field), _p(out))
+        return out
+
+    def residual(self, op, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        r = np.zeros(self.nn)
+        lib().orc_pk_residual(C.byref(self.prob.m), C.byref(self.S), C.byref(self.prob.p),
+                              C.byref(op), _p(x), _p(r))
+        return r
+
+    def jacobian(self, op, x, fd=False):
+        import scipy.sparse as sp
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        A = OrcCsr()
+        L = lib()
+        L.orc_pk_csr_pattern(C.byref(self.prob.m), C.byref(self.S), C.byref(A))
+        L.orc_pk_jacobian(C.byref(self.prob.m), C.byref(self.S), C.byref(self.prob.p),
+                          C.byref(op), _p(x), int(fd), C.byref(A))
+        n, nnz = A.n, A.nnz
+        rp = np.ctypeslib.as_array(A.rowptr, shape=(n + 1,)).copy()
+        col = np.ctypeslib.as_array(A.col, shape=(nnz,)).copy()
+        val = np.ctypeslib.as_array(A.val, shape=(nnz,)).copy()
+        L.orc_csr_free(C.byref(A))
+        return sp.csr_matrix((val, col, rp), shape=(n, n))
+
+    def initial_state(self, phi_pb):
+        out = np.zeros(3 * self.nn)
+        phi = None if phi_pb is None else np.ascontiguousarray(phi_pb, dtype=np.float64)
+        lib().orc_pk_initial_state(C.byref(self.prob.m), C.byref(self.S), C.byref(self.prob.p),
+                                   _p(phi), _p(out))
+        return out
+
+    def ion_flux(self, x):
+        n = self.prob.p.nsurf
+        ip, im = np.zeros(n), np.zeros(n)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        lib().orc_pk_ion_flux(C.byref(self.prob.m), C.byref(self.S), C.byref(self.prob.p), _p(x),
+                              _p(ip), _p(im))
+        return ip, im
+
+    def basis(self, xi, eta):
+        phi = np.zeros(self.nl)
+        dphi = np.zeros((self.nl, 2))
+        lib().orc_pk_basis(self.k, C.c_double(xi), C.c_double(eta), _p(phi), _p(dphi))
+        return phi, dphi
+
+    def newton(self, op, u, reduction=1e-10, maxit=30):
+        """Plain Newton with exact sparse solves on the oracle's residual / analytic Jacobian
+        (PB on P_k: PDELab's line search never shortens a step on these problems)."""
+        import scipy.sparse.linalg as spla
+        u = np.array(u, dtype=np.float64)
+        r = self.residual(op, u)
+        d0 = np.linalg.norm(r)
+        for _ in range(maxit):
+            if np.linalg.norm(r) <= reduction * d0 or np.linalg.norm(r) < 1e-14:
+                break
+            J = self.jacobian(op, u)
+            u -= spla.spsolve(J.tocsc(), r)
+            r = self.residual(op, u)
+        return u
 
 
 def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
