@@ -10,6 +10,8 @@
 //                 [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec ...] [--amg-smoother s]
 //                 [--device d] [--out prefix]
 //                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]
+//                 [--degree k]   (md / pb modes: PDEGREE, src/instationary_pnp_from_pb_md.hh:26-28;
+//                                 the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111)
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
 #include <algorithm>
@@ -43,7 +45,7 @@ static void usage() {
       "                [--amg-smoother ssor|ilu0|jacobi]\n"
       "                [--out prefix] [--md-reduction r]\n"
       "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
-      "                [--abs-limit a] [--dump-steps n1,n2,...]\n");
+      "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -167,7 +169,7 @@ int main(int argc, char **argv) {
   }
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
   std::string amg_smoother;  // empty: SSOR for the PB phase, ILU(0) for the PNP phases
-  int refine = 0, steps = -1, device = -1;
+  int refine = 0, steps = -1, device = -1, degree = 1;
   double mesh_scale = 1.0;  // size scale when the mesh comes from a .geo (gmsh -clscale)
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
   // Newton absolute limit (PDELab NewtonTerminate abs_limit, default 1e-12 as in PDELab); the
@@ -194,6 +196,7 @@ int main(int argc, char **argv) {
     else if (a == "--md-reduction") md_reduction = std::atof(next().c_str());
     else if (a == "--linear-solver") linsolver = next();
     else if (a == "--abs-limit") abs_limit = std::atof(next().c_str());
+    else if (a == "--degree") degree = std::atoi(next().c_str());
     else if (a == "--dump-steps") {
       std::string l = next();
       for (size_t p = 0; p < l.size();) {
@@ -233,11 +236,15 @@ int main(int argc, char **argv) {
       }
       comm.rccl_unique_id = uid.data();
     }
-    pnp_gpu::Context ctx(mesh, params, device, world > 1 ? &comm : nullptr);
-    int nv = mesh.nv();
+    if (degree != 1 && mode != "md" && mode != "pb")  // PnpOperator is P1 in the reference
+      throw pnp_gpu::Error(PNP_E_ARG, "--degree applies to the md and pb modes (the stationary "
+                                      "and instationary drivers are P1: src/stationary_pnp_from_pb.hh:206-208)");
+    pnp_gpu::Context ctx(mesh, params, device, world > 1 ? &comm : nullptr, degree);
+    int nv = ctx.nv();  // DOF nodes of the P_degree space
     if (rank == 0)
-      std::printf("mesh %s refined %d: %d vertices, config %s (%s)\n", s.cfg.meshfile, refine, nv,
-                  cfgfile.c_str(), s.cfg.cylindrical ? "cylindrical" : "planar");
+      std::printf("mesh %s refined %d: %d vertices, P%d: %d nodes, config %s (%s)\n",
+                  s.cfg.meshfile, refine, mesh.nv(), degree, nv, cfgfile.c_str(),
+                  s.cfg.cylindrical ? "cylindrical" : "planar");
 
     // ---- PB (src/stationary_pnp_from_pb.hh:105-185): pbu = 0, Newton, BCGS_SSORk ----------
     pnp_gpu::Operator pblop(PNP_OP_PB);

@@ -105,11 +105,15 @@ struct Sysparams {
 // ---- one GPU (one rank) ------------------------------------------------------------------------
 class Context {
  public:
+  // degree: the GridFunctionSpace's Pk2DLocalFiniteElementMap degree (PDEGREE); vectors are over
+  // its nv() Lagrange nodes (the mesh vertices for degree 1)
   Context(const Mesh &mesh, const pnp_params &params, int device = 0,
-          const pnp_comm *comm = nullptr) {
-    int rc = pnp_create(&mesh.view(), &params, device, comm, &ctx_);
+          const pnp_comm *comm = nullptr, int degree = 1) {
+    int rc = pnp_create_pk(&mesh.view(), &params, degree, device, comm, &ctx_);
     check(rc);
-    nv_ = mesh.nv();
+    pnp_info info{};
+    check(pnp_get_info(ctx_, &info), ctx_);
+    nv_ = info.nv_global;
   }
   ~Context() { pnp_destroy(ctx_); }
   Context(const Context &) = delete;

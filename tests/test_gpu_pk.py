@@ -268,3 +268,89 @@ def test_pk3_indefinite_systems_behave_like_the_oracle():
     assert res["converged"] == 1
     assert np.abs(z - zo[perm]).max() <= 1e-8 * np.abs(zo).max()
     ctx.close()
+
+
+def _md_oracle_pk(S, orc, cfg, x0, nsteps):
+    """the _md time loop (src/instationary_pnp_from_pb_md.hh:411-454) on the oracle's P_k
+    operators with exact sparse solves (as test_gpu.py's P1 loop)"""
+    s = cfg.system
+    nn = S.nn
+    phi, cp, cm = x0[:nn].copy(), x0[nn:2 * nn].copy(), x0[2 * nn:].copy()
+    a, dt = 1.0 - 0.5 * np.sqrt(2.0), s["tau"]
+    upd, outf = max(1, int(s["potentialUpdateFreq"])), max(1, int(s["outputFreq"]))
+
+    def solve(op, x, extra=None):
+        r = S.residual(op, x) + (0 if extra is None else extra)
+        return x - spla.spsolve(S.jacobian(op, x).tocsc(), r)
+
+    def poisson(phi, cp, cm):
+        op = orc.operator(O.OP_POISSON, flux=orc.flux(), mask=S.mask(0),
+                          cp=np.ascontiguousarray(cp), cm=np.ascontiguousarray(cm))
+        return solve(op, phi)
+
+    def alexander2(c, z, field, phi):
+        mask = S.mask(field)
+        u0 = np.ascontiguousarray(c)
+        op1 = orc.operator(O.OP_DIFF_IE, mask=mask, dt=a * dt, z=z, phi=np.ascontiguousarray(phi),
+                           x_old=u0)
+        u1 = solve(op1, u0.copy())
+        opr = orc.operator(O.OP_DIFF, mask=mask, z=z, phi=np.ascontiguousarray(phi))
+        r1 = (1.0 - a) * dt * S.residual(opr, u1)
+        r1[mask != 0] = 0.0  # c_extra: constrained rows stay 0
+        return solve(op1, u1, r1)
+
+    t, fluxes = 0.0, []
+    for i in range(nsteps):
+        cp = alexander2(cp, +1.0, 1, phi)
+        cm = alexander2(cm, -1.0, 2, phi)
+        t += dt
+        if i % upd == 0:
+            phi = poisson(phi, cp, cm)
+        if i % outf == 0:
+            fluxes.append((t, S.ion_flux(np.concatenate([phi, cp, cm]))))
+    phi = poisson(phi, cp, cm)
+    return np.concatenate([phi, cp, cm]), fluxes
+
+
+def test_pk_md_driver_matches_oracle_loop(tmp_path):
+    """pnp_main --degree 2 (the reference's dune_pnp_BCGS_SSORk_2 program): the PB Newton on P2
+    (--mode pb) vs the oracle's P2 PB Newton, the Boltzmann initial state interpolated at the P2
+    nodes, and the operator-split loop (--mode md, 11 steps, reductions 1e-12) vs the oracle's
+    loop with exact solves: final phi / c+ / c- and the current.dat lines."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    pre = str(tmp_path / "md2")
+    out = subprocess.run([exe, cfgp, "--mode", "pb", "--degree", "2", "--out", pre],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    mesh, ctx, orc, S, perm = spaces("cylinder", 2)
+    pb = np.loadtxt(pre + "_pb.dat")
+    pbo = S.newton(orc.operator(O.OP_PB, flux=orc.flux(), mask=S.mask(0)), np.zeros(S.nn),
+                   reduction=1e-12)
+    # the driver's Newton stops at the config's reduction: compare at that accuracy
+    assert np.abs(pb - pbo[perm]).max() <= 1e-6 * np.abs(pbo).max()
+    out = subprocess.run([exe, cfgp, "--mode", "md", "--degree", "2", "--steps", "11",
+                          "--md-reduction", "1e-12", "--out", pre],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    nn = S.nn
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(nn)
+    to_orc = lambda v: np.concatenate([v[f * nn:(f + 1) * nn][inv] for f in range(3)])
+    x0 = to_orc(np.loadtxt(pre + "_x0.dat").T.ravel())
+    np.testing.assert_array_equal(x0, S.initial_state(pb[inv]))
+    u_drv = to_orc(np.loadtxt(pre + "_pnp.dat").T.ravel())
+    cur = np.atleast_2d(np.loadtxt(pre + "_current.dat"))
+    cfg = P.read_config(cfgp)
+    u_orc, fluxes = _md_oracle_pk(S, orc, cfg, x0, 11)
+    for f in range(3):
+        ref = u_orc[f * nn:(f + 1) * nn]
+        assert np.abs(u_drv[f * nn:(f + 1) * nn] - ref).max() <= 1e-8 * max(np.abs(ref).max(), 1e-30)
+    assert cur.shape[0] == len(fluxes)
+    for row, (t, (ip, im)) in zip(cur, fluxes):
+        assert row[0] == pytest.approx(t)
+        got = row[1:].reshape(-1, 4)
+        scale = max(np.abs(ip).max(), np.abs(im).max(), 1e-30)
+        assert np.abs(got[:, 0] - ip).max() <= 1e-8 * scale
+        assert np.abs(got[:, 2] - im).max() <= 1e-8 * scale
