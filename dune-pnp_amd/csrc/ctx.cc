@@ -101,9 +101,8 @@ struct pnp_ctx {
   pnp::Mesh mesh, tmesh;
   pnp::PkSpace pks;
   pnp::PkDev pkd;
-  DBuf<int> pk_enode, pk_vdata, pk_cdata;
-  DBuf<long long> pk_vptr, pk_rptr;
-  DBuf<double> pk_rel, pk_jel;
+  DBuf<int> pk_enode, pk_ioff, pk_icnt, pk_inc;
+  DBuf<uint32_t> pk_islot;
   pnp::Params params;
   pnp::Fans fans;
   pnp::LocalLayout L;
@@ -565,11 +564,11 @@ struct pnp_ctx {
   }
 
   // P_k element lists (once per context): the local elements (every element with an owned node,
-  // ascending global id), their local nodes (SoA), and per owned row the residual codes and, per
-  // SELL slot, the element-matrix codes summed into that block, in ascending element order
+  // ascending global id) and their local nodes (SoA); per owned row its incident elements in
+  // ascending order, in SELL-chunk layout (PkDev), with the row's slot of every element node
   int pk_build() {
     const pnp::Mesh &m = tmesh;
-    const int nl = pks.nl;
+    const int nl = pks.nl, nw = (nl + 3) / 4;
     std::vector<int> en;
     std::vector<int> elist;
     for (int e = 0; e < m.nt; e++) {
@@ -585,81 +584,62 @@ struct pnp_ctx {
       elist.push_back(e);
     }
     const int ne = int(elist.size());
-    if ((long long)ne * nl * nl >= (1LL << 31)) return fail(PNP_E_MESH, "P_k: too many local elements");
+    if (ne >= (1 << 27)) return fail(PNP_E_MESH, "P_k: too many local elements");
     en.resize(size_t(ne) * nl);
     for (int e = 0; e < ne; e++)
       for (int a = 0; a < nl; a++) en[size_t(a) * ne + e] = L.g2l[pks.enode[size_t(elist[e]) * nl + a]];
-    auto pos_of = [&](int row, int col) -> long long {
+    auto slot_of = [&](int row, int col) -> int {
       const int ch = row / pnp::kRows, ln = row % pnp::kRows, len = pnp::meta_len(L.rowmeta[row]);
-      if (col == row) return L.chunk_off[ch] + ln;
-      for (int sl = 1; sl < len; sl++) {
-        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
-        if (L.colidx[p] == col) return p;
-      }
+      if (col == row) return 0;
+      for (int sl = 1; sl < len; sl++)
+        if (L.colidx[L.chunk_off[ch] + 64LL * sl + ln] == col) return sl;
       return -1;
     };
-    std::vector<long long> vptr(L.n_owned + 1, 0);
-    std::vector<int> cnt(size_t(L.nslots) + 1, 0);
+    // incidences per owned row, ascending element order
+    std::vector<int> icnt(L.n_owned, 0);
+    for (int e = 0; e < ne; e++)
+      for (int a = 0; a < nl; a++) {
+        const int ra = en[size_t(a) * ne + e];
+        if (ra < L.n_owned) icnt[ra]++;
+      }
+    std::vector<int> ioff(L.nchunks + 1, 0);
+    for (int c = 0; c < L.nchunks; c++) {
+      int mx = 0;
+      for (int ln = 0; ln < pnp::kRows && c * pnp::kRows + ln < L.n_owned; ln++)
+        mx = std::max(mx, icnt[c * pnp::kRows + ln]);
+      ioff[c + 1] = ioff[c] + pnp::kRows * mx;
+    }
+    std::vector<int> inc(std::max(1, ioff[L.nchunks]), 0), fill(L.n_owned, 0);
+    std::vector<uint32_t> islot(size_t(std::max(1, ioff[L.nchunks])) * nw, 0);
     for (int e = 0; e < ne; e++)
       for (int a = 0; a < nl; a++) {
         const int ra = en[size_t(a) * ne + e];
         if (ra >= L.n_owned) continue;
-        vptr[ra + 1]++;
+        const int c = ra / pnp::kRows, ln = ra % pnp::kRows;
+        const size_t p = size_t(ioff[c]) + size_t(pnp::kRows) * fill[ra]++ + ln;
+        inc[p] = e << 4 | a;
         for (int b = 0; b < nl; b++) {
-          const long long p = pos_of(ra, en[size_t(b) * ne + e]);
-          if (p < 0) return fail(PNP_E_MESH, "P_k: element pair outside the pattern");
-          cnt[p]++;
+          const int sl = slot_of(ra, en[size_t(b) * ne + e]);
+          if (sl < 0) return fail(PNP_E_MESH, "P_k: element pair outside the pattern");
+          islot[p * nw + (b >> 2)] |= uint32_t(sl) << (8 * (b & 3));
         }
       }
-    for (int i = 0; i < L.n_owned; i++) vptr[i + 1] += vptr[i];
-    std::vector<int> vdata((size_t)vptr[L.n_owned]);
-    std::vector<long long> rptr(L.n_owned + 1, 0);
-    for (int i = 0; i < L.n_owned; i++) {
-      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
-      long long n = 0;
-      for (int sl = 0; sl < len; sl++) n += 1 + cnt[L.chunk_off[ch] + 64LL * sl + ln];
-      rptr[i + 1] = rptr[i] + n;
-    }
-    std::vector<long long> at((size_t)L.nslots, -1LL), vat(vptr.begin(), vptr.end() - 1);
-    std::vector<int> data((size_t)rptr[L.n_owned]);
-    for (int i = 0; i < L.n_owned; i++) {
-      const int ch = i / pnp::kRows, ln = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
-      long long q = rptr[i];
-      for (int sl = 0; sl < len; sl++) {
-        const long long p = L.chunk_off[ch] + 64LL * sl + ln;
-        data[q] = cnt[p];
-        at[p] = q + 1;
-        q += 1 + cnt[p];
-      }
-    }
-    for (int e = 0; e < ne; e++)
-      for (int a = 0; a < nl; a++) {
-        const int ra = en[size_t(a) * ne + e];
-        if (ra >= L.n_owned) continue;
-        vdata[vat[ra]++] = a * ne + e;
-        for (int b = 0; b < nl; b++)
-          data[at[pos_of(ra, en[size_t(b) * ne + e])]++] = (a * nl + b) * ne + e;
-      }
     int rc;
-    if ((rc = upv(pk_enode, en, "P_k elements")) || (rc = upv(pk_vptr, vptr, "P_k vptr")) ||
-        (rc = upv(pk_vdata, vdata, "P_k residual codes")) || (rc = upv(pk_rptr, rptr, "P_k rptr")) ||
-        (rc = upv(pk_cdata, data, "P_k matrix codes")))
+    if ((rc = upv(pk_enode, en, "P_k elements")) || (rc = upv(pk_ioff, ioff, "P_k ioff")) ||
+        (rc = upv(pk_icnt, icnt, "P_k icnt")) || (rc = upv(pk_inc, inc, "P_k incidences")) ||
+        (rc = upv(pk_islot, islot, "P_k slots")))
       return rc;
-    hipError_t e = pk_rel.alloc(std::max<size_t>(1, size_t(ne) * nl));
-    if (e == hipSuccess) e = pk_jel.alloc(std::max<size_t>(1, size_t(ne) * nl * nl));
-    if (e == hipSuccess) e = pnp::pk_upload_tables(pks.k, stream);
+    hipError_t e = pnp::pk_upload_tables(pks.k, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    if (e != hipSuccess) return hipfail(e, "P_k scratch");
+    if (e != hipSuccess) return hipfail(e, "P_k tables");
     pkd.k = pks.k;
     pkd.nl = nl;
     pkd.ne = ne;
     pkd.enode = pk_enode.p;
-    pkd.vptr = pk_vptr.p;
-    pkd.vdata = pk_vdata.p;
-    pkd.rptr = pk_rptr.p;
-    pkd.cdata = pk_cdata.p;
-    pkd.rel = pk_rel.p;
-    pkd.jel = pk_jel.p;
+    pkd.ioff = pk_ioff.p;
+    pkd.icnt = pk_icnt.p;
+    pkd.inc = pk_inc.p;
+    pkd.islot = pk_islot.p;
     // ion-flux segments handled by this rank: those whose element is local and whose lower
     // global vertex is owned here, {local element, face, group}, in global segment order
     std::vector<int> eloc(m.nt, -1);

@@ -387,15 +387,14 @@ hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_
 
 // ---- P_k (k = 2, 3) scalar operators (pk_assemble.hip, pk.h) ----------------------------------
 // ne local elements (every element with an owned node; its nodes are all local), enode[a * ne + e]
-// the local node of local node a; per owned row: vdata[vptr[i] .. vptr[i+1]) the residual codes
-// a * ne + e, and cdata from rptr[i] for each slot the count then the codes (a * nl + b) * ne + e
-// into the element matrices; rel / jel the element scratch
+// the local node of local node a.  Per owned row i (SELL chunk c, lane l): icnt[i] incident
+// elements, the t-th at position p = ioff[c] + 64 t + l: inc[p] = e << 4 | (local index of i in
+// e), islot[p * NW + w] the SELL slots (bytes) of the element's nl nodes in row i, NW = ceil(nl/4)
 struct PkDev {
   int k = 1, nl = 3, ne = 0;
   const int *enode = nullptr;
-  const long long *vptr = nullptr, *rptr = nullptr;
-  const int *vdata = nullptr, *cdata = nullptr;
-  double *rel = nullptr, *jel = nullptr;
+  const int *ioff = nullptr, *icnt = nullptr, *inc = nullptr;
+  const uint32_t *islot = nullptr;
 };
 hipError_t pk_upload_tables(int k, hipStream_t s);
 // jac 0 residual, 1 analytic Jacobian, 2 forward-difference Jacobian (PNP_JAC_FD)

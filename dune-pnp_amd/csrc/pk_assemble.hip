@@ -6,17 +6,15 @@
 // (PB / Poisson 3, Diffusion 2 -- the default of its constructor, :36 --, DiffusionT 5, the
 // `cptop(5)` of src/instationary_pnp_from_pb_md.hh:363).
 //
-// Two launches, no atomics, deterministic:
-//   k_pk_element  one thread per local element: the element residual (nl values) and the element
-//                 matrix (nl x nl; analytic, or PDELab's forward differences for PNP_JAC_FD) into
-//                 SoA scratch rel[a][e], jel[a*nl+b][e] (coalesced stores across the wave);
-//   k_pk_gather   one thread per owned node row (SELL lane order): the row's residual and every
-//                 SELL block summed from its element contributions in ascending element order
-//                 (the order PDELab's element loop accumulates them), blocks stored slot by slot,
-//                 i.e. one coalesced 512-byte line per slot and wave.
-// The P1 path keeps its fan-walk kernels (assemble.hip); the element work of P_k is small next to
-// its matrix traffic (P2: 36, P3: 100 entries per element) and the two-pass form keeps every
-// store whole-line and every sum in a fixed order.
+// One launch, owner-computes, no atomics, deterministic (k_pk_row): one thread per owned node
+// row walks the elements that contain its node (ascending element order, the order PDELab's
+// element loop accumulates them) and computes only its own row of each element's residual and
+// matrix, adding the matrix row into its SELL slots in place.  The row's slots stay in L2 while
+// they accumulate, so each is written to HBM once, and no element matrix is ever stored.
+// Measured at pore_pnp k=3 (profiles/r02/bench_pk_*.log): a first two-pass form (element matrices
+// into SoA scratch, then a per-slot gather of their codes) took 506 us (P2) / 1574 us (P3) per
+// Poisson assembly, 80 % of it in the latency-bound gather of 28 / 100 scattered values per
+// element.  The P1 path keeps its fan-walk kernels (assemble.hip).
 #include <cmath>
 #include <vector>
 
@@ -99,79 +97,6 @@ __device__ __forceinline__ double factor(const PkGeo &G, const PkPoint<NL> &P, i
   return f;
 }
 
-// element residual rl[NL] (zeroed here) of the operator at local values xl; f0 / f1 the frozen
-// fields (DIFF: phi; POISSON: c+, c-)
-template <int K>
-__device__ void pk_residual(const PkGeo &G, const PkArgs &a, const double *xl, const double *f0,
-                            const double *f1, double *rl) {
-  constexpr int NL = PkK<K>::NL;
-  const auto &T = tab<K>();
-  const double PI = a.pi;
-#pragma unroll
-  for (int i = 0; i < NL; i++) rl[i] = 0.0;
-  if (a.mass || a.kind == OP_DIFF_IE) {  // DiffusionTOperator, order 5, u * phi_i
-    for (int q = 0; q < 7; q++) {
-      const auto &P = T.q5[q];
-      double u = 0.0;
-#pragma unroll
-      for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
-      const double f = P.w * G.adet;
-#pragma unroll
-      for (int i = 0; i < NL; i++) rl[i] += u * P.phi[i] * f;
-    }
-    if (a.mass) return;
-  }
-  if (a.kind == OP_PB || a.kind == OP_POISSON) {  // order 3 (src/pb_operator.hh:114-120,
-    for (int q = 0; q < 4; q++) {                 //  src/poisson_operator.hh:119-125)
-      const auto &P = T.q3[q];
-      const double f = factor(G, P, a.cyl, PI);
-      double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
-#pragma unroll
-      for (int i = 0; i < NL; i++) {
-        double g0, g1;
-        grad(G, P, i, g0, g1);
-        u += xl[i] * P.phi[i];
-        gu0 += xl[i] * g0;
-        gu1 += xl[i] * g1;
-        if (a.kind == OP_POISSON) {
-          cp += f0[i] * P.phi[i];
-          cm += f1[i] * P.phi[i];
-        }
-      }
-      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
-#pragma unroll
-      for (int i = 0; i < NL; i++) {
-        double g0, g1;
-        grad(G, P, i, g0, g1);
-        rl[i] += (gu0 * g0 + gu1 * g1 + s * P.phi[i]) * f;
-      }
-    }
-  } else {  // OP_DIFF / OP_DIFF_IE: order 2, no cylindrical weight (Q8), grad of the frozen phi
-    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
-    for (int q = 0; q < 3; q++) {
-      const auto &P = T.q2[q];
-      double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < NL; i++) {
-        double g0, g1;
-        grad(G, P, i, g0, g1);
-        u += xl[i] * P.phi[i];
-        gu0 += xl[i] * g0;
-        gu1 += xl[i] * g1;
-        gP0 += f0[i] * g0;
-        gP1 += f0[i] * g1;
-      }
-      const double f = P.w * G.adet;
-#pragma unroll
-      for (int i = 0; i < NL; i++) {  // src/diffusion_operator.hh:109-110, a = 0
-        double g0, g1;
-        grad(G, P, i, g0, g1);
-        rl[i] += sc * ((gu0 * g0 + gu1 * g1 + u * a.z * (gP0 * g0 + gP1 * g1) + 0.0 * u * P.phi[i]) * f);
-      }
-    }
-  }
-}
-
 // analytic element matrix row a: J[a][b] = d rl[a] / d xl[b]
 template <int K>
 __device__ void pk_jac_row(const PkGeo &G, const PkArgs &a, int ra, const double *xl,
@@ -234,88 +159,154 @@ __device__ void pk_jac_row(const PkGeo &G, const PkArgs &a, int ra, const double
   }
 }
 
-// JAC 0: residual only, 1: analytic Jacobian, 2: forward differences (NumericalJacobianVolume,
-// eps 1e-7 (1 + |x_j|))
-template <int K, int JAC>
-__global__ __launch_bounds__(kB) void k_pk_element(int ne, const int *__restrict__ enode,
-                                                   const double *__restrict__ xy,
-                                                   const double *__restrict__ x,
-                                                   const double *__restrict__ aux0,
-                                                   const double *__restrict__ aux1, PkArgs a,
-                                                   double *__restrict__ rel,
-                                                   double *__restrict__ jel) {
+// residual of local row ra of the element (the reference's element loop restricted to one test
+// function; same statements, so the same value as that row of pk_residual)
+template <int K>
+__device__ double pk_row_residual(const PkGeo &G, const PkArgs &a, int ra, const double *xl,
+                                  const double *f0, const double *f1) {
   constexpr int NL = PkK<K>::NL;
-  const int e = blockIdx.x * kB + threadIdx.x;
-  if (e >= ne) return;
-  int nd[NL];
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+  double r = 0.0;
+  if (a.mass || a.kind == OP_DIFF_IE) {
+    for (int q = 0; q < 7; q++) {
+      const auto &P = T.q5[q];
+      double u = 0.0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) nd[i] = enode[size_t(i) * ne + e];
-  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
-  const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
-  double xl[NL], f0[NL], f1[NL], rl[NL];
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    xl[i] = x[nd[i]];
-    f0[i] = aux0 ? aux0[nd[i]] : 0.0;
-    f1[i] = aux1 ? aux1[nd[i]] : 0.0;
-  }
-  pk_residual<K>(G, a, xl, f0, f1, rl);
-#pragma unroll
-  for (int i = 0; i < NL; i++) rel[size_t(i) * ne + e] = rl[i];
-  if constexpr (JAC == 1) {
-    for (int r = 0; r < NL; r++) {
-      double Jr[NL];
-      pk_jac_row<K>(G, a, r, xl, f0, Jr);
-#pragma unroll
-      for (int b = 0; b < NL; b++) jel[size_t(r * NL + b) * ne + e] = Jr[b];
+      for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+      const double f = P.w * G.adet;
+      r += u * P.phi[ra] * f;
     }
-  } else if constexpr (JAC == 2) {
-    for (int j = 0; j < NL; j++) {
-      double up[NL];
-      const double xj = xl[j], delta = 1e-7 * (1.0 + fabs(xj));
-      xl[j] = xj + delta;
-      pk_residual<K>(G, a, xl, f0, f1, up);
-      xl[j] = xj;
-#pragma unroll
-      for (int i = 0; i < NL; i++) jel[size_t(i * NL + j) * ne + e] = (up[i] - rl[i]) / delta;
-    }
+    if (a.mass) return r;
   }
-}
-
-// residual rows: mode 0 r = (dmask ? 0 : cvec + sum), mode 1 cvec -= sum (old-time mass)
-__global__ __launch_bounds__(kB) void k_pk_gather_res(int n, const long long *__restrict__ vptr,
-                                                      const int *__restrict__ vdata,
-                                                      const double *__restrict__ rel, int mode,
-                                                      const uint8_t *__restrict__ dmask,
-                                                      double *__restrict__ cvec,
-                                                      double *__restrict__ r) {
-  const int row = blockIdx.x * kB + threadIdx.x;
-  if (row >= n) return;
-  double s = 0.0;
-  for (long long p = vptr[row]; p < vptr[row + 1]; p++) s += rel[vdata[p]];
-  if (mode == 1) {
-    cvec[row] -= s;
+  if (a.kind == OP_PB || a.kind == OP_POISSON) {
+    for (int q = 0; q < 4; q++) {
+      const auto &P = T.q3[q];
+      const double f = factor(G, P, a.cyl, PI);
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g0;
+        gu1 += xl[i] * g1;
+        if (a.kind == OP_POISSON) {
+          cp += f0[i] * P.phi[i];
+          cm += f1[i] * P.phi[i];
+        }
+      }
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+      double g0, g1;
+      grad(G, P, ra, g0, g1);
+      r += (gu0 * g0 + gu1 * g1 + s * P.phi[ra]) * f;
+    }
   } else {
-    const double rv = s + cvec[row];
-    r[row] = dmask[row] != 0 ? 0.0 : rv;
+    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+    for (int q = 0; q < 3; q++) {
+      const auto &P = T.q2[q];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        double g0, g1;
+        grad(G, P, i, g0, g1);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g0;
+        gu1 += xl[i] * g1;
+        gP0 += f0[i] * g0;
+        gP1 += f0[i] * g1;
+      }
+      const double f = P.w * G.adet;
+      double g0, g1;
+      grad(G, P, ra, g0, g1);
+      r += sc * ((gu0 * g0 + gu1 * g1 + u * a.z * (gP0 * g0 + gP1 * g1) + 0.0 * u * P.phi[ra]) * f);
+    }
   }
+  return r;
 }
 
-// SELL blocks of the owned rows: cdata per row, for each slot the count then the codes into jel
-__global__ __launch_bounds__(kB) void k_pk_gather_jac(DevLayout L, const long long *__restrict__ rptr,
-                                                      const int *__restrict__ cdata,
-                                                      const double *__restrict__ jel,
-                                                      double *__restrict__ vals) {
-  const int row = blockIdx.x * kB + threadIdx.x;
+// One thread per owned node row (SELL lane order), owner-computes like the P1 fan walk: the row
+// walks its incident elements (inc: element << 4 | local index of the row), computes its own row
+// of each element's residual and matrix (JAC 0 residual only, 1 analytic, 2 PDELab forward
+// differences eps 1e-7 (1 + |x_j|)), and adds the matrix row into its slots (islot: the slot of
+// each element node in this row, packed bytes).  The slots accumulate in LDS (acc[s][thread], the
+// thread's own column: no atomics, no barrier) and are stored once at the end, slot by slot, i.e.
+// one coalesced 512-byte line per slot and wave.  The next incidence's code is fetched before
+// the current one is computed.  mode 1 (old-time mass): cvec -= M(x) instead.
+template <int K, int JAC>
+__global__ __launch_bounds__(kB) void k_pk_row(DevLayout L, PkDev D, const double *__restrict__ x,
+                                               const double *__restrict__ aux0,
+                                               const double *__restrict__ aux1, PkArgs a, int mode,
+                                               const double *__restrict__ cvec_in,
+                                               const uint8_t *__restrict__ dmask,
+                                               double *__restrict__ r, double *__restrict__ cvec_out,
+                                               double *__restrict__ vals) {
+  constexpr int NL = PkK<K>::NL, NW = (NL + 3) / 4;
+  extern __shared__ double acc[];  // [max_slots][kB]
+  const int row = row_block(L, blockIdx.x, gridDim.x) * kB + threadIdx.x;
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = L.chunk_off[chunk], len = int(L.rowmeta[row] & 63);
-  long long p = rptr[row];
-  for (int s = 0; s < len; s++) {
-    double acc = 0.0;
-    const int n = cdata[p++];
-    for (int k = 0; k < n; k++) acc += jel[cdata[p++]];
-    __builtin_nontemporal_store(acc, vals + size_t(off) + size_t(s) * kRows + lane);
+  double *arow = acc + threadIdx.x;
+  if constexpr (JAC != 0)
+    for (int s = 0; s < len; s++) arow[s * kB] = 0.0;
+  const int ne = D.ne, cnt = D.icnt[row];
+  const int ib = D.ioff[chunk] + lane;
+  const double2 *xy2 = reinterpret_cast<const double2 *>(L.xy);
+  double R = 0.0;
+  int code_next = cnt > 0 ? D.inc[ib] : 0;
+  for (int t = 0; t < cnt; t++) {
+    const int p = ib + t * kRows;
+    const int code = code_next;
+    const int e = code >> 4, ra = code & 15;
+    int nd[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
+    if (t + 1 < cnt) code_next = D.inc[p + kRows];
+    uint32_t sw[NW];
+    if constexpr (JAC != 0) {
+#pragma unroll
+      for (int w = 0; w < NW; w++) sw[w] = D.islot[size_t(p) * NW + w];
+    }
+    const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
+    double xl[NL], f0[NL], f1[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+      xl[i] = x[nd[i]];
+      f0[i] = aux0 ? aux0[nd[i]] : 0.0;
+      f1[i] = aux1 ? aux1[nd[i]] : 0.0;
+    }
+    const double r0 = pk_row_residual<K>(G, a, ra, xl, f0, f1);
+    R += r0;
+    if constexpr (JAC != 0) {
+      double Jr[NL];
+      if constexpr (JAC == 1) {
+        pk_jac_row<K>(G, a, ra, xl, f0, Jr);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+          const double xj = xl[j], delta = 1e-7 * (1.0 + fabs(xj));
+          xl[j] = xj + delta;
+          Jr[j] = (pk_row_residual<K>(G, a, ra, xl, f0, f1) - r0) / delta;
+          xl[j] = xj;
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < NL; b++) {
+        const int s = (sw[b >> 2] >> (8 * (b & 3))) & 0xff;
+        arow[s * kB] += Jr[b];
+      }
+    }
+  }
+  if constexpr (JAC != 0) {
+    double *vrow = vals + size_t(off) + lane;
+    for (int s = 0; s < len; s++) __builtin_nontemporal_store(arow[s * kB], vrow + size_t(s) * kRows);
+  }
+  if (mode == 1) {
+    cvec_out[row] -= R;
+  } else {
+    const double rv = R + cvec_in[row];
+    r[row] = dmask[row] != 0 ? 0.0 : rv;
   }
 }
 
@@ -427,18 +418,36 @@ hipError_t upload_tab(hipStream_t s) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_tab3), &T, sizeof T, 0, hipMemcpyHostToDevice, s);
 }
 
-template <int K>
-hipError_t element_launch(int ne, const int *enode, const double *xy, const double *x,
-                          const double *aux0, const double *aux1, const PkArgs &a, int jac,
-                          double *rel, double *jel, hipStream_t s) {
-  const dim3 g((ne + kB - 1) / kB), b(kB);
-  if (jac == 0)
-    hipLaunchKernelGGL((k_pk_element<K, 0>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
-  else if (jac == 1)
-    hipLaunchKernelGGL((k_pk_element<K, 1>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
-  else
-    hipLaunchKernelGGL((k_pk_element<K, 2>), g, b, 0, s, ne, enode, xy, x, aux0, aux1, a, rel, jel);
+template <int K, int JAC>
+hipError_t row_launch1(const DevLayout &L, const PkDev &D, const double *x, const double *aux0,
+                       const double *aux1, const PkArgs &a, int mode, const double *cvec_in,
+                       const uint8_t *dmask, double *r, double *cvec_out, double *vals,
+                       hipStream_t s) {
+  const size_t lds = JAC ? size_t(L.max_slots) * kB * sizeof(double) : 0;
+  static bool attr = false;  // up to 160 KB of LDS per workgroup on gfx950 (P3: 55 slots)
+  if (JAC && !attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pk_row<K, JAC>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int nwg = (L.n_owned + kB - 1) / kB;
+  hipLaunchKernelGGL((k_pk_row<K, JAC>), dim3(nwg), dim3(kB), lds, s, L, D, x, aux0, aux1, a,
+                     mode, cvec_in, dmask, r, cvec_out, vals);
   return hipGetLastError();
+}
+
+template <int K>
+hipError_t row_launch(const DevLayout &L, const PkDev &D, const double *x, const double *aux0,
+                      const double *aux1, const PkArgs &a, int jac, int mode, const double *cvec_in,
+                      const uint8_t *dmask, double *r, double *cvec_out, double *vals,
+                      hipStream_t s) {
+  if (jac == 0)
+    return row_launch1<K, 0>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
+  if (jac == 1)
+    return row_launch1<K, 1>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
+  return row_launch1<K, 2>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
 }
 
 }  // namespace
@@ -452,39 +461,25 @@ hipError_t pk_upload_tables(int k, hipStream_t s) {
 hipError_t launch_pk_assemble(const DevLayout &L, const AsmArgs &aa, const PkDev &P, int jac,
                               hipStream_t s) {
   if (P.k != 2 && P.k != 3) return hipErrorInvalidValue;
+  if (L.n_owned == 0) return hipSuccess;
   const bool diff = aa.kind == OP_DIFF || aa.kind == OP_DIFF_IE;
   const double *f0 = (diff || aa.kind == OP_POISSON) ? aa.aux0 : nullptr;
   const double *f1 = aa.kind == OP_POISSON ? aa.aux1 : nullptr;
   PkArgs a{aa.kind, aa.cylindrical, 0, aa.l_b, aa.c0, aa.pi, aa.dt, aa.z};
-  hipError_t e = hipSuccess;
-  if (P.ne > 0) {
-    e = P.k == 2 ? element_launch<2>(P.ne, P.enode, L.xy, aa.x, f0, f1, a, jac, P.rel, P.jel, s)
-                 : element_launch<3>(P.ne, P.enode, L.xy, aa.x, f0, f1, a, jac, P.rel, P.jel, s);
-    if (e != hipSuccess) return e;
-  }
-  if (L.n_owned == 0) return hipSuccess;
-  const dim3 gr((L.n_owned + kB - 1) / kB), b(kB);
-  hipLaunchKernelGGL(k_pk_gather_res, gr, b, 0, s, L.n_owned, P.vptr, P.vdata, P.rel, 0, aa.dmask,
-                     const_cast<double *>(aa.cvec), aa.r);
-  if (jac) hipLaunchKernelGGL(k_pk_gather_jac, gr, b, 0, s, L, P.rptr, P.cdata, P.jel, aa.vals);
-  return hipGetLastError();
+  return P.k == 2 ? row_launch<2>(L, P, aa.x, f0, f1, a, jac, 0, aa.cvec, aa.dmask, aa.r, nullptr,
+                                  aa.vals, s)
+                  : row_launch<3>(L, P, aa.x, f0, f1, a, jac, 0, aa.cvec, aa.dmask, aa.r, nullptr,
+                                  aa.vals, s);
 }
 
 hipError_t launch_pk_mass_apply(const DevLayout &L, const PkDev &P, const double *x_old,
                                 double *cvec, hipStream_t s) {
-  PkArgs a{OP_DIFF_IE, 0, 1, 0, 0, 0, 0, 0};
-  hipError_t e = hipSuccess;
-  if (P.ne > 0) {
-    e = P.k == 2 ? element_launch<2>(P.ne, P.enode, L.xy, x_old, nullptr, nullptr, a, 0, P.rel,
-                                     nullptr, s)
-                 : element_launch<3>(P.ne, P.enode, L.xy, x_old, nullptr, nullptr, a, 0, P.rel,
-                                     nullptr, s);
-    if (e != hipSuccess) return e;
-  }
   if (L.n_owned == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pk_gather_res, dim3((L.n_owned + kB - 1) / kB), dim3(kB), 0, s, L.n_owned,
-                     P.vptr, P.vdata, P.rel, 1, nullptr, cvec, nullptr);
-  return hipGetLastError();
+  PkArgs a{OP_DIFF_IE, 0, 1, 0, 0, 0, 0, 0};
+  return P.k == 2 ? row_launch<2>(L, P, x_old, nullptr, nullptr, a, 0, 1, nullptr, nullptr,
+                                  nullptr, cvec, nullptr, s)
+                  : row_launch<3>(L, P, x_old, nullptr, nullptr, a, 0, 1, nullptr, nullptr,
+                                  nullptr, cvec, nullptr, s);
 }
 
 hipError_t launch_pk_ion_flux(const DevLayout &L, const PkDev &P, int ns, const int4 *seg,
