@@ -1497,7 +1497,8 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       int len = int(L.rowmeta[row] & 63), nl = 0, nu = 1;
       for (int sl = 1; sl < len; sl++) {
         int j = L.colidx[size_t(L.chunk_off[ch]) + 64 * sl + ln];
-        if (j >= L.n_owned || j == row) continue;
+        // ghost and same-colour columns are outside the sweeps (mesh.cc absorb_top)
+        if (j >= L.n_owned || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
         (j < row ? nl : nu)++;
       }
       ml = std::max(ml, nl);
@@ -1521,7 +1522,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       for (int sl = 1; sl < len; sl++) {
         int pos = L.chunk_off[ch] + 64 * sl + ln;
         int j = L.colidx[pos];
-        if (j >= L.n_owned || j == row) continue;
+        if (j >= L.n_owned || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
         if (j < row) {
           lcol[size_t(lco[ch]) + 64 * kl + ln] = j;
           lsrc[size_t(lco[ch]) + 64 * kl + ln] = row << 6 | sl;
@@ -1779,6 +1780,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->uslots = (int64_t)c->d_usrc.n;
   info->ilu_f32 = c->ilu_f32;
   info->degree = c->degree;
+  info->color_conflicts = c->L.conflicts;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->b.n + c->prevu.n + c->ext.n) * 8;

@@ -377,6 +377,16 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
 // Rows of one colour never couple, so each colour is one parallel launch: the rows it needs
 // (lower neighbours) were factorised by earlier launches.  Entry (f,g) of slot t of row i is
 // lu[(off_c + 64 t) * NV + 64 pat(f,g) + lane].
+// Same-colour couplings (mesh.cc absorb_top: a thin top colour merged into the colours below) are
+// outside the sweeps' pattern: the split storage has no slot for them and the factorisation
+// neither eliminates by them nor updates into them
+__device__ __forceinline__ bool same_color(const DevLayout &L, int a, int b) {
+  return L.rowcolor[a] == L.rowcolor[b];
+}
+__device__ __forceinline__ bool dropped(const DevLayout &L, int row, int col) {
+  return col != row && col < L.n_owned && same_color(L, row, col);
+}
+
 template <int NF, int PAT>
 __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int r1,
                                                         double *__restrict__ lu) {
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
     int j = 0x7fffffff, s = -1;
     for (int t = 1; t < leni; t++) {
       const int c = cixi[t * kRows];
-      if (c < row && c > prev && c < j) {
+      if (c < row && c > prev && c < j && !same_color(L, c, row)) {
         j = c;
         s = t;
       }
@@ -425,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
         for (int t = 0; t < leni; t++) {
           const int m = cixi[t * kRows];
           if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;  // padding -> m == row
+          if (dropped(L, row, m) || dropped(L, j, m)) continue;
           for (int u = 1; u < lenj; u++) {
             if (cixj[u * kRows] != m) continue;
             for (int h = 0; h < NF; h++)
@@ -526,7 +537,7 @@ __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, i
     int j = 0x7fffffff, s = -1;
     for (int t = 1; t < leni; t++) {
       const int c = cixi[t];
-      if (c < row && c > prev && c < j) {
+      if (c < row && c > prev && c < j && !same_color(L, c, row)) {
         j = c;
         s = t;
       }
@@ -558,6 +569,7 @@ __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, i
     for (int t = 0; t < leni; t++) {
       const int m = cixi[t];
       if (m <= j || m >= L.n_owned || (t > 0 && m == row)) continue;
+      if (dropped(L, row, m) || dropped(L, j, m)) continue;
       int u = 1;
       while (u < lenj && cixj[u] != m) u++;
       if (u == lenj) continue;
@@ -626,7 +638,7 @@ __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, i
   int kl = 0, ku = 1;
   for (int t = 1; t < leni; t++) {
     const int c = cixi[t];
-    if (c >= L.n_owned || c == row) continue;
+    if (c >= L.n_owned || c == row || same_color(L, c, row)) continue;
     double B[NV];
     ld(vi, t, B);
     if (c < row)

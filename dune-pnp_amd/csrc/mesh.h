@@ -115,6 +115,7 @@ struct LocalLayout {
                                    // 31 = absent
   long long nslots = 0;            // total SELL slots incl. padding
   long long nblocks = 0;           // real blocks (V+2E restricted to owned rows)
+  long long conflicts = 0;         // owned neighbour pairs of one colour (left out of the sweeps)
   // halo: per neighbour rank q, ghosts [ghost_ptr[q], ghost_ptr[q+1]) (offsets into ghosts) are
   // received from q; send_idx[send_ptr[q] .. send_ptr[q+1]) are local owned rows sent to q
   std::vector<int> nbr_ranks;

@@ -91,7 +91,8 @@ class _Info(C.Structure):
                 ("max_slots", C.c_int32), ("nranks", C.c_int32), ("nblocks", C.c_int64),
                 ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
                 ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
-                ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32)]
+                ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32),
+                ("color_conflicts", C.c_int64)]
 
 
 class _SpaceInfo(C.Structure):

@@ -163,6 +163,8 @@ typedef struct {
   int64_t lslots, uslots;/* slots of the strictly-lower / diagonal+upper split storage */
   int32_t ilu_f32;       /* PNP_OPT_ILU_F32 */
   int32_t degree;        /* polynomial degree of the space (pnp_create_pk); nv_global = its nodes */
+  int64_t color_conflicts; /* owned neighbour pairs sharing a colour: couplings the multicolour
+                              sweeps (SSOR, ILU(0)) leave out, see DESIGN.md §3 */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 
