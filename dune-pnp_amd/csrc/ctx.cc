@@ -2643,6 +2643,7 @@ extern "C" int pnp_layout_view(const pnp_layout_buf *b, pnp_layout *v) {
   v->recv_ptr = L.recv_ptr.data();
   v->send_ptr = L.send_ptr.data();
   v->send_idx = L.send_idx.data();
+  v->color_conflicts = L.conflicts;
   return PNP_OK;
 }
 

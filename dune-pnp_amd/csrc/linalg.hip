@@ -19,6 +19,11 @@
 
 #include "kernels.h"
 
+// split sweeps: issue a batch's L/U value loads with its column-index loads (1) or after them (0)
+#ifndef SPLIT_VALS_EARLY
+#define SPLIT_VALS_EARLY 1
+#endif
+
 namespace pnp {
 
 namespace {
@@ -279,6 +284,18 @@ __device__ __forceinline__ void split_row_dot(const SplitRow<VT> &R, int s0, int
       j[b] = s < R.len ? R.cix[s * kRows] : row;  // (non-temporal here: slower, reused)
     }
     double vj[B][NF], a[B][NV];
+    // values first: they depend on the slot count only, so they are in flight with the column
+    // indices instead of waiting for them (padding slots are zeroed after the loads)
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int s = sb + b * LPR;
+      if (SPLIT_VALS_EARLY && s < R.len) {
+        load_split_vals<NV, NT>(R.vc + size_t(s) * NS * kRows, R.lane, a[b]);
+      } else {
+#pragma unroll
+        for (int qq = 0; qq < NV; qq++) a[b][qq] = 0.0;
+      }
+    }
 #pragma unroll
     for (int b = 0; b < B; b++) {
       const int s = sb + b * LPR;
@@ -288,9 +305,8 @@ __device__ __forceinline__ void split_row_dot(const SplitRow<VT> &R, int s0, int
 #pragma unroll
         for (int g = 0; g < NF; g++) vj[b][g] = 0.0;
       }
-      if (use) {
-        load_split_vals<NV, NT>(R.vc + size_t(s) * NS * kRows, R.lane, a[b]);
-      } else {
+      if (!SPLIT_VALS_EARLY && use) load_split_vals<NV, NT>(R.vc + size_t(s) * NS * kRows, R.lane, a[b]);
+      if (SPLIT_VALS_EARLY && !use) {
 #pragma unroll
         for (int qq = 0; qq < NV; qq++) a[b][qq] = 0.0;
       }

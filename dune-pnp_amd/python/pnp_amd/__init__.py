@@ -164,7 +164,8 @@ class _Layout(C.Structure):
                 ("chunk_len", C.POINTER(C.c_int32)), ("chunk_off", C.POINTER(C.c_int32)),
                 ("colidx", C.POINTER(C.c_int32)), ("rowmeta", C.POINTER(C.c_uint64)),
                 ("nbr_ranks", C.POINTER(C.c_int32)), ("recv_ptr", C.POINTER(C.c_int32)),
-                ("send_ptr", C.POINTER(C.c_int32)), ("send_idx", C.POINTER(C.c_int32))]
+                ("send_ptr", C.POINTER(C.c_int32)), ("send_idx", C.POINTER(C.c_int32)),
+                ("color_conflicts", C.c_int64)]
 
 
 _LIB = None
@@ -391,6 +392,7 @@ class Layout:
         self.recv_ptr = arr(v.recv_ptr, v.nnbr + 1)
         self.send_ptr = arr(v.send_ptr, v.nnbr + 1)
         self.send_idx = arr(v.send_idx, int(self.send_ptr[-1]) if v.nnbr else 0)
+        self.color_conflicts = int(v.color_conflicts)
         lib().pnp_layout_free(buf)
 
     def row_len(self, i):

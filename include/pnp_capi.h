@@ -439,6 +439,8 @@ typedef struct {
   const int32_t *recv_ptr;     /* nnbr + 1: ghost ranges received from each neighbour */
   const int32_t *send_ptr;     /* nnbr + 1 */
   const int32_t *send_idx;     /* local owned rows sent to each neighbour */
+  int64_t color_conflicts;     /* owned neighbour pairs sharing a colour (absorbed thin top colour,
+                                  mesh.cc absorb_top); left out of the multicolour sweeps */
 } pnp_layout;
 /* the partition + local layout pnp_create would build for (rank, nranks) */
 int pnp_layout_build(const pnp_mesh *mesh, int32_t rank, int32_t nranks, pnp_layout_buf **out);
