@@ -38,6 +38,10 @@ struct DBuf {
     if (count == 0) return hipSuccess;
     hipError_t e = hipMalloc(&p, sizeof(T) * count);
     if (e == hipSuccess) e = hipMemset(p, 0, sizeof(T) * count);  // no reliance on fresh pages
+    // the memset runs on the null stream, which does not order against the context's
+    // non-blocking streams: finish it before a kernel there writes the buffer (seen as zeroed
+    // FD element matrices with 8 in-process ranks competing for the GPU)
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     return e;
   }
   void release() {
@@ -92,6 +96,10 @@ struct pnp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int rank = 0, nranks = 1;
+  // the multi-rank code path (reduce -> allreduce -> derive, halo-split SpMV, two-reduction
+  // BiCGSTAB): more than one rank, or one rank with an RCCL communicator of its own (a pnp_comm of
+  // size 1 with an RCCL id -- the N > 1 path on one GPU, every allreduce a real ncclAllReduce)
+  bool dist = false;
   ncclComm_t comm = nullptr;
   std::shared_ptr<LocalGroup> lg;  // test transport instead of RCCL
 
@@ -384,7 +392,7 @@ struct pnp_ctx {
 
   // in-place sum over ranks of k doubles in device memory
   int allreduce_dev(double *d, int k) {
-    if (nranks == 1) return PNP_OK;
+    if (!dist) return PNP_OK;
     if (lg) {
       std::vector<double> h(k);
       hipError_t e = hipMemcpyAsync(h.data(), d, sizeof(double) * k, hipMemcpyDeviceToHost, stream);
@@ -407,7 +415,7 @@ struct pnp_ctx {
   }
 
   int allreduce_red(int k) {
-    if (nranks == 1) return PNP_OK;
+    if (!dist) return PNP_OK;
     hipEvent_t t0 = tb(T_ALLRED);
     double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p) +
                                              offsetof(pnp::Scalars, red));
@@ -421,7 +429,7 @@ struct pnp_ctx {
   int reduce_derive(int np, int k, int stage, bool from2 = false) {
     hipError_t e;
     const double *src = from2 ? partials2.p : partials.p;
-    if (nranks == 1) {
+    if (!dist) {
       e = pnp::launch_reduce(src, np, k, S.p, stream, stage);
       return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
     }
@@ -436,7 +444,7 @@ struct pnp_ctx {
   // S->red[0..ka) = sum of partials (spmv), S->red[ka..) = sum of partials2, all ranks; derive
   int reduce_derive2(int npa, int ka, int npb, int kb, int stage) {
     hipError_t e;
-    if (nranks == 1) {
+    if (!dist) {
       e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream, stage);
       return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
     }
@@ -459,7 +467,7 @@ struct pnp_ctx {
     }
     if (e != hipSuccess) return hipfail(e, "norm");
     te(T_BLAS, t0);
-    if (nranks > 1) {
+    if (dist) {
       double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(S.p + 1) +
                                                offsetof(pnp::Scalars, red));
       int rc = allreduce_dev(red, 1);
@@ -1044,7 +1052,7 @@ struct pnp_ctx {
     // on by default with more than one rank, where each reduction is an allreduce round trip;
     // PNP_OPT_BICG_TWORED (or PNP_BICG_TWORED) 0/1 forces it off/on.  Half-step counts keep
     // ISTL's semantics.
-    const bool twored = twored_opt >= 0 ? twored_opt == 1 : nranks > 1;
+    const bool twored = twored_opt >= 0 ? twored_opt == 1 : dist;
     int pending_np = 0;
     for (int k = 0; k < maxit; k++) {
       // p = r + beta (p - omega v)
@@ -1461,7 +1469,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     g_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return PNP_E_HIP;
   }
-  if (c->nranks > 1 && comm->rccl_unique_id) {
+  if (comm && comm->rccl_unique_id && (c->nranks > 1 || comm->size == 1)) {
     ncclUniqueId id;
     std::memcpy(&id, comm->rccl_unique_id, sizeof id);
     ncclResult_t nr = ncclCommInitRank(&c->comm, c->nranks, id, c->rank);
@@ -1471,6 +1479,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       return PNP_E_RCCL;
     }
   }
+  c->dist = c->nranks > 1 || c->comm != nullptr;
   pnp::LocalLayout &L = c->L;
   int nloc = L.n_owned + L.n_ghost;
   std::vector<double> xy(2 * size_t(nloc));
@@ -1646,8 +1655,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
   // buffers
   size_t nv3 = 3 * size_t(nloc);
   auto al = [&](auto &buf, size_t n, const char *what) -> int {
-    hipError_t e2 = buf.alloc(n);
-    if (e2 == hipSuccess && n) e2 = hipMemset(buf.p, 0, sizeof(*buf.p) * n);
+    hipError_t e2 = buf.alloc(n);  // zeroed, and the zeroing finished (DBuf::alloc)
     if (e2 != hipSuccess) return cp->hipfail(e2, what);
     return PNP_OK;
   };
@@ -1682,7 +1690,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     g_err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return PNP_E_HIP;
   }
-  if (c->nranks > 1) {  // halo-overlapped SpMV: interior / boundary 256-row blocks
+  if (c->dist) {  // halo-overlapped SpMV: interior / boundary 256-row blocks
     const char *ev = getenv("PNP_HALO_OVERLAP");
     if (!(ev && atoi(ev) == 0) && L.n_owned > 0) {
       const int nblk = (L.n_owned + 255) / 256;
@@ -1781,6 +1789,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->ilu_f32 = c->ilu_f32;
   info->degree = c->degree;
   info->color_conflicts = c->L.conflicts;
+  info->transport = c->comm ? 2 : (c->lg ? 1 : 0);
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->b.n + c->prevu.n + c->ext.n) * 8;
@@ -2289,7 +2298,7 @@ extern "C" int pnp_ion_flux(pnp_ctx *c, const double *x, int32_t nsurf, double *
     acc[2 * size_t(g)] += out[2 * size_t(k)];
     acc[2 * size_t(g) + 1] += out[2 * size_t(k) + 1];
   }
-  if (c->nranks > 1 && nsurf > 0) {
+  if (c->dist && nsurf > 0) {
     CK(hipMemcpy(c->fluxred.p, acc.data(), sizeof(double) * acc.size(), hipMemcpyHostToDevice),
        "ion flux");
     if ((rc = c->allreduce_dev(c->fluxred.p, 2 * nsurf))) return rc;
@@ -2416,7 +2425,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
 
 extern "C" int pnp_sync_vector(pnp_ctx *c, double *v, int32_t nfields) {
   if (!c || !v || nfields < 1 || nfields > 3) return PNP_E_ARG;
-  if (c->nranks == 1) return PNP_OK;
+  if (!c->dist) return PNP_OK;
   hipSetDevice(c->device);
   size_t nv = size_t(c->mesh.nv), n = nv * nfields;
   std::vector<double> mine(n, 0.0);

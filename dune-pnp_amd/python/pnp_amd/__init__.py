@@ -92,7 +92,7 @@ class _Info(C.Structure):
                 ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
                 ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
                 ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32),
-                ("color_conflicts", C.c_int64)]
+                ("color_conflicts", C.c_int64), ("transport", C.c_int32)]
 
 
 class _SpaceInfo(C.Structure):

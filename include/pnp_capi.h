@@ -148,7 +148,8 @@ int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int32_t degree
 void pnp_destroy(pnp_ctx *ctx);
 /* message of the last failure on ctx (or of the last failed pnp_create / mesh call if ctx NULL) */
 const char *pnp_last_error(const pnp_ctx *ctx);
-/* fills a 128-byte buffer with a fresh RCCL unique id (rank 0 calls this, then broadcasts) */
+/* fills a 128-byte buffer with a fresh RCCL unique id (rank 0 calls this, then broadcasts); a
+   1-rank pnp_comm given one gets an RCCL communicator of its own (pnp_info.transport) */
 int pnp_rccl_unique_id(void *out128);
 
 typedef struct {
@@ -165,6 +166,9 @@ typedef struct {
   int32_t degree;        /* polynomial degree of the space (pnp_create_pk); nv_global = its nodes */
   int64_t color_conflicts; /* owned neighbour pairs sharing a colour: couplings the multicolour
                               sweeps (SSOR, ILU(0)) leave out, see DESIGN.md §3 */
+  int32_t transport;     /* 0 one rank, 1 in-process local group, 2 RCCL (also a 1-rank RCCL
+                            communicator: a pnp_comm of size 1 with an RCCL id runs the
+                            multi-rank code path, every reduction an ncclAllReduce) */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 

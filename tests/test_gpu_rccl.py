@@ -1,0 +1,77 @@
+"""The RCCL transport on hardware (-m gpu).  A GPU box here has one MI355X and RCCL refuses two
+ranks on one device, so the multi-rank tests (test_gpu_multirank.py) run the partition, halo and
+reductions through the in-process transport.  What they cannot show is that the RCCL calls
+themselves work inside the solver: this file creates contexts with a 1-rank RCCL communicator of
+their own (pnp_comm of size 1 with an RCCL unique id, pnp_info.transport == 2).  Such a context
+runs the multi-rank code path -- partials reduced, then ncclAllReduce on the context's stream,
+then the derive kernel; the halo-split SpMV with its second stream and events; the two-reduction
+BiCGSTAB; the ion-flux and sync_vector allreduces -- on one GPU.  A sum over one rank is a copy,
+so every result must equal the plain 1-rank context's (same reduction order inside the rank).
+The N > 1 byte movement (ncclSend / ncclRecv between GPUs) is left to the driver's 8-GPU run."""
+import os
+
+import numpy as np
+import pytest
+
+import pnp_amd as P
+from conftest import DATA
+from test_gpu import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def pair(mesh, par):
+    plain = P.Context(mesh, par, device=0)
+    rccl = P.Context(mesh, par, device=0, rank=0, size=1, unique_id=P.rccl_unique_id())
+    assert plain.info()["transport"] == 0 and rccl.info()["transport"] == 2
+    return plain, rccl
+
+
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_SSOR, P.PREC_ILU0, P.PREC_AMG])
+def test_rccl_linear_solve_equals_plain(prec):
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["newton_pnp_x0"]
+    out = []
+    for ctx in pair(mesh, par):
+        ctx.set_operator(P.OP_PNP)
+        # the same iteration on both sides: the two-reduction form is the RCCL context's default
+        ctx.set_option(P.OPT_BICG_TWORED, 1)
+        ctx.jacobian(x)
+        rhs = ctx.residual(x)
+        ctx.timers(enable=True, reset=True)
+        sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-8, maxit=20000)
+        t = ctx.timers(enable=False)
+        out.append((sol, res, t, rhs))
+        ctx.close()
+    (s0, r0, t0, b0), (s1, r1, t1, b1) = out
+    np.testing.assert_array_equal(b0, b1)
+    assert r0["converged"] == 1 and r1["converged"] == 1, (r0, r1)
+    assert r0["iterations"] == r1["iterations"], (r0, r1)
+    np.testing.assert_array_equal(s0, s1)
+    assert t0["allreduce_ms"] == 0.0 and t1["allreduce_ms"] > 0.0, (t0, t1)
+
+
+def test_rccl_pb_then_pnp_newton_and_ion_flux_equal_plain():
+    """The driver sequence (PB Newton -> BCExtension -> PNP Newton -> calcIonFlux) on
+    test/cylinder.msh refined once."""
+    cfg = P.read_config(os.path.join(DATA, "cylinder_config.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(1)
+    par = P.Params.from_config(cfg)
+    out = []
+    for ctx in pair(mesh, par):
+        ctx.set_option(P.OPT_BICG_TWORED, 1)
+        ctx.set_operator(P.OP_PB)
+        phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_SSOR)
+        phi = ctx.sync_vector(phi, 1)
+        x0 = ctx.initial_state(phi)
+        ctx.set_operator(P.OP_PNP)
+        u, res = ctx.newton(x0, prec=P.PREC_ILU0)
+        u = ctx.sync_vector(u)
+        out.append((u, res, rpb, ctx.ion_flux(u)))
+        ctx.close()
+    (u0, res0, pb0, f0), (u1, res1, pb1, f1) = out
+    assert pb0["converged"] == 1 and res0["converged"] == 1, (pb0, res0)
+    assert (pb0["linear_iterations"], res0["linear_iterations"]) == \
+        (pb1["linear_iterations"], res1["linear_iterations"])
+    np.testing.assert_array_equal(u0, u1)
+    np.testing.assert_array_equal(np.asarray(f0), np.asarray(f1))
