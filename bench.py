@@ -354,6 +354,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(1)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch only times the copy-rate calibration and syncs around the timed regions: bind it to
+    # this rank's GPU (its default is device 0, whatever LOCAL_RANK the library runs on)
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
