@@ -26,6 +26,9 @@ namespace pnp {
 namespace {
 
 constexpr int kB = 256;
+#ifndef PK_PIPE
+#define PK_PIPE 1  // A/B knob (build flag): element nodes one incidence ahead
+#endif
 
 template <int NL>
 struct PkPoint {
@@ -254,15 +257,35 @@ __global__ __launch_bounds__(kB) void k_pk_row(DevLayout L, PkDev D, const doubl
   const int ib = D.ioff[chunk] + lane;
   const double2 *xy2 = reinterpret_cast<const double2 *>(L.xy);
   double R = 0.0;
-  int code_next = cnt > 0 ? D.inc[ib] : 0;
+  // software pipeline over the incidences: the element nodes of incidence t+1 and the code of
+  // t+2 are in flight while t gathers and computes, so an incidence costs one dependent round
+  // trip (its node data), not three (code -> nodes -> data)
+  int code = cnt > 0 ? D.inc[ib] : 0;
+  int code_next = cnt > 1 ? D.inc[ib + kRows] : 0;
+  int nd_next[NL];
+  if (PK_PIPE) {
+#pragma unroll
+    for (int i = 0; i < NL; i++) nd_next[i] = cnt > 0 ? D.enode[size_t(i) * ne + (code >> 4)] : 0;
+  }
   for (int t = 0; t < cnt; t++) {
     const int p = ib + t * kRows;
-    const int code = code_next;
     const int e = code >> 4, ra = code & 15;
     int nd[NL];
+    if (PK_PIPE) {
 #pragma unroll
-    for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
-    if (t + 1 < cnt) code_next = D.inc[p + kRows];
+      for (int i = 0; i < NL; i++) nd[i] = nd_next[i];
+      if (t + 1 < cnt) {
+#pragma unroll
+        for (int i = 0; i < NL; i++) nd_next[i] = D.enode[size_t(i) * ne + (code_next >> 4)];
+      }
+      code = code_next;
+      if (t + 2 < cnt) code_next = D.inc[p + 2 * kRows];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
+      code = code_next;
+      if (t + 2 < cnt) code_next = D.inc[p + 2 * kRows];
+    }
     uint32_t sw[NW];
     if constexpr (JAC != 0) {
 #pragma unroll
