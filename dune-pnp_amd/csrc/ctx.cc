@@ -226,6 +226,7 @@ struct pnp_ctx {
   long long t_n[T_NCAT] = {0};
 
   ~pnp_ctx() {
+    graphs_clear();
     for (auto &v : ev_pending)
       for (auto &pr : v) {
         hipEventDestroy(pr.first);
@@ -239,6 +240,69 @@ struct pnp_ctx {
     if (ev_halo) hipEventDestroy(ev_halo);
     if (cstream) hipStreamDestroy(cstream);
     if (stream) hipStreamDestroy(stream);
+  }
+
+  // ---- hipGraph replay of BiCGSTAB iteration blocks (PNP_OPT_GRAPH) ------------------------------
+  // -1 auto: on for up to 131,072 owned rows (launch-bound sizes), 0 off, 1 on
+  int graph_opt = [] {
+    const char *e = std::getenv("PNP_GRAPH");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  bool use_graphs() const {
+    return graph_opt == 1 || (graph_opt < 0 && L.n_owned <= (1 << 17));
+  }
+  struct GraphKey {
+    int count, prec, fuse, nf, pat, f32;
+    const void *zout, *dmask;
+    long long epoch;
+    bool operator==(const GraphKey &o) const {
+      return count == o.count && prec == o.prec && fuse == o.fuse && nf == o.nf && pat == o.pat &&
+             f32 == o.f32 && zout == o.zout && dmask == o.dmask && epoch == o.epoch;
+    }
+  };
+  // kernel arguments captured in a graph stay valid while the buffers and the layout do: anything
+  // that changes an operator, an option or a buffer bumps the epoch
+  long long graph_epoch = 0;
+  struct GraphSlot {
+    GraphKey key;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<GraphSlot> graph_cache;
+  void graphs_clear() {
+    for (auto &g : graph_cache)
+      if (g.exec) hipGraphExecDestroy(g.exec);
+    graph_cache.clear();
+    graph_epoch++;
+  }
+  // replay the launches `issue` makes on the stream as a graph (captured on first use of `key`)
+  template <typename F>
+  int graph_run(const GraphKey &key, F &&issue) {
+    for (auto &g : graph_cache)
+      if (g.key == key) {
+        hipError_t e = hipGraphLaunch(g.exec, stream);
+        return e == hipSuccess ? PNP_OK : hipfail(e, "graph launch");
+      }
+    hipError_t e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return hipfail(e, "graph capture");
+    const int rc = issue();
+    hipGraph_t graph = nullptr;
+    hipError_t e2 = hipStreamEndCapture(stream, &graph);
+    if (rc) {
+      if (graph) hipGraphDestroy(graph);
+      return rc;
+    }
+    if (e2 != hipSuccess) return hipfail(e2, "graph capture");
+    hipGraphExec_t exec = nullptr;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    if (e != hipSuccess) return hipfail(e, "graph instantiate");
+    if (graph_cache.size() >= 8) {
+      hipGraphExecDestroy(graph_cache.front().exec);
+      graph_cache.erase(graph_cache.begin());
+    }
+    graph_cache.push_back({key, exec});
+    e = hipGraphLaunch(exec, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "graph launch");
   }
 
   int fail(int code, const std::string &msg) {
@@ -546,6 +610,7 @@ struct pnp_ctx {
   // analytic (k-form) or forward-difference (expanded, kPat*FD) storage of the next Jacobian
   int set_fd(bool on) {
     if (on == fd_mode) return PNP_OK;
+    graphs_clear();
     int rc;
     // P_k: the element kernel differentiates by itself; scalar blocks need no FD value layout
     if (on && !fd_built && degree == 1 && (rc = fd_build())) return rc;
@@ -1054,9 +1119,12 @@ struct pnp_ctx {
     // ISTL's semantics.
     const bool twored = twored_opt >= 0 ? twored_opt == 1 : dist;
     int pending_np = 0;
-    for (int k = 0; k < maxit; k++) {
+    // one BiCGSTAB iteration; for k >= 1 (and without the two-reduction variant's host state) it
+    // launches the same kernels with the same arguments every time, which is what the graph
+    // replay below relies on
+    auto body = [&](int k) -> int {
       // p = r + beta (p - omega v)
-      t0 = tb(T_BLAS);
+      hipEvent_t t0 = tb(T_BLAS);
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 0, k == 0 ? 1 : 0, nullptr, nullptr,
                                     rs.p, v.p, p.p, uvals.p, y.p, nullptr, nullptr, stream,
@@ -1131,12 +1199,36 @@ struct pnp_ctx {
                      k + 1, hS->it_half, hS->rho, hS->rho_new, hS->alpha, hS->omega, hS->h,
                      hS->norm, hS->done, hS->breakdown);
       }
-      if ((k + 1) % check == 0 || k + 1 == maxit) {
-        e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(stream);
-        if (e != hipSuccess) return hipfail(e, "bicgstab poll");
-        if (hS->done) break;
+      return PNP_OK;
+    };
+    // the iterations between two polls of the device scalars (every `check`): eagerly, or as one
+    // hipGraph replay (small systems, where launching ~20 kernels per iteration from the host
+    // costs more than running them: PNP_OPT_GRAPH)
+    const bool graphs = use_graphs() && !twored && !debug_trace && !timing &&
+                        prec != PNP_PREC_AMG;
+    for (int k = 0; k < maxit;) {
+      const int kend = std::min(maxit, (k / check + 1) * check);  // next poll
+      if (k == 0) {
+        if ((rc = body(0))) return rc;
+        k = 1;
       }
+      if (k < kend && graphs) {
+        const GraphKey key{kend - k, prec, fuse ? 1 : 0, nf, pat, f32_now(), zout, dl.dmask,
+                           graph_epoch};
+        if ((rc = graph_run(key, [&]() -> int {
+               for (int i = 0; i < key.count; i++)
+                 if (int r2 = body(1)) return r2;
+               return PNP_OK;
+             })))
+          return rc;
+        k = kend;
+      }
+      for (; k < kend; k++)
+        if ((rc = body(k))) return rc;
+      e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return hipfail(e, "bicgstab poll");
+      if (hS->done) break;
     }
     if (twored && pending_np > 0 && (rc = reduce_derive(pending_np, 1, 33, true))) return rc;
     e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
@@ -1805,6 +1897,8 @@ extern "C" int pnp_nfields(pnp_ctx *c) { return c ? c->nf : PNP_E_ARG; }
 
 extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   if (!c || !a) return PNP_E_ARG;
+  // no graphs_clear(): the operator's pattern and mask pointer are in the graph key, and nothing
+  // else a BiCGSTAB launch takes changes with the operator
   if (a->kind < PNP_OP_PNP || a->kind > PNP_OP_POISSON)
     return c->fail(PNP_E_ARG, "unknown operator kind");
   hipSetDevice(c->device);
@@ -2160,6 +2254,12 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
 
 extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
   if (!c) return PNP_E_ARG;
+  c->graphs_clear();
+  if (option == PNP_OPT_GRAPH) {
+    if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_GRAPH takes -1, 0 or 1");
+    c->graph_opt = int(value);
+    return PNP_OK;
+  }
   if (option == PNP_OPT_ILU_F32) {
     if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0 or 1");
     if (c->ilu_f32 != int(value)) {
@@ -2201,6 +2301,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_ILU_FUSED_FACTOR) {
     *value = c->ilu_fused;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_GRAPH) {
+    *value = c->graph_opt;
     return PNP_OK;
   }
   if (option == PNP_OPT_JAC_FD) {

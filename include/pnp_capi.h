@@ -346,7 +346,14 @@ enum {
    * divergence this guarded against came from a too-small coarsest level (<= 64 blocks): with
    * the default (<= 1024 blocks, exact dense solve) config 4 runs 100 steps without a failed
    * AMG solve (profiles/r02/amg_c4_*.log). */
-  PNP_OPT_AMG_FALLBACK = 5
+  PNP_OPT_AMG_FALLBACK = 5,
+  /* BiCGSTAB (pnp_linear_solve, pnp_newton, pnp_bicgstab_iterations) runs the iterations between
+   * two polls of its device-resident scalars as one hipGraph replay, captured on first use and
+   * kept until the operator or an option changes.  Same kernels, same arguments, same results;
+   * it saves the host's per-kernel launch cost where the kernels are shorter than it.  -1
+   * (default): on for contexts of up to 131,072 owned rows; 0 off; 1 on (the environment
+   * variable PNP_GRAPH=0/1 sets the default).  Not used with AMG, timers or more than one rank. */
+  PNP_OPT_GRAPH = 6
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
