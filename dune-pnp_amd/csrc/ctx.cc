@@ -1204,7 +1204,7 @@ struct pnp_ctx {
     // the iterations between two polls of the device scalars (every `check`): eagerly, or as one
     // hipGraph replay (small systems, where launching ~20 kernels per iteration from the host
     // costs more than running them: PNP_OPT_GRAPH)
-    const bool graphs = use_graphs() && !twored && !debug_trace && !timing &&
+    const bool graphs = use_graphs() && !dist && !twored && !debug_trace && !timing &&
                         prec != PNP_PREC_AMG;
     for (int k = 0; k < maxit;) {
       const int kend = std::min(maxit, (k / check + 1) * check);  // next poll
