@@ -29,6 +29,9 @@ constexpr int kB = 256;
 #ifndef PK_PIPE
 #define PK_PIPE 1  // A/B knob (build flag): element nodes one incidence ahead
 #endif
+#ifndef PK_FUSED
+#define PK_FUSED 1  // A/B knob (build flag): residual and Jacobian rows in one pass (pk_row_both)
+#endif
 
 template <int NL>
 struct PkPoint {
@@ -228,6 +231,85 @@ __device__ double pk_row_residual(const PkGeo &G, const PkArgs &a, int ra, const
   return r;
 }
 
+// pk_row_residual and pk_jac_row in one pass (JAC 1): the same statements, with each quadrature
+// point's physical basis gradients computed once and shared by the residual row and the Jacobian
+// row (the kernel is VALU-bound: profiles/r02/ab_pk_table_select.log).  Not for the mass-only mode.
+template <int K>
+__device__ void pk_row_both(const PkGeo &G, const PkArgs &a, int ra, const double *xl,
+                            const double *f0, const double *f1, double &r, double *Jr) {
+  constexpr int NL = PkK<K>::NL;
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+  r = 0.0;
+#pragma unroll
+  for (int b = 0; b < NL; b++) Jr[b] = 0.0;
+  if (a.kind == OP_DIFF_IE) {
+#pragma unroll 1
+    for (int q = 0; q < 7; q++) {
+      const auto &P = T.q5[q];
+      double u = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+      const double f = P.w * G.adet;
+      r += u * P.phi[ra] * f;
+#pragma unroll
+      for (int b = 0; b < NL; b++) Jr[b] += P.phi[ra] * P.phi[b] * f;
+    }
+  }
+  if (a.kind == OP_PB || a.kind == OP_POISSON) {
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) {
+      const auto &P = T.q3[q];
+      const double f = factor(G, P, a.cyl, PI);
+      double g[NL][2];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        grad(G, P, i, g[i][0], g[i][1]);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g[i][0];
+        gu1 += xl[i] * g[i][1];
+        if (a.kind == OP_POISSON) {
+          cp += f0[i] * P.phi[i];
+          cm += f1[i] * P.phi[i];
+        }
+      }
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+      const double c = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * cosh(u) * P.phi[ra] : 0.0;
+      double ga0, ga1;
+      grad(G, P, ra, ga0, ga1);
+      r += (gu0 * ga0 + gu1 * ga1 + s * P.phi[ra]) * f;
+#pragma unroll
+      for (int b = 0; b < NL; b++) Jr[b] += (ga0 * g[b][0] + ga1 * g[b][1] + c * P.phi[b]) * f;
+    }
+  } else {
+    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+#pragma unroll 1
+    for (int q = 0; q < 3; q++) {
+      const auto &P = T.q2[q];
+      double g[NL][2];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        grad(G, P, i, g[i][0], g[i][1]);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g[i][0];
+        gu1 += xl[i] * g[i][1];
+        gP0 += f0[i] * g[i][0];
+        gP1 += f0[i] * g[i][1];
+      }
+      const double f = P.w * G.adet;
+      double ga0, ga1;
+      grad(G, P, ra, ga0, ga1);
+      r += sc * ((gu0 * ga0 + gu1 * ga1 + u * a.z * (gP0 * ga0 + gP1 * ga1) + 0.0 * u * P.phi[ra]) * f);
+      const double drift = a.z * (gP0 * ga0 + gP1 * ga1);
+#pragma unroll
+      for (int b = 0; b < NL; b++)
+        Jr[b] += sc * ((ga0 * g[b][0] + ga1 * g[b][1] + P.phi[b] * drift) * f);
+    }
+  }
+}
+
 // One thread per owned node row (SELL lane order), owner-computes like the P1 fan walk: the row
 // walks its incident elements (inc: element << 4 | local index of the row), computes its own row
 // of each element's residual and matrix (JAC 0 residual only, 1 analytic, 2 PDELab forward
@@ -299,12 +381,16 @@ __global__ __launch_bounds__(kB) void k_pk_row(DevLayout L, PkDev D, const doubl
       f0[i] = aux0 ? aux0[nd[i]] : 0.0;
       f1[i] = aux1 ? aux1[nd[i]] : 0.0;
     }
-    const double r0 = pk_row_residual<K>(G, a, ra, xl, f0, f1);
+    double Jr[NL];
+    double r0;
+    if (JAC == 1 && PK_FUSED && !a.mass)
+      pk_row_both<K>(G, a, ra, xl, f0, f1, r0, Jr);
+    else
+      r0 = pk_row_residual<K>(G, a, ra, xl, f0, f1);
     R += r0;
     if constexpr (JAC != 0) {
-      double Jr[NL];
       if constexpr (JAC == 1) {
-        pk_jac_row<K>(G, a, ra, xl, f0, Jr);
+        if (!PK_FUSED || a.mass) pk_jac_row<K>(G, a, ra, xl, f0, Jr);
       } else {
 #pragma unroll
         for (int j = 0; j < NL; j++) {
