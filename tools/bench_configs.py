@@ -9,7 +9,7 @@ driver-level solve it stands for.  Prints one JSON object per config.
   config 5: PNP on test/pore_without_dna (the .geo meshed natively, size scale 0.85, refined
             k=6: ~10M DOF), PB -> PNP Newton, assembly + BiCGSTAB rates
   config 5f: the earlier fallback, test/pore_pnp refined k=5 (8.8M DOF)
-usage: python tools/bench_configs.py [1 2 4 4r 5 5f]"""
+usage: python tools/bench_configs.py [1 2 4 4r 5 5x 5f]"""
 import json
 import os
 import sys
@@ -153,14 +153,17 @@ def config4r(nsteps=100):
             "assembled_dofs_per_s": n / (r["assemble_us"] * 1e-6), **r}
 
 
-def config5():
-    """test/pore_without_dna: the .geo meshed here (size scale 0.85), refined k=6 -> ~10 M DOF."""
+def config5(refine=6):
+    """test/pore_without_dna: the .geo meshed here (size scale 0.85), refined k=6 -> ~10 M DOF
+    (refine 7, "5x": 35 M DOF on one GPU, the sizing check)."""
     cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
     t0 = time.perf_counter()
     base = P.Mesh.load(cfg.meshfile, size_scale=0.85)
     tmesh = time.perf_counter() - t0
-    mesh = base.refine(6)
+    mesh = base.refine(refine)
+    t0 = time.perf_counter()
     ctx = P.Context(mesh, P.Params.from_config(cfg))
+    t_setup = time.perf_counter() - t0
     phi, pbres, tpb = pb_then(ctx, mesh, prec=P.PREC_ILU0)
     x0 = ctx.initial_state(phi)
     ctx.set_operator(P.OP_PNP)
@@ -171,8 +174,10 @@ def config5():
     u, res = ctx.newton(x0, prec=pnp_prec(ctx), reduction=cfg.system["newtonReduction"],
                         min_linear_reduction=cfg.system["newtonMinLinearReduction"])
     t_pnp = time.perf_counter() - t0
-    return {"config": "5 (pore_without_dna.geo meshed natively, scale 0.85, k=6, one GPU)",
-            "base_vertices": base.nv, "mesher_s": tmesh, "dofs": n, "pb_newton_s": tpb,
+    return {"config": f"5{'x' if refine != 6 else ''} (pore_without_dna.geo meshed natively, "
+                      f"scale 0.85, k={refine}, one GPU)",
+            "base_vertices": base.nv, "mesher_s": tmesh, "context_setup_s": t_setup,
+            "device_bytes": ctx.info()["device_bytes"], "dofs": n, "pb_newton_s": tpb,
             "pb_converged": pbres["converged"], "pnp_newton_s": t_pnp,
             "pnp_newton_iterations": res["iterations"],
             "pnp_linear_iterations": res["linear_iterations"], "pnp_converged": res["converged"],
@@ -199,6 +204,6 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["1", "2", "4", "4r", "5"]
     for w in which:
         out = {"1": config1, "2": config2, "4": config4, "4r": config4r, "5": config5,
-               "5f": config5_fallback}[w]()
+               "5x": lambda: config5(7), "5f": config5_fallback}[w]()
         out["pnp_preconditioner"] = os.environ.get("PNP_BENCH_PREC", "ilu0")
         print(json.dumps(out), flush=True)
