@@ -119,6 +119,8 @@ struct pnp_ctx {
   DBuf<int> d_chunk_len, d_chunk_off, d_colidx, d_l2g, d_send_idx, d_color_idx;
   DBuf<uint8_t> d_rowcolor;
   DBuf<uint64_t> d_rowmeta;
+  DBuf<int> d_uptr, d_ulist;   // LDS-staged SpMV lists (PNP_SPMV_LDS, DevLayout::uptr)
+  DBuf<uint16_t> d_lidx;
   DBuf<double> d_xy;
 
   // operator
@@ -1741,6 +1743,48 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
   c->dl.chunk_off = c->d_chunk_off.p;
   c->dl.colidx = c->d_colidx.p;
   c->dl.rowmeta = c->d_rowmeta.p;
+  if (const char *ev = getenv("PNP_SPMV_LDS"); !(ev && atoi(ev) == 0)) {
+    // per 256-row block: its distinct columns, and per slot the column's position among them
+    const int nblk = (L.n_owned + 255) / 256;
+    std::vector<int> uptr(nblk + 1, 0), ulist;
+    std::vector<uint16_t> lidx(size_t(L.nslots), 0);
+    std::vector<int> cols;
+    int umax = 0;
+    bool fits = true;
+    for (int b = 0; b < nblk && fits; b++) {
+      cols.clear();
+      const int r1 = std::min(L.n_owned, 256 * b + 256);
+      for (int i = 256 * b; i < r1; i++) {
+        const int ch = i / pnp::kRows, ln = i % pnp::kRows;
+        for (int sl = 0; sl < L.chunk_len[ch]; sl++)
+          cols.push_back(L.colidx[size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln]);
+      }
+      std::sort(cols.begin(), cols.end());
+      cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+      if (cols.size() > 65535) fits = false;
+      umax = std::max(umax, int(cols.size()));
+      for (int i = 256 * b; i < r1; i++) {
+        const int ch = i / pnp::kRows, ln = i % pnp::kRows;
+        for (int sl = 0; sl < L.chunk_len[ch]; sl++) {
+          const size_t pos = size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln;
+          lidx[pos] = uint16_t(std::lower_bound(cols.begin(), cols.end(), L.colidx[pos]) - cols.begin());
+        }
+      }
+      ulist.insert(ulist.end(), cols.begin(), cols.end());
+      uptr[b + 1] = int(ulist.size());
+    }
+    if (fits && size_t(umax) * 3 * 8 <= 64 * 1024) {
+      if ((rc = up(c->d_uptr, uptr, "uptr")) || (rc = up(c->d_ulist, ulist, "ulist")) ||
+          (rc = up(c->d_lidx, lidx, "lidx"))) {
+        g_err = c->err;
+        return rc;
+      }
+      c->dl.uptr = c->d_uptr.p;
+      c->dl.ulist = c->d_ulist.p;
+      c->dl.lidx = c->d_lidx.p;
+      c->dl.umax = umax;
+    }
+  }
   c->dl.xy = c->d_xy.p;
   c->dl.color_idx = c->d_color_idx.p;
   c->dl.rowcolor = c->d_rowcolor.p;

@@ -231,6 +231,12 @@ struct DevLayout {
   const int *uchunk_len = nullptr, *uchunk_off = nullptr, *ucolidx = nullptr;
   // Dirichlet mask of the current operator, [n_owned * nf] (see mask_rows)
   const uint8_t *dmask = nullptr;
+  // LDS-staged SpMV (PNP_SPMV_LDS): per 256-row block the distinct columns its rows touch
+  // (ulist[uptr[b] .. uptr[b+1])), and per SELL slot the position of its column in that list
+  // (lidx, same indexing as colidx); umax = the longest list
+  const int *uptr = nullptr, *ulist = nullptr;
+  const uint16_t *lidx = nullptr;
+  int umax = 0;
 };
 
 template <int NF>

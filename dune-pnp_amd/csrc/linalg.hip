@@ -175,6 +175,116 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
   }
 }
 
+// The SpMV with the x gathers staged through LDS (PNP_SPMV_LDS): a workgroup first loads x at the
+// distinct columns of its 256 rows (config 3: 1,016 per block against 1,796 slots, so half the
+// scattered gathers), then every slot reads its x record from LDS by a 16-bit list position.
+// One lane per row, slots in batches of SB; the same products in the same order as k_spmv<.., 1>,
+// so the same result bits.
+template <int NF, int PAT, int MODE, int SB, int NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *__restrict__ vals,
+                                                     const double *__restrict__ x,
+                                                     double *__restrict__ y,
+                                                     const double *__restrict__ w,
+                                                     double *__restrict__ partials,
+                                                     const double *__restrict__ w2) {
+  constexpr int NV = popc9(PAT), NK = nks_of(PAT);
+  extern __shared__ double sx[];  // [cnt][NF]
+  const int blk = row_block(L, blockIdx.x, gridDim.x);
+  const int row = blk * kBlock + threadIdx.x;
+  const bool live = row < L.n_owned;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = live ? L.chunk_off[chunk] : 0, len = live ? L.chunk_len[chunk] : 0;
+  const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
+  for (int k = threadIdx.x; k < cnt; k += kBlock) {
+    double t[NF];
+    load_nf<NF>(x, size_t(L.ulist[u0 + k]), t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
+  }
+  __syncthreads();
+  double d[3] = {0, 0, 0};
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0;
+  const uint16_t *__restrict__ lix = L.lidx + off + lane;
+  const double *__restrict__ vc = vals + size_t(off) * NK;
+  for (int s0 = 0; s0 < len; s0 += SB) {
+    int li[SB];
+    double k[SB][NK];
+#pragma unroll
+    for (int b = 0; b < SB; b++) {
+      const int sl = s0 + b;
+      li[b] = sl < len ? lix[sl * kRows] : 0;
+      if (sl < len) {
+        if (NT)
+          load_vals_nt<NK>(vc + size_t(sl) * NK * kRows, lane, k[b]);
+        else
+          load_vals<NK>(vc + size_t(sl) * NK * kRows, lane, k[b]);
+      } else {
+#pragma unroll
+        for (int qq = 0; qq < NK; qq++) k[b][qq] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < SB; b++) {
+      double a[NV], xj[NF];
+#pragma unroll
+      for (int g = 0; g < NF; g++) xj[g] = sx[li[b] * NF + g];
+      expand_k<PAT>(k[b], a);
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int v = pat_index(PAT, f, g);
+          if (v >= 0) acc[f] += a[v] * xj[g];
+        }
+    }
+  }
+  if (live) {
+    const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
+    if (dm) {
+      double xr[NF];
+      load_nf<NF>(x, size_t(row), xr);
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+        if ((dm >> f) & 1) acc[f] = xr[f];
+    }
+    if constexpr (MODE == 3) {  // residual: y = w - A x
+      double wr[NF];
+      load_nf<NF>(w, size_t(row), wr);
+#pragma unroll
+      for (int f = 0; f < NF; f++) acc[f] = wr[f] - acc[f];
+    }
+    store_nf<NF>(y, size_t(row), acc);
+    if constexpr (MODE == 1 || MODE == 2 || MODE == 4) {
+      double wr[NF];
+      load_nf<NF>(w, size_t(row), wr);
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[0] += acc[f] * wr[f];
+    }
+    if constexpr (MODE == 2 || MODE == 4) {
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[1] += acc[f] * acc[f];
+    }
+    if constexpr (MODE == 4) {
+      double wr[NF];
+      load_nf<NF>(w2, size_t(row), wr);
+#pragma unroll
+      for (int f = 0; f < NF; f++) d[2] += acc[f] * wr[f];
+    }
+  }
+  if constexpr (MODE == 1) {
+    double v1[1] = {d[0]};
+    block_sum<1>(v1, partials + blockIdx.x);
+  } else if constexpr (MODE == 2) {
+    double v2[2] = {d[0], d[1]};
+    block_sum<2>(v2, partials + 2 * blockIdx.x);
+  } else if constexpr (MODE == 4) {
+    double v3[3] = {d[0], d[1], d[2]};
+    block_sum<3>(v3, partials + 3 * blockIdx.x);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // preconditioners
 // ------------------------------------------------------------------------------------------
@@ -1209,6 +1319,16 @@ static int spmv_batch() {
   }();
   return v;
 }
+// LDS-staged SpMV (k_spmv_lds, one lane per row) when the layout carries its lists (default;
+// PNP_SPMV_LDS=0: the direct-gather k_spmv).  Config 3: 57.6 -> 52.4 us per SpMV, BiCGSTAB
+// 338.7 -> 327.8 us/it, same result bits (profiles/r02/ab_spmv_lds.log)
+static bool spmv_lds() {
+  static const bool v = [] {
+    const char *e = std::getenv("PNP_SPMV_LDS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
 static int spmv_lpr() {
   static const int v = [] {
     const char *e = std::getenv("PNP_SPMV_LPR");
@@ -1216,6 +1336,7 @@ static int spmv_lpr() {
   }();
   return v;
 }
+static bool spmv_uses_lds(const DevLayout &L) { return spmv_lds() && L.uptr != nullptr; }
 // non-temporal loads of the matrix values (streamed once per launch; leaves L2 to the x
 // gathers): SpMV -2..3 %, and the following sweeps -1..2 % (profiles/r01/ab_spmv_nt.log);
 // PNP_SPMV_NT=0 turns it off (A/B)
@@ -1238,6 +1359,16 @@ static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double 
   hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc, NTc>), dim3(g.x * LPRc), dim3(kBlock), \
                      0, s, L, vals, x, y, w, partials, w2)
   const int b = spmv_batch(), l = spmv_lpr();
+  if (spmv_uses_lds(L)) {
+    const size_t lds = size_t(L.umax) * NF * sizeof(double);
+    if (b == 4)
+      hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 4, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
+                         w, partials, w2);
+    else
+      hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
+                         w, partials, w2);
+    return;
+  }
   if (spmv_nt() && l == 2 && b == 2) {
     PNP_SPMV_GO2(2, 2, 1);
     return;
@@ -1257,7 +1388,8 @@ static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double 
 #undef PNP_SPMV_GO2
 }
 
-int spmv_parts(int nrows) { return int(rows_grid(nrows).x) * spmv_lpr(); }
+// partials per SpMV launch at most (buffer sizing; launch_spmv returns the actual count)
+int spmv_parts(int nrows) { return int(rows_grid(nrows).x) * 2; }
 
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
@@ -1267,7 +1399,7 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
     return hipSuccess;
   }
   dim3 g = L.blkcount > 0 ? dim3(L.blkcount) : rows_grid(L.n_owned);
-  if (nparts) *nparts = int(g.x) * spmv_lpr();
+  if (nparts) *nparts = int(g.x) * (spmv_uses_lds(L) ? 1 : spmv_lpr());
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
