@@ -384,13 +384,41 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 // (profiles/r01/ab_asm_gather_all.log, ab_blkmap_gather_all.log, ab_asm_ga_split_blkmap.log).
 // SPLIT < FANR: only slots 1 .. SPLIT-1 are gathered up front; the rest are issued after element
 // SPLIT-2, when the first elements' neighbour registers are free again (fewer live VGPRs).
-template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR, int STAGE = 0>
+// LDSG: the fan neighbours' coordinates, dofs and frozen fields come from LDS, where the
+// workgroup first gathered them once per distinct column of its 256 rows (DevLayout::uptr /
+// ulist / lidx, as the LDS-staged SpMV): half the scattered gathers of the direct walk.
+template <int OP>
+__host__ __device__ constexpr int asm_lds_rec() {  // doubles per staged column
+  return 2 + OpTraits<OP>::NF + (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) +
+         (OP == OP_POISSON);
+}
+template <int OP, int JAC, int MINW, int FANR, int SPLIT = FANR, int STAGE = 0, int LDSG = 0>
 __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs a) {
   using T = OpTraits<OP>;
   constexpr int NF = T::NF, NK = T::NK, NS = FANR;
   constexpr bool AUX0 = OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON;
   constexpr bool AUX1 = OP == OP_POISSON;
-  const int row = row_block(L, blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  constexpr int RW = asm_lds_rec<OP>();
+  extern __shared__ double srec[];  // LDSG: [cnt][RW] = x, y, dofs, aux0, aux1
+  const int blk = row_block(L, blockIdx.x, gridDim.x);
+  const int row = blk * blockDim.x + threadIdx.x;
+  if constexpr (LDSG) {
+    const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+      const int j = L.ulist[u0 + k];
+      const double2 p = reinterpret_cast<const double2 *>(L.xy)[j];
+      double u[NF];
+      load_nf<NF>(a.x, size_t(j), u);
+      double *r = srec + size_t(k) * RW;
+      r[0] = p.x;
+      r[1] = p.y;
+#pragma unroll
+      for (int f = 0; f < NF; f++) r[2 + f] = u[f];
+      if constexpr (AUX0) r[2 + NF] = a.aux0[j];
+      if constexpr (AUX1) r[3 + NF] = a.aux1[j];
+    }
+    __syncthreads();
+  }
   if (row >= L.n_owned) return;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = L.chunk_off[chunk];
@@ -398,12 +426,18 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   const int len = int(meta & 63);
   const bool closed = (meta >> 6) & 1;
   const unsigned brk = unsigned(meta >> 8);  // fan-break bits, bit s: no element after slot s
-  const int *__restrict__ cix = L.colidx + off + lane;
   double *__restrict__ vc = a.vals + size_t(off) * NK;  // chunk base (k-form), see vin()
 
-  int cj[NS];
+  int cj[NS];  // the fan's columns (LDSG: their positions in the staged list)
+  if constexpr (LDSG) {
+    const uint16_t *__restrict__ lix = L.lidx + off + lane;
 #pragma unroll
-  for (int k = 1; k < NS; k++) cj[k] = cix[(k < len ? k : 0) * kRows];  // past the fan: the row
+    for (int k = 1; k < NS; k++) cj[k] = lix[(k < len ? k : 0) * kRows];
+  } else {
+    const int *__restrict__ cix = L.colidx + off + lane;
+#pragma unroll
+    for (int k = 1; k < NS; k++) cj[k] = cix[(k < len ? k : 0) * kRows];  // past the fan: the row
+  }
   const double2 pi2 = reinterpret_cast<const double2 *>(L.xy)[row];
   double ui[NF];
   load_nf<NF>(a.x, size_t(row), ui);
@@ -413,10 +447,19 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   double2 pn[NS];
   double un[NS][NF], a0[NS], a1[NS];
   auto gather = [&](int k) {
-    pn[k] = reinterpret_cast<const double2 *>(L.xy)[cj[k]];
-    load_nf<NF>(a.x, size_t(cj[k]), un[k]);
-    a0[k] = AUX0 ? a.aux0[cj[k]] : 0.0;
-    a1[k] = AUX1 ? a.aux1[cj[k]] : 0.0;
+    if constexpr (LDSG) {
+      const double *r = srec + size_t(cj[k]) * RW;
+      pn[k] = make_double2(r[0], r[1]);
+#pragma unroll
+      for (int f = 0; f < NF; f++) un[k][f] = r[2 + f];
+      a0[k] = AUX0 ? r[2 + NF] : 0.0;
+      a1[k] = AUX1 ? r[3 + NF] : 0.0;
+    } else {
+      pn[k] = reinterpret_cast<const double2 *>(L.xy)[cj[k]];
+      load_nf<NF>(a.x, size_t(cj[k]), un[k]);
+      a0[k] = AUX0 ? a.aux0[cj[k]] : 0.0;
+      a1[k] = AUX1 ? a.aux1[cj[k]] : 0.0;
+    }
   };
 #pragma unroll
   for (int k = 1; k < SPLIT; k++) gather(k);
@@ -625,12 +668,25 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
   // column indices in registers: FANR - 1 >= the longest fan (max_slots - 1; 8 on all meshes
   // seen), 12 as the general case, 0 (index loads in the walk) beyond
   const int fanr = !fanr_ok ? 0 : (L.max_slots <= 9 ? 9 : (L.max_slots <= 12 ? 12 : 0));
+  // LDS-staged neighbour data (A/B knob PNP_ASM_LDS=1), when the layout has the lists and a
+  // workgroup's records fit 53 KiB (3 workgroups per CU at the kernel's 3 waves per SIMD).
+  // Measured at config 3: warm 53.5 -> 57.6 us, cache-cold 86 -> 83 us
+  // (profiles/r02/ab_asm_lds.log): the extra barrier costs more than the halved gathers save
+  // while the inputs sit in the Infinity Cache.  Off by default.
+  static const bool lds_env = [] {
+    const char *e = getenv("PNP_ASM_LDS");
+    return e && atoi(e) == 1;
+  }();
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
     if (!fanr && a.jac)                                                            \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
     else if (!fanr)                                                                \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
+    else if (!a.jac && fanr == 9 && ga && lds_env && L.uptr &&                      \
+             size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9, 9, 0, 1>), grid, block,         \
+                         size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
     else if (!a.jac && fanr == 9 && ga)                                            \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9>), grid, block, 0, s, L, a);  \
     else if (!a.jac)                                                               \
@@ -641,6 +697,10 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
+    else if (ga == 4 && fanr == 9 && lds_env && L.uptr &&                           \
+             size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
+      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \
+                         size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
     else if (ga == 4 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, L, a); \
     else if (ga == 5 && fanr == 9)                                                 \
