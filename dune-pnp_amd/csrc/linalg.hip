@@ -178,8 +178,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
 // The SpMV with the x gathers staged through LDS (PNP_SPMV_LDS): a workgroup first loads x at the
 // distinct columns of its 256 rows (config 3: 1,016 per block against 1,796 slots, so half the
 // scattered gathers), then every slot reads its x record from LDS by a 16-bit list position.
-// One lane per row, slots in batches of SB; the same products in the same order as k_spmv<.., 1>,
-// so the same result bits.
+// One lane per row, slots in pairs.  The arithmetic order is that of the default k_spmv<.., 2, 2>
+// (two lanes per row, even / odd slots, combined at the end; dot partials per 128 rows with the
+// same trees), so results and partials are bitwise those of k_spmv: the BiCGSTAB iterates and
+// iteration counts do not move (they are sensitive to the last bit on the pore system).
 template <int NF, int PAT, int MODE, int SB, int NT>
 __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *__restrict__ vals,
                                                      const double *__restrict__ x,
@@ -202,10 +204,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
     for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
   }
   __syncthreads();
+  static_assert(SB == 2, "slot pairs: even slots into acc2[0], odd into acc2[1]");
   double d[3] = {0, 0, 0};
-  double acc[NF];
+  double acc2[2][NF];
 #pragma unroll
-  for (int f = 0; f < NF; f++) acc[f] = 0;
+  for (int f = 0; f < NF; f++) acc2[0][f] = acc2[1][f] = 0;
   const uint16_t *__restrict__ lix = L.lidx + off + lane;
   const double *__restrict__ vc = vals + size_t(off) * NK;
   for (int s0 = 0; s0 < len; s0 += SB) {
@@ -236,10 +239,13 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
 #pragma unroll
         for (int g = 0; g < NF; g++) {
           const int v = pat_index(PAT, f, g);
-          if (v >= 0) acc[f] += a[v] * xj[g];
+          if (v >= 0) acc2[b][f] += a[v] * xj[g];
         }
     }
   }
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = acc2[0][f] + acc2[1][f];
   if (live) {
     const unsigned dm = row_mask<NF>(L, row);  // Dirichlet rows are identity rows
     if (dm) {
@@ -273,15 +279,28 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
       for (int f = 0; f < NF; f++) d[2] += acc[f] * wr[f];
     }
   }
-  if constexpr (MODE == 1) {
-    double v1[1] = {d[0]};
-    block_sum<1>(v1, partials + blockIdx.x);
-  } else if constexpr (MODE == 2) {
-    double v2[2] = {d[0], d[1]};
-    block_sum<2>(v2, partials + 2 * blockIdx.x);
-  } else if constexpr (MODE == 4) {
-    double v3[3] = {d[0], d[1], d[2]};
-    block_sum<3>(v3, partials + 3 * blockIdx.x);
+  if constexpr (MODE == 1 || MODE == 2 || MODE == 4) {
+    // the trees of k_spmv<.., 2, 2>'s block_sum: per 32 rows xor 16, 8, 4, 2, 1, then per 128
+    // rows the four 32-row sums in order -> two partials per 256-row workgroup
+    constexpr int K = MODE == 1 ? 1 : (MODE == 2 ? 2 : 3);
+    __shared__ double sh[8][K];
+#pragma unroll
+    for (int kk = 0; kk < K; kk++) {
+      double v = d[kk];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if ((threadIdx.x & 31) == 0) sh[threadIdx.x >> 5][kk] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const int h = threadIdx.x;
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) {
+        double t = 0;
+        for (int i = 0; i < 4; i++) t += sh[4 * h + i][kk];
+        partials[size_t(K) * (2 * blockIdx.x + h) + kk] = t;
+      }
+    }
   }
 }
 
@@ -1361,12 +1380,8 @@ static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double 
   const int b = spmv_batch(), l = spmv_lpr();
   if (spmv_uses_lds(L)) {
     const size_t lds = size_t(L.umax) * NF * sizeof(double);
-    if (b == 4)
-      hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 4, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
-                         w, partials, w2);
-    else
-      hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
-                         w, partials, w2);
+    hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
+                       w, partials, w2);
     return;
   }
   if (spmv_nt() && l == 2 && b == 2) {
@@ -1399,7 +1414,7 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
     return hipSuccess;
   }
   dim3 g = L.blkcount > 0 ? dim3(L.blkcount) : rows_grid(L.n_owned);
-  if (nparts) *nparts = int(g.x) * (spmv_uses_lds(L) ? 1 : spmv_lpr());
+  if (nparts) *nparts = int(g.x) * (spmv_uses_lds(L) ? 2 : spmv_lpr());
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
