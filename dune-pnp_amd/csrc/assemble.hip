@@ -401,25 +401,12 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   constexpr int RW = asm_lds_rec<OP>();
   extern __shared__ double srec[];  // LDSG: [cnt][RW] = x, y, dofs, aux0, aux1
   const int blk = row_block(L, blockIdx.x, gridDim.x);
-  const int row = blk * blockDim.x + threadIdx.x;
-  if constexpr (LDSG) {
-    const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
-    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
-      const int j = L.ulist[u0 + k];
-      const double2 p = reinterpret_cast<const double2 *>(L.xy)[j];
-      double u[NF];
-      load_nf<NF>(a.x, size_t(j), u);
-      double *r = srec + size_t(k) * RW;
-      r[0] = p.x;
-      r[1] = p.y;
-#pragma unroll
-      for (int f = 0; f < NF; f++) r[2 + f] = u[f];
-      if constexpr (AUX0) r[2 + NF] = a.aux0[j];
-      if constexpr (AUX1) r[3 + NF] = a.aux1[j];
-    }
-    __syncthreads();
-  }
-  if (row >= L.n_owned) return;
+  const int row0 = blk * blockDim.x + threadIdx.x;
+  const bool live = row0 < L.n_owned;
+  if (!LDSG && !live) return;
+  // the row's own loads first (LDSG: they are in flight while the workgroup stages the
+  // neighbour records, instead of after its barrier)
+  const int row = live ? row0 : 0;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = L.chunk_off[chunk];
   const uint64_t meta = L.rowmeta[row];
@@ -444,6 +431,24 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   double ai = 0, aq = 0;
   if constexpr (AUX0) ai = a.aux0[row];
   if constexpr (AUX1) aq = a.aux1[row];
+  if constexpr (LDSG) {
+    const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+      const int j = L.ulist[u0 + k];
+      const double2 p = reinterpret_cast<const double2 *>(L.xy)[j];
+      double u[NF];
+      load_nf<NF>(a.x, size_t(j), u);
+      double *r = srec + size_t(k) * RW;
+      r[0] = p.x;
+      r[1] = p.y;
+#pragma unroll
+      for (int f = 0; f < NF; f++) r[2 + f] = u[f];
+      if constexpr (AUX0) r[2 + NF] = a.aux0[j];
+      if constexpr (AUX1) r[3 + NF] = a.aux1[j];
+    }
+    __syncthreads();
+    if (!live) return;
+  }
   double2 pn[NS];
   double un[NS][NF], a0[NS], a1[NS];
   auto gather = [&](int k) {
@@ -670,9 +675,10 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
   const int fanr = !fanr_ok ? 0 : (L.max_slots <= 9 ? 9 : (L.max_slots <= 12 ? 12 : 0));
   // LDS-staged neighbour data (A/B knob PNP_ASM_LDS=1), when the layout has the lists and a
   // workgroup's records fit 53 KiB (3 workgroups per CU at the kernel's 3 waves per SIMD).
-  // Measured at config 3: warm 53.5 -> 57.6 us, cache-cold 86 -> 83 us
-  // (profiles/r02/ab_asm_lds.log): the extra barrier costs more than the halved gathers save
-  // while the inputs sit in the Infinity Cache.  Off by default.
+  // Measured at config 3, with the row's own loads issued before the staging barrier: warm
+  // 53.5 -> 60-63 us, cache-cold 87 -> 77.7 us (profiles/r02/ab_asm_lds2.log): the barrier costs
+  // more than the halved gathers save while the inputs sit in the Infinity Cache, and less when
+  // they come from HBM.  Off by default (the back-to-back assembly is the benchmark's number).
   static const bool lds_env = [] {
     const char *e = getenv("PNP_ASM_LDS");
     return e && atoi(e) == 1;
