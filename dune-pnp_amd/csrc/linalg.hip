@@ -1482,7 +1482,7 @@ static bool sweep_nt() {  // default on: ILU0 apply -7 %, SGS -7 % (profiles/r01
         CALL;                                      \
       } break;                                     \
       case 36: {                                   \
-        constexpr int LPRc = 2, Bc = 4, NTc = 0;   \
+        constexpr int LPRc = 2, Bc = 4, NTc = 1;   \
         CALL;                                      \
       } break;                                     \
       default:                                     \
