@@ -111,6 +111,7 @@ struct pnp_ctx {
   pnp::PkDev pkd;
   DBuf<int> pk_enode, pk_ioff, pk_icnt, pk_inc;
   DBuf<uint32_t> pk_islot;
+  DBuf<double> pk_eres;
   pnp::Params params;
   pnp::Fans fans;
   pnp::LocalLayout L;
@@ -704,7 +705,9 @@ struct pnp_ctx {
         (rc = upv(pk_icnt, icnt, "P_k icnt")) || (rc = upv(pk_inc, inc, "P_k incidences")) ||
         (rc = upv(pk_islot, islot, "P_k slots")))
       return rc;
-    hipError_t e = pnp::pk_upload_tables(pks.k, stream);
+    hipError_t e = pk_eres.alloc(std::max<size_t>(1, size_t(ne) * nl));
+    if (e != hipSuccess) return hipfail(e, "P_k element residual scratch");
+    e = pnp::pk_upload_tables(pks.k, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "P_k tables");
     pkd.k = pks.k;
@@ -715,6 +718,7 @@ struct pnp_ctx {
     pkd.icnt = pk_icnt.p;
     pkd.inc = pk_inc.p;
     pkd.islot = pk_islot.p;
+    pkd.eres = pk_eres.p;
     // ion-flux segments handled by this rank: those whose element is local and whose lower
     // global vertex is owned here, {local element, face, group}, in global segment order
     std::vector<int> eloc(m.nt, -1);

@@ -401,6 +401,7 @@ struct PkDev {
   const int *enode = nullptr;
   const int *ioff = nullptr, *icnt = nullptr, *inc = nullptr;
   const uint32_t *islot = nullptr;
+  double *eres = nullptr;  // [nl][ne] element residual rows of the two-pass residual-only launch
 };
 hipError_t pk_upload_tables(int k, hipStream_t s);
 // jac 0 residual, 1 analytic Jacobian, 2 forward-difference Jacobian (PNP_JAC_FD)

@@ -419,6 +419,131 @@ __global__ __launch_bounds__(kB) void k_pk_row(DevLayout L, PkDev D, const doubl
   }
 }
 
+// Residual-only launches in two passes (the Jacobian launches keep k_pk_row).  Pass 1, one thread
+// per local element: every row of the element residual, pk_row_residual's statements with each
+// quadrature point's u, grad u and source computed once for all NL rows instead of once per row
+// (the row walk repeats them for each of the element's NL nodes), into eres[ra * ne + e].
+// Pass 2 (k_pk_res_gather): each owned row sums its incidences' entries in the row walk's
+// ascending element order, so the residual is the row walk's, bit for bit.
+template <int K>
+__global__ __launch_bounds__(kB) void k_pk_elem_res(PkDev D, const double *__restrict__ xy,
+                                                    const double *__restrict__ x,
+                                                    const double *__restrict__ aux0,
+                                                    const double *__restrict__ aux1, PkArgs a) {
+  constexpr int NL = PkK<K>::NL;
+  const int ne = D.ne, e = blockIdx.x * kB + threadIdx.x;
+  if (e >= ne) return;
+  int nd[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
+  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
+  const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
+  double xl[NL], f0[NL], f1[NL], r[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    xl[i] = x[nd[i]];
+    f0[i] = aux0 ? aux0[nd[i]] : 0.0;
+    f1[i] = aux1 ? aux1[nd[i]] : 0.0;
+    r[i] = 0.0;
+  }
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+  if (a.mass || a.kind == OP_DIFF_IE) {
+#pragma unroll 1
+    for (int q = 0; q < 7; q++) {
+      const auto &P = T.q5[q];
+      double u = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+      const double f = P.w * G.adet;
+#pragma unroll
+      for (int ra = 0; ra < NL; ra++) r[ra] += u * P.phi[ra] * f;
+    }
+  }
+  if (a.mass) {
+  } else if (a.kind == OP_PB || a.kind == OP_POISSON) {
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) {
+      const auto &P = T.q3[q];
+      const double f = factor(G, P, a.cyl, PI);
+      double g[NL][2];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        grad(G, P, i, g[i][0], g[i][1]);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g[i][0];
+        gu1 += xl[i] * g[i][1];
+        if (a.kind == OP_POISSON) {
+          cp += f0[i] * P.phi[i];
+          cm += f1[i] * P.phi[i];
+        }
+      }
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+#pragma unroll
+      for (int ra = 0; ra < NL; ra++)
+        r[ra] += (gu0 * g[ra][0] + gu1 * g[ra][1] + s * P.phi[ra]) * f;
+    }
+  } else {
+    const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+#pragma unroll 1
+    for (int q = 0; q < 3; q++) {
+      const auto &P = T.q2[q];
+      double g[NL][2];
+      double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+        grad(G, P, i, g[i][0], g[i][1]);
+        u += xl[i] * P.phi[i];
+        gu0 += xl[i] * g[i][0];
+        gu1 += xl[i] * g[i][1];
+        gP0 += f0[i] * g[i][0];
+        gP1 += f0[i] * g[i][1];
+      }
+      const double f = P.w * G.adet;
+#pragma unroll
+      for (int ra = 0; ra < NL; ra++)
+        r[ra] += sc * ((gu0 * g[ra][0] + gu1 * g[ra][1] +
+                        u * a.z * (gP0 * g[ra][0] + gP1 * g[ra][1]) + 0.0 * u * P.phi[ra]) * f);
+    }
+  }
+#pragma unroll
+  for (int ra = 0; ra < NL; ra++) D.eres[size_t(ra) * ne + e] = r[ra];
+}
+
+// pass 2: one thread per owned row (SELL lane order, the spatial block order), the incidence codes
+// of up to four elements loaded before their entries, the entries summed in incidence order
+__global__ __launch_bounds__(kB) void k_pk_res_gather(DevLayout L, PkDev D, int mode,
+                                                      const double *__restrict__ cvec_in,
+                                                      const uint8_t *__restrict__ dmask,
+                                                      double *__restrict__ r,
+                                                      double *__restrict__ cvec_out) {
+  const int row = row_block(L, blockIdx.x, gridDim.x) * kB + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int cnt = D.icnt[row], ib = D.ioff[chunk] + lane;
+  const double *__restrict__ er = D.eres;
+  double R = 0.0;
+  for (int t0 = 0; t0 < cnt; t0 += 4) {
+    int code[4];
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) code[j] = t0 + j < cnt ? D.inc[ib + (t0 + j) * kRows] : -1;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      v[j] = code[j] >= 0 ? er[size_t(code[j] & 15) * D.ne + (code[j] >> 4)] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (code[j] >= 0) R += v[j];
+  }
+  if (mode == 1) {
+    cvec_out[row] -= R;
+  } else {
+    const double rv = R + cvec_in[row];
+    r[row] = dmask[row] != 0 ? 0.0 : rv;
+  }
+}
+
 // calcIonFlux (src/ionFlux.hh:50-91) on P_k: one thread per boundary segment of this rank;
 // seg = {element (local), local face, group}; the three fields at the face centre from the
 // element's nodes.  out[2s] / out[2s+1]: ip / im contributions (summed on the host in segment order)
@@ -527,6 +652,15 @@ hipError_t upload_tab(hipStream_t s) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_tab3), &T, sizeof T, 0, hipMemcpyHostToDevice, s);
 }
 
+// PNP_PK_RES2=0 sends residual-only launches through the row walk (A/B knob)
+bool res_two_pass() {
+  static const bool on = [] {
+    const char *v = getenv("PNP_PK_RES2");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <int K, int JAC>
 hipError_t row_launch1(const DevLayout &L, const PkDev &D, const double *x, const double *aux0,
                        const double *aux1, const PkArgs &a, int mode, const double *cvec_in,
@@ -552,6 +686,13 @@ hipError_t row_launch(const DevLayout &L, const PkDev &D, const double *x, const
                       const double *aux1, const PkArgs &a, int jac, int mode, const double *cvec_in,
                       const uint8_t *dmask, double *r, double *cvec_out, double *vals,
                       hipStream_t s) {
+  if (jac == 0 && D.eres && res_two_pass()) {
+    hipLaunchKernelGGL(k_pk_elem_res<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
+                       aux0, aux1, a);
+    hipLaunchKernelGGL(k_pk_res_gather, dim3((L.n_owned + kB - 1) / kB), dim3(kB), 0, s, L, D,
+                       mode, cvec_in, dmask, r, cvec_out);
+    return hipGetLastError();
+  }
   if (jac == 0)
     return row_launch1<K, 0>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
   if (jac == 1)
