@@ -111,7 +111,7 @@ struct pnp_ctx {
   pnp::PkDev pkd;
   DBuf<int> pk_enode, pk_ioff, pk_icnt, pk_inc;
   DBuf<uint32_t> pk_islot;
-  DBuf<double> pk_eres;
+  DBuf<double> pk_eres, pk_ejac;
   pnp::Params params;
   pnp::Fans fans;
   pnp::LocalLayout L;
@@ -707,6 +707,8 @@ struct pnp_ctx {
       return rc;
     hipError_t e = pk_eres.alloc(std::max<size_t>(1, size_t(ne) * nl));
     if (e != hipSuccess) return hipfail(e, "P_k element residual scratch");
+    e = pk_ejac.alloc(std::max<size_t>(1, size_t(ne) * nl * ((nl + 2) & ~1)));
+    if (e != hipSuccess) return hipfail(e, "P_k element matrix scratch");
     e = pnp::pk_upload_tables(pks.k, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "P_k tables");
@@ -719,6 +721,7 @@ struct pnp_ctx {
     pkd.inc = pk_inc.p;
     pkd.islot = pk_islot.p;
     pkd.eres = pk_eres.p;
+    pkd.ejac = pk_ejac.p;
     // ion-flux segments handled by this rank: those whose element is local and whose lower
     // global vertex is owned here, {local element, face, group}, in global segment order
     std::vector<int> eloc(m.nt, -1);

@@ -402,6 +402,7 @@ struct PkDev {
   const int *ioff = nullptr, *icnt = nullptr, *inc = nullptr;
   const uint32_t *islot = nullptr;
   double *eres = nullptr;  // [nl][ne] element residual rows of the two-pass residual-only launch
+  double *ejac = nullptr;  // [ne][nl][W] element matrix + residual rows of the two-pass Jacobian
 };
 hipError_t pk_upload_tables(int k, hipStream_t s);
 // jac 0 residual, 1 analytic Jacobian, 2 forward-difference Jacobian (PNP_JAC_FD)

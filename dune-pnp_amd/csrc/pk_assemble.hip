@@ -14,7 +14,11 @@
 // Measured at pore_pnp k=3 (profiles/r02/bench_pk_*.log): a first two-pass form (element matrices
 // into SoA scratch, then a per-slot gather of their codes) took 506 us (P2) / 1574 us (P3) per
 // Poisson assembly, 80 % of it in the latency-bound gather of 28 / 100 scattered values per
-// element.  The P1 path keeps its fan-walk kernels (assemble.hip).
+// element.  The row walk's price is the element's quadrature data recomputed for each of its
+// nodes; the default launches now split it the other way (k_pk_elem_res / k_pk_elem_jac below):
+// each element's rows computed once into per-(element, row) records, then the row walk's own
+// accumulation reading them (profiles/r02/ab_pk_res2).  The P1 path keeps its fan-walk kernels
+// (assemble.hip).
 #include <cmath>
 #include <vector>
 
@@ -544,6 +548,201 @@ __global__ __launch_bounds__(kB) void k_pk_res_gather(DevLayout L, PkDev D, int 
   }
 }
 
+// Analytic Jacobian launches in two passes as well (PNP_PK_JAC2, default on).  Pass 1, one thread per
+// local element: each row ra of the element residual and matrix with pk_row_both's statements,
+// the quadrature point's basis gradients, u, grad u and source shared by RG rows at a time (RG
+// rows of the matrix in registers: all 6 at P2, 5 at P3), into one record of W doubles per
+// (element, row): the NL matrix entries, then the residual entry, padded to 16 B.  Measured
+// against one thread per (element, row group), and with register caps for more waves per SIMD
+// (profiles/r02/ab_pk_elem): both slower or spilling.
+// Pass 2 (k_pk_jac_gather): k_pk_row's slot accumulation with each incidence's record read
+// instead of computed -- the same sums in the same order, so residual and matrix are k_pk_row's,
+// bit for bit.
+#ifndef PK_RG2
+#define PK_RG2 6  // A/B knob (build flag): element rows per register group of the P2 element pass
+#endif
+#ifndef PK_RG3
+#define PK_RG3 5  // the same at P3
+#endif
+template <int K>
+struct PkRec {
+  static constexpr int NL = PkK<K>::NL, W = (NL + 2) & ~1, RG = K == 2 ? PK_RG2 : PK_RG3;
+};
+
+template <int K>
+__global__ __launch_bounds__(kB) void k_pk_elem_jac(PkDev D, const double *__restrict__ xy,
+                                                    const double *__restrict__ x,
+                                                    const double *__restrict__ aux0,
+                                                    const double *__restrict__ aux1, PkArgs a) {
+  constexpr int NL = PkK<K>::NL, W = PkRec<K>::W, RG = PkRec<K>::RG;
+  const int ne = D.ne, e = blockIdx.x * kB + threadIdx.x;
+  if (e >= ne) return;
+  int nd[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
+  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
+  const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
+  double xl[NL], f0[NL], f1[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    xl[i] = x[nd[i]];
+    f0[i] = aux0 ? aux0[nd[i]] : 0.0;
+    f1[i] = aux1 ? aux1[nd[i]] : 0.0;
+  }
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+  double *rec0 = D.ejac + size_t(e) * NL * W;
+#pragma unroll 1
+  for (int ra0 = 0; ra0 < NL; ra0 += RG) {
+    double r[RG], Jr[RG][NL];
+#pragma unroll
+    for (int j = 0; j < RG; j++) {
+      r[j] = 0.0;
+#pragma unroll
+      for (int b = 0; b < NL; b++) Jr[j][b] = 0.0;
+    }
+    if (a.kind == OP_DIFF_IE) {
+#pragma unroll 1
+      for (int q = 0; q < 7; q++) {
+        const auto &P = T.q5[q];
+        double u = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+        const double f = P.w * G.adet;
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          r[j] += u * P.phi[ra] * f;
+#pragma unroll
+          for (int b = 0; b < NL; b++) Jr[j][b] += P.phi[ra] * P.phi[b] * f;
+        }
+      }
+    }
+    if (a.kind == OP_PB || a.kind == OP_POISSON) {
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) {
+        const auto &P = T.q3[q];
+        const double f = factor(G, P, a.cyl, PI);
+        double g[NL][2];
+        double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+          grad(G, P, i, g[i][0], g[i][1]);
+          u += xl[i] * P.phi[i];
+          gu0 += xl[i] * g[i][0];
+          gu1 += xl[i] * g[i][1];
+          if (a.kind == OP_POISSON) {
+            cp += f0[i] * P.phi[i];
+            cm += f1[i] * P.phi[i];
+          }
+        }
+        const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+        const double ch = a.kind == OP_PB ? cosh(u) : 0.0;
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          const double c = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * ch * P.phi[ra] : 0.0;
+          double ga0, ga1;
+          grad(G, P, ra, ga0, ga1);
+          r[j] += (gu0 * ga0 + gu1 * ga1 + s * P.phi[ra]) * f;
+#pragma unroll
+          for (int b = 0; b < NL; b++) Jr[j][b] += (ga0 * g[b][0] + ga1 * g[b][1] + c * P.phi[b]) * f;
+        }
+      }
+    } else {
+      const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+#pragma unroll 1
+      for (int q = 0; q < 3; q++) {
+        const auto &P = T.q2[q];
+        double g[NL][2];
+        double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+          grad(G, P, i, g[i][0], g[i][1]);
+          u += xl[i] * P.phi[i];
+          gu0 += xl[i] * g[i][0];
+          gu1 += xl[i] * g[i][1];
+          gP0 += f0[i] * g[i][0];
+          gP1 += f0[i] * g[i][1];
+        }
+        const double f = P.w * G.adet;
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          double ga0, ga1;
+          grad(G, P, ra, ga0, ga1);
+          r[j] += sc * ((gu0 * ga0 + gu1 * ga1 + u * a.z * (gP0 * ga0 + gP1 * ga1) + 0.0 * u * P.phi[ra]) * f);
+          const double drift = a.z * (gP0 * ga0 + gP1 * ga1);
+#pragma unroll
+          for (int b = 0; b < NL; b++)
+            Jr[j][b] += sc * ((ga0 * g[b][0] + ga1 * g[b][1] + P.phi[b] * drift) * f);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RG; j++) {
+      if (ra0 + j >= NL) break;
+      double2 *rec = reinterpret_cast<double2 *>(rec0 + size_t(ra0 + j) * W);
+      double v[W];
+#pragma unroll
+      for (int b = 0; b < NL; b++) v[b] = Jr[j][b];
+      v[NL] = r[j];
+#pragma unroll
+      for (int b = NL + 1; b < W; b++) v[b] = 0.0;
+#pragma unroll
+      for (int w = 0; w < W / 2; w++) rec[w] = make_double2(v[2 * w], v[2 * w + 1]);
+    }
+  }
+}
+
+// pass 2: one thread per owned row, k_pk_row's slot accumulation in LDS with each incidence's
+// record (and slot codes) loaded instead of computed; the code of the next incidence is in flight
+// while the current record is added
+template <int K>
+__global__ __launch_bounds__(kB) void k_pk_jac_gather(DevLayout L, PkDev D,
+                                                      const double *__restrict__ cvec_in,
+                                                      const uint8_t *__restrict__ dmask,
+                                                      double *__restrict__ r,
+                                                      double *__restrict__ vals) {
+  constexpr int NL = PkK<K>::NL, NW = (NL + 3) / 4, W = PkRec<K>::W;
+  extern __shared__ double acc[];  // [max_slots][kB]
+  const int row = row_block(L, blockIdx.x, gridDim.x) * kB + threadIdx.x;
+  if (row >= L.n_owned) return;
+  const int chunk = row / kRows, lane = row % kRows;
+  const int off = L.chunk_off[chunk], len = int(L.rowmeta[row] & 63);
+  double *arow = acc + threadIdx.x;
+  for (int s = 0; s < len; s++) arow[s * kB] = 0.0;
+  const int cnt = D.icnt[row], ib = D.ioff[chunk] + lane;
+  double R = 0.0;
+  int code = cnt > 0 ? D.inc[ib] : 0;
+  for (int t = 0; t < cnt; t++) {
+    const int p = ib + t * kRows;
+    const int e = code >> 4, ra = code & 15;
+    if (t + 1 < cnt) code = D.inc[p + kRows];
+    uint32_t sw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) sw[w] = D.islot[size_t(p) * NW + w];
+    const double2 *rec = reinterpret_cast<const double2 *>(D.ejac + (size_t(e) * NL + ra) * W);
+    double v[W];
+#pragma unroll
+    for (int w = 0; w < W / 2; w++) {
+      const double2 q = rec[w];
+      v[2 * w] = q.x;
+      v[2 * w + 1] = q.y;
+    }
+    R += v[NL];
+#pragma unroll
+    for (int b = 0; b < NL; b++) {
+      const int s = (sw[b >> 2] >> (8 * (b & 3))) & 0xff;
+      arow[s * kB] += v[b];
+    }
+  }
+  double *vrow = vals + size_t(off) + lane;
+  for (int s = 0; s < len; s++) __builtin_nontemporal_store(arow[s * kB], vrow + size_t(s) * kRows);
+  const double rv = R + cvec_in[row];
+  r[row] = dmask[row] != 0 ? 0.0 : rv;
+}
+
 // calcIonFlux (src/ionFlux.hh:50-91) on P_k: one thread per boundary segment of this rank;
 // seg = {element (local), local face, group}; the three fields at the face centre from the
 // element's nodes.  out[2s] / out[2s+1]: ip / im contributions (summed on the host in segment order)
@@ -652,13 +851,39 @@ hipError_t upload_tab(hipStream_t s) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_tab3), &T, sizeof T, 0, hipMemcpyHostToDevice, s);
 }
 
-// PNP_PK_RES2=0 sends residual-only launches through the row walk (A/B knob)
+// PNP_PK_RES2=0 / PNP_PK_JAC2=0 send residual-only / analytic Jacobian launches through the row
+// walk (A/B knobs)
+bool env_on(const char *name) {
+  const char *v = getenv(name);
+  return !(v && v[0] == '0');
+}
 bool res_two_pass() {
-  static const bool on = [] {
-    const char *v = getenv("PNP_PK_RES2");
-    return !(v && v[0] == '0');
-  }();
+  static const bool on = env_on("PNP_PK_RES2");
   return on;
+}
+bool jac_two_pass() {
+  static const bool on = env_on("PNP_PK_JAC2");
+  return on;
+}
+
+template <int K>
+hipError_t jac_launch2(const DevLayout &L, const PkDev &D, const double *x, const double *aux0,
+                       const double *aux1, const PkArgs &a, const double *cvec_in,
+                       const uint8_t *dmask, double *r, double *vals, hipStream_t s) {
+  const size_t lds = size_t(L.max_slots) * kB * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pk_jac_gather<K>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
+                     aux0, aux1, a);
+  hipLaunchKernelGGL(k_pk_jac_gather<K>, dim3((L.n_owned + kB - 1) / kB), dim3(kB), lds, s, L, D,
+                     cvec_in, dmask, r, vals);
+  return hipGetLastError();
 }
 
 template <int K, int JAC>
@@ -695,6 +920,8 @@ hipError_t row_launch(const DevLayout &L, const PkDev &D, const double *x, const
   }
   if (jac == 0)
     return row_launch1<K, 0>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
+  if (jac == 1 && mode == 0 && !a.mass && D.ejac && jac_two_pass())
+    return jac_launch2<K>(L, D, x, aux0, aux1, a, cvec_in, dmask, r, vals, s);
   if (jac == 1)
     return row_launch1<K, 1>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);
   return row_launch1<K, 2>(L, D, x, aux0, aux1, a, mode, cvec_in, dmask, r, cvec_out, vals, s);

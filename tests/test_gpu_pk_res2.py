@@ -1,9 +1,10 @@
-"""The two-pass P_k residual (k_pk_elem_res + k_pk_res_gather, the default for residual-only
-launches) against the row walk (k_pk_row<K, 0>, PNP_PK_RES2=0), -m gpu.  The knob is read once per
-process, so each variant runs in a child process.  Both evaluate pk_row_residual's statements per
-element row and sum a row's elements in the same ascending order, so every residual -- the four
-scalar operators at k = 2 and 3, including the implicit-Euler operator's old-time mass term -- and
-a P2 PB Newton solve must be bitwise the same."""
+"""The two-pass P_k assembly (element pass + ordered per-row gather: k_pk_elem_res /
+k_pk_res_gather for residual-only launches, k_pk_elem_jac / k_pk_jac_gather for the analytic
+Jacobian, the defaults) against the row walk (k_pk_row, PNP_PK_RES2=0 PNP_PK_JAC2=0), -m gpu.  The
+knobs are read once per process, so each variant runs in a child process.  Both evaluate the row
+walk's statements per element row and sum a row's elements in the same ascending order, so every
+residual and Jacobian -- the four scalar operators at k = 2 and 3, including the implicit-Euler
+operator's old-time mass term -- and a P2 PB Newton solve must be bitwise the same."""
 import json
 import os
 import subprocess
@@ -39,7 +40,8 @@ for name in ("pore_small", "cylinder"):
                 kw = dict(cp=rng.uniform(0.0, 0.1, nn), cm=rng.uniform(0.0, 0.1, nn))
             ctx.set_operator(KINDS[kind][0], **kw)
             x = rng.uniform(-1, 1, nn) if kind in ("pb", "poisson") else rng.uniform(0, 0.1, nn)
-            out[f"{name}/{k}/{kind}"] = h(ctx.residual(x))
+            J = ctx.jacobian(x).tocsr()
+            out[f"{name}/{k}/{kind}"] = [h(ctx.residual(x)), h(J.data), h(J.indices)]
         if k == 2:  # P3 matrices are indefinite (quirk Q10): no preconditioned Newton there
             ctx.set_operator(P.OP_PB)
             u, res = ctx.newton(np.zeros(nn), prec=P.PREC_SSOR)
@@ -50,7 +52,7 @@ print("RESULT " + json.dumps(out))
 
 
 def run(two_pass):
-    env = dict(os.environ, PNP_PK_RES2=str(two_pass))
+    env = dict(os.environ, PNP_PK_RES2=str(two_pass), PNP_PK_JAC2=str(two_pass))
     code = CHILD.replace("HERE", repr(HERE))
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300, cwd=HERE)

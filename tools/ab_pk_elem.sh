@@ -1,0 +1,13 @@
+#!/bin/bash
+# P_k element-pass shapes: the in-tree library and dune-pnp_amd/ab/lib_<v>.so for each v given,
+# tools/bench_pk.py (pore_pnp k=3, degrees 2 and 3) interleaved twice, after the bitwise test of the
+# two-pass assembly.  usage: tools/ab_pk_elem.sh <tag> <variant>...
+set -u
+OUT=gpurun_out/$1; shift; mkdir -p "$OUT"
+timeout -k 10 300 python -u -m pytest -q --timeout 250 --timeout-method thread tests/test_gpu_pk_res2.py > "$OUT/pk_tests.log" 2>&1 || exit $?
+for i in 1 2; do
+  PNP_PK_NO_SOLVE=1 timeout -k 10 200 python tools/bench_pk.py 3 2 3 > "$OUT/pk_head_$i.log" 2>&1 || exit $?
+  for v in "$@"; do
+    PNP_PK_NO_SOLVE=1 PNP_AMD_LIB=dune-pnp_amd/ab/lib_$v.so timeout -k 10 200 python tools/bench_pk.py 3 2 3 > "$OUT/pk_${v}_$i.log" 2>&1 || exit $?
+  done
+done

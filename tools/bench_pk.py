@@ -2,11 +2,13 @@
 Lagrange space of degree k (src/instationary_pnp_from_pb_md.hh:26-28, 125, 245-247), on
 test/pore_pnp/pore.msh refined r times (default 3: 185K vertices, 367K triangles).
 Per degree: DOF nodes, residual + Jacobian assembly time (HIP events) of PoissonOperator and
-PBOperator, and the two-pass kernels' algorithmic bytes:
-  element pass: reads nl node values + nl frozen values per element (gathers, 8 B each) and the
-                3 vertex coordinates (16 B), writes nl + nl^2 element values (8 B)
-  gather pass : reads the codes (4 B per element entry + 4 B per slot count) and the element
-                values they point at (8 B), writes one value per SELL slot (8 B) and the residual
+PBOperator, and the two-pass Jacobian kernels' algorithmic bytes (pk_assemble.hip):
+  element pass: reads nl node indices (4 B) + nl node values and nl per frozen field (8 B each) and
+                the 3 vertex coordinates (16 B); writes nl records of W = nl + 2 rounded to even
+                doubles (the matrix row, the residual entry, padding)
+  gather pass : per incidence (ne * nl of them) the code (4 B), the slot bytes (4 B per 4 nodes)
+                and the record (8 W B); per row the count, load vector, mask and residual
+                (4 + 8 + 1 + 8 B); one value per SELL slot written (8 B)
 A PoissonOperator BiCGSTAB solve (ILU(0) for P1/P2, no preconditioner for P3: Q10) is timed too.
 Prints one JSON object per degree.  usage: python tools/bench_pk.py [refine] [degrees...]   (PNP_PK_NO_SOLVE=1: assembly only)"""
 import json
@@ -65,8 +67,9 @@ def main():
         if k > 1:
             ne = mesh.nt  # one rank: every element is local
             aux = 2  # Poisson: c+ and c- frozen
-            elem = ne * (nl * (1 + aux) * 8 + 3 * 16 + (nl + nl * nl) * 8)
-            gather = ne * nl * nl * (4 + 8) + ne * nl * (4 + 8) + info["nslots"] * (4 + 8) + nn * 16
+            W = (nl + 2) & ~1
+            elem = ne * (nl * 4 + nl * (1 + aux) * 8 + 3 * 16 + nl * W * 8)
+            gather = ne * nl * (4 + 4 * ((nl + 3) // 4) + 8 * W) + nn * 21 + info["nslots"] * 8
             out["poisson"]["bytes_element_pass"] = elem
             out["poisson"]["bytes_gather_pass"] = gather
             out["poisson"]["achieved_gbs"] = (elem + gather) / (out["poisson"]["assemble_us"] * 1e-6) / 1e9
