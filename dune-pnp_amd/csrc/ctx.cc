@@ -112,6 +112,7 @@ struct pnp_ctx {
   DBuf<int> pk_enode, pk_ioff, pk_icnt, pk_inc;
   DBuf<uint32_t> pk_islot;
   DBuf<double> pk_eres, pk_ejac;
+  DBuf<int> pk_blk_short, pk_blk_long;
   pnp::Params params;
   pnp::Fans fans;
   pnp::LocalLayout L;
@@ -722,6 +723,42 @@ struct pnp_ctx {
     pkd.islot = pk_islot.p;
     pkd.eres = pk_eres.p;
     pkd.ejac = pk_ejac.p;
+    // the Jacobian gather pass accumulates a row's slots in LDS, sized for the longest row: the
+    // vertex rows (up to 55 slots at P3) would hold every workgroup to one per CU.  When the
+    // longest row needs more than 64 KB per workgroup, blocks whose rows are all at most the
+    // median block length (the edge and interior node rows) run in a launch of their own with an
+    // LDS accumulator of that length: P3 438 -> 395 us; at P2 (one launch at 3 workgroups per CU)
+    // the second launch costs more than it gains, 135 -> 145 us (profiles/r02/ab_pk_split).
+    // PNP_PK_SPLIT=0: always one launch, 1: split whenever the median is at most half the longest
+    {
+      const char *ev = getenv("PNP_PK_SPLIT");
+      const int nblk = (L.n_owned + 255) / 256;
+      std::vector<int> order(nblk), blen(nblk, 0);
+      for (int b = 0; b < nblk; b++) order[b] = b;
+      if (dl.blkmap && nblk > 0) {
+        e = hipMemcpy(order.data(), dl.blkmap, sizeof(int) * nblk, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hipfail(e, "blkmap");
+      }
+      for (int r = 0; r < L.n_owned; r++)
+        blen[r / 256] = std::max(blen[r / 256], pnp::meta_len(L.rowmeta[r]));
+      std::vector<int> srt(blen);
+      std::nth_element(srt.begin(), srt.begin() + nblk / 2, srt.end());
+      const int T = nblk > 0 ? srt[nblk / 2] : 0;
+      const int mx = nblk > 0 ? *std::max_element(blen.begin(), blen.end()) : 0;
+      const bool want = ev ? ev[0] == '1' : size_t(mx) * 256 * sizeof(double) > 64 * 1024;
+      if (want && nblk > 0 && 2 * T <= mx) {
+        std::vector<int> sh, lo;
+        for (int b : order) (blen[b] <= T ? sh : lo).push_back(b);
+        if ((rc = upv(pk_blk_short, sh, "P_k short blocks")) ||
+            (rc = upv(pk_blk_long, lo, "P_k long blocks")))
+          return rc;
+        pkd.blk_short = pk_blk_short.p;
+        pkd.blk_long = pk_blk_long.p;
+        pkd.n_short = int(sh.size());
+        pkd.n_long = int(lo.size());
+        pkd.short_len = T;
+      }
+    }
     // ion-flux segments handled by this rank: those whose element is local and whose lower
     // global vertex is owned here, {local element, face, group}, in global segment order
     std::vector<int> eloc(m.nt, -1);

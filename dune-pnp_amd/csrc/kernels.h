@@ -403,6 +403,10 @@ struct PkDev {
   const uint32_t *islot = nullptr;
   double *eres = nullptr;  // [nl][ne] element residual rows of the two-pass residual-only launch
   double *ejac = nullptr;  // [ne][nl][W] element matrix + residual rows of the two-pass Jacobian
+  // the two-pass Jacobian's gather split: 256-row blocks whose rows have at most short_len slots
+  // (blk_short, in the blkmap order) and the others (blk_long); n_short 0: one launch
+  const int *blk_short = nullptr, *blk_long = nullptr;
+  int n_short = 0, n_long = 0, short_len = 0;
 };
 hipError_t pk_upload_tables(int k, hipStream_t s);
 // jac 0 residual, 1 analytic Jacobian, 2 forward-difference Jacobian (PNP_JAC_FD)

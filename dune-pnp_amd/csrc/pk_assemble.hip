@@ -881,6 +881,20 @@ hipError_t jac_launch2(const DevLayout &L, const PkDev &D, const double *x, cons
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
                      aux0, aux1, a);
+  if (D.n_short > 0) {
+    DevLayout Ls = L, Ll = L;
+    Ls.blkmap = D.blk_short;
+    Ls.blkcount = D.n_short;
+    Ll.blkmap = D.blk_long;
+    Ll.blkcount = D.n_long;
+    const size_t lds_s = size_t(D.short_len) * kB * sizeof(double);
+    hipLaunchKernelGGL(k_pk_jac_gather<K>, dim3(D.n_short), dim3(kB), lds_s, s, Ls, D, cvec_in,
+                       dmask, r, vals);
+    if (D.n_long > 0)
+      hipLaunchKernelGGL(k_pk_jac_gather<K>, dim3(D.n_long), dim3(kB), lds, s, Ll, D, cvec_in,
+                         dmask, r, vals);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_pk_jac_gather<K>, dim3((L.n_owned + kB - 1) / kB), dim3(kB), lds, s, L, D,
                      cvec_in, dmask, r, vals);
   return hipGetLastError();
