@@ -559,7 +559,7 @@ __global__ __launch_bounds__(kB) void k_pk_res_gather(DevLayout L, PkDev D, int 
 // instead of computed -- the same sums in the same order, so residual and matrix are k_pk_row's,
 // bit for bit.
 #ifndef PK_RG2
-#define PK_RG2 6  // A/B knob (build flag): element rows per register group of the P2 element pass
+#define PK_RG2 3  // A/B knob (build flag): element rows per register group of the P2 element pass
 #endif
 #ifndef PK_RG3
 #define PK_RG3 5  // the same at P3
@@ -693,6 +693,185 @@ __global__ __launch_bounds__(kB) void k_pk_elem_jac(PkDev D, const double *__res
       for (int w = 0; w < W / 2; w++) rec[w] = make_double2(v[2 * w], v[2 * w + 1]);
     }
   }
+}
+
+// k_pk_elem_jac with the element's node values consumed up front (PK_EJ_PRE): each quadrature
+// point's scalars (factor, u or its source terms, grad u, grad of the frozen field) go to LDS
+// first, so that the row groups hold only their matrix rows and the basis gradients and two waves
+// fit per SIMD (the one-wave kernel is issue-stalled on fp64 dependencies,
+// profiles/r02/pmc_sq_pk3_r2bb.txt).  The same statements on the same values: bitwise
+// k_pk_elem_jac's records.
+#ifndef PK_EJ_PRE
+#define PK_EJ_PRE 1
+#endif
+constexpr int kBE = 128;  // threads per workgroup of k_pk_elem_jac_pre (LDS: 32 doubles each)
+template <int K>
+__global__ __launch_bounds__(kBE) __attribute__((amdgpu_waves_per_eu(2)))
+void k_pk_elem_jac_pre(PkDev D, const double *__restrict__ xy, const double *__restrict__ x,
+                       const double *__restrict__ aux0, const double *__restrict__ aux1, PkArgs a) {
+  constexpr int NL = PkK<K>::NL, W = PkRec<K>::W, RG = PkRec<K>::RG;
+  __shared__ double qv[32][kBE];  // PB / Poisson: 4 x 5 at 0..19; DiffusionT: mass 7 x (u, f) at 0..13,
+                                  // then the diffusion's 3 x 6 at 14..31
+  const int ne = D.ne, e = blockIdx.x * kBE + threadIdx.x;
+  if (e >= ne) return;
+  double *my = &qv[0][threadIdx.x];
+#define QV(i) my[(i) * kBE]
+  const auto &T = tab<K>();
+  const double PI = a.pi;
+  PkGeo G;
+  {
+    int nd[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
+    const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
+    G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
+    double xl[NL], f0[NL], f1[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+      xl[i] = x[nd[i]];
+      f0[i] = aux0 ? aux0[nd[i]] : 0.0;
+      f1[i] = aux1 ? aux1[nd[i]] : 0.0;
+    }
+    if (a.kind == OP_DIFF_IE) {
+#pragma unroll 1
+      for (int q = 0; q < 7; q++) {
+        const auto &P = T.q5[q];
+        double u = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
+        QV(2 * q) = u;
+        QV(2 * q + 1) = P.w * G.adet;
+      }
+    }
+    if (a.kind == OP_PB || a.kind == OP_POISSON) {
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) {
+        const auto &P = T.q3[q];
+        double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+          double g0, g1;
+          grad(G, P, i, g0, g1);
+          u += xl[i] * P.phi[i];
+          gu0 += xl[i] * g0;
+          gu1 += xl[i] * g1;
+          if (a.kind == OP_POISSON) {
+            cp += f0[i] * P.phi[i];
+            cm += f1[i] * P.phi[i];
+          }
+        }
+        QV(5 * q) = factor(G, P, a.cyl, PI);
+        QV(1 + 5 * q) = gu0;
+        QV(2 + 5 * q) = gu1;
+        QV(3 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+        QV(4 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * cosh(u) : 0.0;
+      }
+    } else {
+#pragma unroll 1
+      for (int q = 0; q < 3; q++) {
+        const auto &P = T.q2[q];
+        double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+          double g0, g1;
+          grad(G, P, i, g0, g1);
+          u += xl[i] * P.phi[i];
+          gu0 += xl[i] * g0;
+          gu1 += xl[i] * g1;
+          gP0 += f0[i] * g0;
+          gP1 += f0[i] * g1;
+        }
+        QV(14 + 6 * q) = P.w * G.adet;
+        QV(15 + 6 * q) = gu0;
+        QV(16 + 6 * q) = gu1;
+        QV(17 + 6 * q) = u;
+        QV(18 + 6 * q) = gP0;
+        QV(19 + 6 * q) = gP1;
+      }
+    }
+  }
+  double *rec0 = D.ejac + size_t(e) * NL * W;
+#pragma unroll 1
+  for (int ra0 = 0; ra0 < NL; ra0 += RG) {
+    double r[RG], Jr[RG][NL];
+#pragma unroll
+    for (int j = 0; j < RG; j++) {
+      r[j] = 0.0;
+#pragma unroll
+      for (int b = 0; b < NL; b++) Jr[j][b] = 0.0;
+    }
+    if (a.kind == OP_DIFF_IE) {
+#pragma unroll 1
+      for (int q = 0; q < 7; q++) {
+        const auto &P = T.q5[q];
+        const double u = QV(2 * q), f = QV(2 * q + 1);
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          r[j] += u * P.phi[ra] * f;
+#pragma unroll
+          for (int b = 0; b < NL; b++) Jr[j][b] += P.phi[ra] * P.phi[b] * f;
+        }
+      }
+    }
+    if (a.kind == OP_PB || a.kind == OP_POISSON) {
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) {
+        const auto &P = T.q3[q];
+        const double f = QV(5 * q), gu0 = QV(1 + 5 * q), gu1 = QV(2 + 5 * q);
+        const double s = QV(3 + 5 * q), cb = QV(4 + 5 * q);
+        double g[NL][2];
+#pragma unroll
+        for (int i = 0; i < NL; i++) grad(G, P, i, g[i][0], g[i][1]);
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          const double c = a.kind == OP_PB ? cb * P.phi[ra] : 0.0;
+          double ga0, ga1;
+          grad(G, P, ra, ga0, ga1);
+          r[j] += (gu0 * ga0 + gu1 * ga1 + s * P.phi[ra]) * f;
+#pragma unroll
+          for (int b = 0; b < NL; b++) Jr[j][b] += (ga0 * g[b][0] + ga1 * g[b][1] + c * P.phi[b]) * f;
+        }
+      }
+    } else {
+      const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
+#pragma unroll 1
+      for (int q = 0; q < 3; q++) {
+        const auto &P = T.q2[q];
+        const double f = QV(14 + 6 * q), gu0 = QV(15 + 6 * q), gu1 = QV(16 + 6 * q);
+        const double u = QV(17 + 6 * q), gP0 = QV(18 + 6 * q), gP1 = QV(19 + 6 * q);
+        double g[NL][2];
+#pragma unroll
+        for (int i = 0; i < NL; i++) grad(G, P, i, g[i][0], g[i][1]);
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
+          double ga0, ga1;
+          grad(G, P, ra, ga0, ga1);
+          r[j] += sc * ((gu0 * ga0 + gu1 * ga1 + u * a.z * (gP0 * ga0 + gP1 * ga1) + 0.0 * u * P.phi[ra]) * f);
+          const double drift = a.z * (gP0 * ga0 + gP1 * ga1);
+#pragma unroll
+          for (int b = 0; b < NL; b++)
+            Jr[j][b] += sc * ((ga0 * g[b][0] + ga1 * g[b][1] + P.phi[b] * drift) * f);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RG; j++) {
+      if (ra0 + j >= NL) break;
+      double2 *rec = reinterpret_cast<double2 *>(rec0 + size_t(ra0 + j) * W);
+      double v[W];
+#pragma unroll
+      for (int b = 0; b < NL; b++) v[b] = Jr[j][b];
+      v[NL] = r[j];
+#pragma unroll
+      for (int b = NL + 1; b < W; b++) v[b] = 0.0;
+#pragma unroll
+      for (int w = 0; w < W / 2; w++) rec[w] = make_double2(v[2 * w], v[2 * w + 1]);
+    }
+  }
+#undef QV
 }
 
 // pass 2: one thread per owned row, k_pk_row's slot accumulation in LDS with each incidence's
@@ -879,8 +1058,12 @@ hipError_t jac_launch2(const DevLayout &L, const PkDev &D, const double *x, cons
     attr = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
-                     aux0, aux1, a);
+  if (PK_EJ_PRE)
+    hipLaunchKernelGGL(k_pk_elem_jac_pre<K>, dim3((D.ne + kBE - 1) / kBE), dim3(kBE), 0, s, D, L.xy,
+                       x, aux0, aux1, a);
+  else
+    hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
+                       aux0, aux1, a);
   if (D.n_short > 0) {
     DevLayout Ls = L, Ll = L;
     Ls.blkmap = D.blk_short;
