@@ -551,10 +551,9 @@ __global__ __launch_bounds__(kB) void k_pk_res_gather(DevLayout L, PkDev D, int 
 // Analytic Jacobian launches in two passes as well (PNP_PK_JAC2, default on).  Pass 1, one thread per
 // local element: each row ra of the element residual and matrix with pk_row_both's statements,
 // the quadrature point's basis gradients, u, grad u and source shared by RG rows at a time (RG
-// rows of the matrix in registers: all 6 at P2, 5 at P3), into one record of W doubles per
-// (element, row): the NL matrix entries, then the residual entry, padded to 16 B.  Measured
-// against one thread per (element, row group), and with register caps for more waves per SIMD
-// (profiles/r02/ab_pk_elem): both slower or spilling.
+// rows of the matrix in registers: 3 at P2, 5 at P3), into one record of W doubles per
+// (element, row): the NL matrix entries, then the residual entry, padded to 16 B.  One thread
+// per (element, row group) instead was slower (profiles/r02/ab_pk_elem).
 // Pass 2 (k_pk_jac_gather): k_pk_row's slot accumulation with each incidence's record read
 // instead of computed -- the same sums in the same order, so residual and matrix are k_pk_row's,
 // bit for bit.
@@ -569,145 +568,16 @@ struct PkRec {
   static constexpr int NL = PkK<K>::NL, W = (NL + 2) & ~1, RG = K == 2 ? PK_RG2 : PK_RG3;
 };
 
-template <int K>
-__global__ __launch_bounds__(kB) void k_pk_elem_jac(PkDev D, const double *__restrict__ xy,
-                                                    const double *__restrict__ x,
-                                                    const double *__restrict__ aux0,
-                                                    const double *__restrict__ aux1, PkArgs a) {
-  constexpr int NL = PkK<K>::NL, W = PkRec<K>::W, RG = PkRec<K>::RG;
-  const int ne = D.ne, e = blockIdx.x * kB + threadIdx.x;
-  if (e >= ne) return;
-  int nd[NL];
-#pragma unroll
-  for (int i = 0; i < NL; i++) nd[i] = D.enode[size_t(i) * ne + e];
-  const double2 *xy2 = reinterpret_cast<const double2 *>(xy);
-  const PkGeo G = pk_geometry(xy2[nd[0]], xy2[nd[1]], xy2[nd[2]]);
-  double xl[NL], f0[NL], f1[NL];
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    xl[i] = x[nd[i]];
-    f0[i] = aux0 ? aux0[nd[i]] : 0.0;
-    f1[i] = aux1 ? aux1[nd[i]] : 0.0;
-  }
-  const auto &T = tab<K>();
-  const double PI = a.pi;
-  double *rec0 = D.ejac + size_t(e) * NL * W;
-#pragma unroll 1
-  for (int ra0 = 0; ra0 < NL; ra0 += RG) {
-    double r[RG], Jr[RG][NL];
-#pragma unroll
-    for (int j = 0; j < RG; j++) {
-      r[j] = 0.0;
-#pragma unroll
-      for (int b = 0; b < NL; b++) Jr[j][b] = 0.0;
-    }
-    if (a.kind == OP_DIFF_IE) {
-#pragma unroll 1
-      for (int q = 0; q < 7; q++) {
-        const auto &P = T.q5[q];
-        double u = 0.0;
-#pragma unroll
-        for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
-        const double f = P.w * G.adet;
-#pragma unroll
-        for (int j = 0; j < RG; j++) {
-          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
-          r[j] += u * P.phi[ra] * f;
-#pragma unroll
-          for (int b = 0; b < NL; b++) Jr[j][b] += P.phi[ra] * P.phi[b] * f;
-        }
-      }
-    }
-    if (a.kind == OP_PB || a.kind == OP_POISSON) {
-#pragma unroll 1
-      for (int q = 0; q < 4; q++) {
-        const auto &P = T.q3[q];
-        const double f = factor(G, P, a.cyl, PI);
-        double g[NL][2];
-        double u = 0.0, gu0 = 0.0, gu1 = 0.0, cp = 0.0, cm = 0.0;
-#pragma unroll
-        for (int i = 0; i < NL; i++) {
-          grad(G, P, i, g[i][0], g[i][1]);
-          u += xl[i] * P.phi[i];
-          gu0 += xl[i] * g[i][0];
-          gu1 += xl[i] * g[i][1];
-          if (a.kind == OP_POISSON) {
-            cp += f0[i] * P.phi[i];
-            cm += f1[i] * P.phi[i];
-          }
-        }
-        const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
-        const double ch = a.kind == OP_PB ? cosh(u) : 0.0;
-#pragma unroll
-        for (int j = 0; j < RG; j++) {
-          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
-          const double c = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * ch * P.phi[ra] : 0.0;
-          double ga0, ga1;
-          grad(G, P, ra, ga0, ga1);
-          r[j] += (gu0 * ga0 + gu1 * ga1 + s * P.phi[ra]) * f;
-#pragma unroll
-          for (int b = 0; b < NL; b++) Jr[j][b] += (ga0 * g[b][0] + ga1 * g[b][1] + c * P.phi[b]) * f;
-        }
-      }
-    } else {
-      const double sc = a.kind == OP_DIFF_IE ? a.dt : 1.0;
-#pragma unroll 1
-      for (int q = 0; q < 3; q++) {
-        const auto &P = T.q2[q];
-        double g[NL][2];
-        double u = 0.0, gu0 = 0.0, gu1 = 0.0, gP0 = 0.0, gP1 = 0.0;
-#pragma unroll
-        for (int i = 0; i < NL; i++) {
-          grad(G, P, i, g[i][0], g[i][1]);
-          u += xl[i] * P.phi[i];
-          gu0 += xl[i] * g[i][0];
-          gu1 += xl[i] * g[i][1];
-          gP0 += f0[i] * g[i][0];
-          gP1 += f0[i] * g[i][1];
-        }
-        const double f = P.w * G.adet;
-#pragma unroll
-        for (int j = 0; j < RG; j++) {
-          const int ra = ra0 + j < NL ? ra0 + j : NL - 1;
-          double ga0, ga1;
-          grad(G, P, ra, ga0, ga1);
-          r[j] += sc * ((gu0 * ga0 + gu1 * ga1 + u * a.z * (gP0 * ga0 + gP1 * ga1) + 0.0 * u * P.phi[ra]) * f);
-          const double drift = a.z * (gP0 * ga0 + gP1 * ga1);
-#pragma unroll
-          for (int b = 0; b < NL; b++)
-            Jr[j][b] += sc * ((ga0 * g[b][0] + ga1 * g[b][1] + P.phi[b] * drift) * f);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < RG; j++) {
-      if (ra0 + j >= NL) break;
-      double2 *rec = reinterpret_cast<double2 *>(rec0 + size_t(ra0 + j) * W);
-      double v[W];
-#pragma unroll
-      for (int b = 0; b < NL; b++) v[b] = Jr[j][b];
-      v[NL] = r[j];
-#pragma unroll
-      for (int b = NL + 1; b < W; b++) v[b] = 0.0;
-#pragma unroll
-      for (int w = 0; w < W / 2; w++) rec[w] = make_double2(v[2 * w], v[2 * w + 1]);
-    }
-  }
-}
-
-// k_pk_elem_jac with the element's node values consumed up front (PK_EJ_PRE): each quadrature
-// point's scalars (factor, u or its source terms, grad u, grad of the frozen field) go to LDS
-// first, so that the row groups hold only their matrix rows and the basis gradients and two waves
-// fit per SIMD (the one-wave kernel is issue-stalled on fp64 dependencies,
-// profiles/r02/pmc_sq_pk3_r2bb.txt).  The same statements on the same values: bitwise
-// k_pk_elem_jac's records.
-#ifndef PK_EJ_PRE
-#define PK_EJ_PRE 1
-#endif
-constexpr int kBE = 128;  // threads per workgroup of k_pk_elem_jac_pre (LDS: 32 doubles each)
+// The element pass consumes the element's node values up front: each quadrature point's scalars
+// (factor, u or its source terms, grad u, grad of the frozen field) go to LDS first, so that the
+// row groups hold only their matrix rows and the basis gradients and two waves fit per SIMD.
+// Holding the node values and the rows in registers together (396 VGPRs at P3, one wave per
+// SIMD) left the kernel issue-stalled on fp64 dependencies, P2 134 / P3 390 us against 116 / 350
+// (profiles/r02/pmc_sq_pk3_r2bb.txt, ab_pk_elem_pre/).
+constexpr int kBE = 128;  // threads per workgroup of k_pk_elem_jac (LDS: 32 doubles each)
 template <int K>
 __global__ __launch_bounds__(kBE) __attribute__((amdgpu_waves_per_eu(2)))
-void k_pk_elem_jac_pre(PkDev D, const double *__restrict__ xy, const double *__restrict__ x,
+void k_pk_elem_jac(PkDev D, const double *__restrict__ xy, const double *__restrict__ x,
                        const double *__restrict__ aux0, const double *__restrict__ aux1, PkArgs a) {
   constexpr int NL = PkK<K>::NL, W = PkRec<K>::W, RG = PkRec<K>::RG;
   __shared__ double qv[32][kBE];  // PB / Poisson: 4 x 5 at 0..19; DiffusionT: mass 7 x (u, f) at 0..13,
@@ -1058,12 +928,8 @@ hipError_t jac_launch2(const DevLayout &L, const PkDev &D, const double *x, cons
     attr = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (PK_EJ_PRE)
-    hipLaunchKernelGGL(k_pk_elem_jac_pre<K>, dim3((D.ne + kBE - 1) / kBE), dim3(kBE), 0, s, D, L.xy,
-                       x, aux0, aux1, a);
-  else
-    hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kB - 1) / kB), dim3(kB), 0, s, D, L.xy, x,
-                       aux0, aux1, a);
+  hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kBE - 1) / kBE), dim3(kBE), 0, s, D, L.xy, x,
+                     aux0, aux1, a);
   if (D.n_short > 0) {
     DevLayout Ls = L, Ll = L;
     Ls.blkmap = D.blk_short;
