@@ -679,17 +679,25 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
   // 53.5 -> 60-63 us, cache-cold 87 -> 77.7 us (profiles/r02/ab_asm_lds2.log): the barrier costs
   // more than the halved gathers save while the inputs sit in the Infinity Cache, and less when
   // they come from HBM.  Off by default (the back-to-back assembly is the benchmark's number).
-  static const bool lds_env = [] {
+  // Past the Infinity Cache (config 5, 8.87M DOF) every launch is cache-cold, so the Jacobian
+  // assembly takes the LDS-staged walk there by default: its k-form write stream (~7 blocks per
+  // row on triangle meshes) larger than the 256 MiB Infinity Cache (profiles/r02/ab_cfg5_lds.log).
+  // PNP_ASM_LDS=0 / 1 forces either walk.
+  static const int lds_env = [] {
     const char *e = getenv("PNP_ASM_LDS");
-    return e && atoi(e) == 1;
+    return e ? (atoi(e) == 1 ? 1 : 0) : -1;
   }();
+  const auto lds_walk = [&](int nk) {
+    return lds_env == 1 ||
+           (lds_env < 0 && size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(256) << 20));
+  };
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
     if (!fanr && a.jac)                                                            \
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
     else if (!fanr)                                                                \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
-    else if (!a.jac && fanr == 9 && ga && lds_env && L.uptr &&                      \
+    else if (!a.jac && fanr == 9 && ga && lds_env == 1 && L.uptr &&                 \
              size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9, 9, 0, 1>), grid, block,         \
                          size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
@@ -703,7 +711,7 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
-    else if (ga == 4 && fanr == 9 && lds_env && L.uptr &&                           \
+    else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uptr &&       \
              size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \
                          size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
