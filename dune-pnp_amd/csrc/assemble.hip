@@ -679,17 +679,19 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
   // 53.5 -> 60-63 us, cache-cold 87 -> 77.7 us (profiles/r02/ab_asm_lds2.log): the barrier costs
   // more than the halved gathers save while the inputs sit in the Infinity Cache, and less when
   // they come from HBM.  Off by default (the back-to-back assembly is the benchmark's number).
-  // Past the Infinity Cache (config 5, 8.87M DOF) every launch is cache-cold, so the Jacobian
-  // assembly takes the LDS-staged walk there by default: its k-form write stream (~7 blocks per
-  // row on triangle meshes) larger than the 256 MiB Infinity Cache (profiles/r02/ab_cfg5_lds.log).
-  // PNP_ASM_LDS=0 / 1 forces either walk.
+  // Well past the Infinity Cache every launch is cache-cold, so the Jacobian assembly takes the
+  // LDS-staged walk there by default: its k-form write stream (~7 blocks per row on triangle
+  // meshes) larger than twice the 256 MiB Infinity Cache.  Config 5 (828 MB): 344.8 -> 319.5 us
+  // (profiles/r02/ab_cfg5_lds.log); config 2 (311 MB, still partly cache-resident back to back):
+  // 79 -> 84 us, so the direct walk below 512 MiB (ab_cfg2_lds.log).  PNP_ASM_LDS=0 / 1 forces
+  // either walk.
   static const int lds_env = [] {
     const char *e = getenv("PNP_ASM_LDS");
     return e ? (atoi(e) == 1 ? 1 : 0) : -1;
   }();
   const auto lds_walk = [&](int nk) {
     return lds_env == 1 ||
-           (lds_env < 0 && size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(256) << 20));
+           (lds_env < 0 && size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(512) << 20));
   };
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
