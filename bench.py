@@ -282,6 +282,10 @@ def measure(ctx, mesh, args, prec, dist, world):
         ctx.assemble_state(1)
         ctx.timers(enable=False)
     tm_cold = ctx.timers()
+    # the warm roofline's launch time: one event pair around K back-to-back launches (the per-launch
+    # event pairs above add ~3 us each, r2bj: 50.2 us against rocprofv3's 47.4 us)
+    ctx.assemble_state(2)
+    asm_batch_s = ctx.assemble_state_timed(args.steps) / args.steps
     t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
 
     nf = 3
@@ -289,7 +293,8 @@ def measure(ctx, mesh, args, prec, dist, world):
     N_local = 3 * info["nv_owned"]
     T_local = int(round(mesh.nt * info["nv_owned"] / mesh.nv))
     B = byte_models(info, nf, N_local, T_local, prec)
-    asm_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
+    asm_ev_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
+    asm_s = asm_batch_s
     asm_cold_s = tm_cold["assemble_ms"] / max(1, tm_cold["assemble_launches"]) / 1e3
     it_ev = (tm["spmv_ms"] + tm["prec_ms"] + tm["blas_ms"] + tm["halo_ms"] +
              tm["allreduce_ms"]) / 1e3 / args.bicg_iters
@@ -304,6 +309,7 @@ def measure(ctx, mesh, args, prec, dist, world):
         "dofs_per_s": N_global * args.steps / t_asm,
         "iters_per_s": args.steps * args.bicg_iters / t_bicg,
         "asm_warm": rl(B["asm"], asm_s), "asm_cold": rl(B["asm"], asm_cold_s),
+        "asm_warm_per_launch_events_s": asm_ev_s,
         "it_contract": rl(B["it_contract"], it_ev), "it_stored": rl(B["it_stored"], it_ev),
         "spmv_stored": rl(B["spmv_stored"], spmv_s),
         "ilu_stored": rl(B["ilu_stored"], prec_s) if prec != P.PREC_NONE else None,
@@ -499,6 +505,10 @@ def main():
                                            "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
                          "bytes_per_launch": aw["bytes"], "avg_launch_us": aw["seconds"] * 1e6,
+                         "timing": "one HIP event pair on the library stream around K back-to-"
+                                   "back launches",
+                         "avg_launch_us_per_launch_events":
+                             M["asm_warm_per_launch_events_s"] * 1e6,
                          "note": "warm: back-to-back launches, the matrix write stream stays in "
                                  "the Infinity Cache at config 3; see roofline_cold"},
             "roofline_cold": {"bound": "hbm", "achieved": ac["achieved"], "peak": HBM_PEAK_GBS,

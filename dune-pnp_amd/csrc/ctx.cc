@@ -2686,6 +2686,30 @@ extern "C" int pnp_assemble_state(pnp_ctx *c, int32_t n) {
   return PNP_OK;
 }
 
+extern "C" int pnp_assemble_state_timed(pnp_ctx *c, int32_t n, double *ms) {
+  if (!c || !ms || n == 0) return PNP_E_ARG;
+  hipSetDevice(c->device);
+  // one event pair around the whole batch (no per-launch events inside it): the device time of
+  // |n| back-to-back launches, as a kernel trace sees them
+  const bool timing = c->timing;
+  c->timing = false;
+  hipEvent_t e0 = c->ev_get(), e1 = c->ev_get();
+  hipEventRecord(e0, c->stream);
+  int rc = PNP_OK;
+  for (int k = 0; k < (n >= 0 ? n : -n) && rc == PNP_OK; k++) rc = c->assemble(c->x.p, n >= 0);
+  hipEventRecord(e1, c->stream);
+  c->timing = timing;
+  const hipError_t e = hipStreamSynchronize(c->stream);
+  float t = 0;
+  if (rc == PNP_OK && e == hipSuccess) hipEventElapsedTime(&t, e0, e1);
+  c->ev_pool.push_back(e0);
+  c->ev_pool.push_back(e1);
+  if (rc) return rc;
+  CK(e, "assemble_state_timed");
+  *ms = t;
+  return PNP_OK;
+}
+
 extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_solve_result *res) {
   if (!c || !res || n <= 0) return PNP_E_ARG;
   hipSetDevice(c->device);

@@ -631,6 +631,12 @@ class Context:
     def assemble_state(self, n=1):
         self._ck(lib().pnp_assemble_state(self.h, int(n)))
 
+    def assemble_state_timed(self, n=1):
+        """n assemblies of the state; returns their device time (s) from one event pair."""
+        ms = C.c_double()
+        self._ck(lib().pnp_assemble_state_timed(self.h, int(n), C.byref(ms)))
+        return ms.value / 1e3
+
     def bicgstab_iterations(self, n, prec=PREC_NONE):
         r = _SolveResult()
         self._ck(lib().pnp_bicgstab_iterations(self.h, int(n), int(prec), C.byref(r)))

@@ -405,6 +405,8 @@ int pnp_state_set(pnp_ctx *ctx, const double *x);
 int pnp_state_get(pnp_ctx *ctx, double *x);
 /* n fused residual+Jacobian assemblies of the state vector, on the device */
 int pnp_assemble_state(pnp_ctx *ctx, int32_t n);  /* n < 0: |n| residual-only assemblies */
+/* the same, with the device time of the whole batch from one HIP event pair around it (ms) */
+int pnp_assemble_state_timed(pnp_ctx *ctx, int32_t n, double *ms);
 /* n BiCGSTAB iterations (no convergence stop) on J z = r of the last assembly */
 int pnp_bicgstab_iterations(pnp_ctx *ctx, int32_t n, int32_t prec, pnp_solve_result *res);
 
