@@ -183,6 +183,14 @@ struct pnp_ctx {
   DBuf<int> csr_rowptr, csr_col, csr_src;
   DBuf<unsigned char> csr_vidx;
   DBuf<double> csr_val;
+  bool csr_vals_valid = false;  // csr_val holds the current Jacobian
+  // natural-order SSOR (PNP_PREC_SSOR_NATURAL, ssor_natural.hip): level schedule of the forward
+  // and backward sweeps over the external-layout rows (built with the CSR structure), the
+  // position of each row's diagonal, and external-layout work vectors
+  std::vector<int> nat_lptr_f, nat_lptr_b;
+  DBuf<int> nat_rows_f, nat_rows_b, nat_diag;
+  DBuf<double> nat_d, nat_v;
+  int nat_pat = -1, nat_nf = 0;
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
   // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
   // global segment order
@@ -215,6 +223,8 @@ struct pnp_ctx {
 
   // vectors (sized n_local * 3)
   DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials, partials2;
+  std::vector<int> newton_its;        // pnp_newton_history: linear iterations per Newton step
+  std::vector<double> newton_defects; // and the defect after each step
   DBuf<pnp::Scalars> S;
   pnp::Scalars *hS = nullptr;  // pinned host mirror
 
@@ -607,8 +617,140 @@ struct pnp_ctx {
       lu_valid = false;
       split_of = 0;
       amg_valid = false;
+      csr_vals_valid = false;
     }
     return PNP_OK;
+  }
+
+  // structure of the external-layout CSR view of the current block pattern (host, once per
+  // pattern): rows f*nv + g of the owned vertices, columns sorted; per entry the source block
+  // (row << 6 | slot) and the value's index in the block pattern.  Also the natural-order SSOR
+  // level schedule over these rows.
+  int csr_structure() {
+    const int nv = mesh.nv, mask = pat & 0x1FF;
+    if (csr_pat == mask && csr_nf == nf) return PNP_OK;
+    const int n = nf * nv;
+    std::vector<int> cnt(n + 1, 0);
+    for (int i = 0; i < L.n_owned; i++) {
+      const int len = pnp::meta_len(L.rowmeta[i]);
+      for (int f = 0; f < nf; f++) {
+        int k = 0;
+        for (int g = 0; g < nf; g++) k += pnp::pat_index(mask, f, g) >= 0;
+        cnt[f * nv + L.l2g[i] + 1] += k * len;
+      }
+    }
+    for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+    const long long nnz = cnt[n];
+    std::vector<int> col(nnz), src(nnz);
+    std::vector<unsigned char> vid(nnz);
+    struct E {
+      int col, src;
+      unsigned char v;
+    };
+    std::vector<E> tmp;
+    for (int i = 0; i < L.n_owned; i++) {
+      const int chunk = i / pnp::kRows, lane = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
+      for (int f = 0; f < nf; f++) {
+        tmp.clear();
+        for (int sl = 0; sl < len; sl++) {
+          const int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(sl) * pnp::kRows + lane];
+          for (int g = 0; g < nf; g++) {
+            const int v = pnp::pat_index(mask, f, g);
+            if (v >= 0) tmp.push_back({g * nv + L.l2g[j], i << 6 | sl, (unsigned char)v});
+          }
+        }
+        std::sort(tmp.begin(), tmp.end(), [](const E &a, const E &b) { return a.col < b.col; });
+        long long q = cnt[f * nv + L.l2g[i]];
+        for (const E &e : tmp) {
+          col[q] = e.col;
+          src[q] = e.src;
+          vid[q] = e.v;
+          q++;
+        }
+      }
+    }
+    int rc;
+    if ((rc = upv(csr_rowptr, cnt, "csr rowptr")) || (rc = upv(csr_col, col, "csr col")) ||
+        (rc = upv(csr_src, src, "csr src")) || (rc = upv(csr_vidx, vid, "csr vidx")))
+      return rc;
+    hipError_t e = csr_val.alloc(std::max<long long>(1, nnz));
+    if (e != hipSuccess) return hipfail(e, "csr values");
+    // natural-order SSOR schedule.  A row R must run after every row it shares a matrix entry with
+    // (A_RC or A_CR stored) that comes before it in the sweep, and before every such later row:
+    // level(R) = 1 + max level of its earlier partners, computed in sweep order with the partners
+    // of the transposed entries pushed forward.  Rows of other ranks' vertices are empty and stay
+    // out (their columns read zero).
+    auto empty = [&](int R) { return cnt[R] == cnt[R + 1]; };
+    std::vector<int> diag(n, -1);
+    for (int R = 0; R < n; R++)
+      for (int k = cnt[R]; k < cnt[R + 1]; k++)
+        if (col[k] == R) diag[R] = k;
+    for (int R = 0; R < n; R++)
+      if (!empty(R) && diag[R] < 0) return fail(PNP_E_STATE, "natural SSOR: row without diagonal");
+    auto schedule = [&](bool fwd, std::vector<int> &lptr, DBuf<int> &rows) -> int {
+      std::vector<int> lev(n, -1), push(n, 0);
+      int nlev = 0;
+      for (int s = 0; s < n; s++) {
+        const int R = fwd ? s : n - 1 - s;
+        if (empty(R)) continue;
+        int l = push[R];
+        for (int k = cnt[R]; k < cnt[R + 1]; k++) {
+          const int C = col[k];
+          if (C != R && (fwd ? C < R : C > R) && !empty(C)) l = std::max(l, lev[C] + 1);
+        }
+        lev[R] = l;
+        nlev = std::max(nlev, l + 1);
+        for (int k = cnt[R]; k < cnt[R + 1]; k++) {
+          const int C = col[k];
+          if (C != R && (fwd ? C > R : C < R) && !empty(C)) push[C] = std::max(push[C], l + 1);
+        }
+      }
+      lptr.assign(nlev + 1, 0);
+      for (int R = 0; R < n; R++)
+        if (lev[R] >= 0) lptr[lev[R] + 1]++;
+      for (int l = 0; l < nlev; l++) lptr[l + 1] += lptr[l];
+      std::vector<int> fill(lptr.begin(), lptr.end() - 1), rl(std::max(1, lptr[nlev]));
+      for (int R = 0; R < n; R++)
+        if (lev[R] >= 0) rl[fill[lev[R]]++] = R;
+      return upv(rows, rl, "natural SSOR rows");
+    };
+    if ((rc = schedule(true, nat_lptr_f, nat_rows_f)) ||
+        (rc = schedule(false, nat_lptr_b, nat_rows_b)) || (rc = upv(nat_diag, diag, "ssor diag")))
+      return rc;
+    if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess)
+      return hipfail(e, "natural SSOR vectors");
+    csr_nnz = nnz;
+    csr_pat = mask;
+    csr_nf = nf;
+    csr_vals_valid = false;
+    return PNP_OK;
+  }
+
+  // the CSR view's values from the current k-form matrix (once per assembly)
+  int csr_values() {
+    int rc;
+    if ((rc = csr_structure())) return rc;
+    if (csr_vals_valid) return PNP_OK;
+    hipError_t e = pnp::launch_csr_fill(dl, nf, pat, vals.p, csr_nnz, csr_src.p, csr_vidx.p,
+                                        csr_val.p, stream);
+    if (e != hipSuccess) return hipfail(e, "csr fill");
+    csr_vals_valid = true;
+    return PNP_OK;
+  }
+
+  // v = SSOR_natural^{-1} d on internal-layout owned rows (ssor_natural.hip); csr_values() first
+  hipError_t ssor_natural(const double *d, double *vout) {
+    const int nv = mesh.nv;
+    hipError_t e = hipMemsetAsync(nat_v.p, 0, sizeof(double) * nat_v.n, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_ssor_natural(int(nat_lptr_f.size()) - 1, nat_lptr_f.data(), nat_rows_f.p,
+                                   int(nat_lptr_b.size()) - 1, nat_lptr_b.data(), nat_rows_b.p,
+                                   csr_rowptr.p, csr_col.p, csr_val.p, nat_diag.p, nat_d.p,
+                                   nat_v.p, stream);
+    if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
+    return e;
   }
 
   // analytic (k-form) or forward-difference (expanded, kPat*FD) storage of the next Jacobian
@@ -953,6 +1095,7 @@ struct pnp_ctx {
     }
     const int sm = amg_opts.smoother;
     if (sm == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (sm == PNP_PREC_SSOR_NATURAL && (rc = csr_values())) return rc;
     if (sm == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     if (amg_valid) return PNP_OK;
     hipEvent_t t0 = tb(T_FACT);
@@ -1077,6 +1220,8 @@ struct pnp_ctx {
     } else if (prec == PNP_PREC_ILU0) {
       e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout,
                                  stream, 0, nullptr, nullptr, f32_now());
+    } else if (prec == PNP_PREC_SSOR_NATURAL) {
+      e = ssor_natural(d, vout);
     } else {
       e = hipMemcpyAsync(vout, d, sizeof(double) * nown(), hipMemcpyDeviceToDevice, stream);
     }
@@ -1087,6 +1232,7 @@ struct pnp_ctx {
   int precond(int prec, const double *d, double *vout) {
     int rc;
     if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (prec == PNP_PREC_SSOR_NATURAL && (rc = csr_values())) return rc;
     if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     if (prec == PNP_PREC_AMG && (rc = amg_setup())) return rc;
     hipEvent_t t0 = tb(T_PREC);
@@ -1140,6 +1286,7 @@ struct pnp_ctx {
     int prec = o.prec;
     if (prec == PNP_PREC_ILU0 && ((rc = ilu_factor()) || (rc = split(2)))) return rc;
     if (prec == PNP_PREC_SSOR && (rc = split(1))) return rc;
+    if (prec == PNP_PREC_SSOR_NATURAL && (rc = csr_values())) return rc;
     if (prec == PNP_PREC_AMG && (rc = amg_setup())) return rc;
     int nsp = 0, npu = 0;
     // ILU(0): the two vector updates that feed the preconditioner also do colour 0 of its
@@ -2014,6 +2161,7 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   c->lu_valid = false;
   c->split_of = 0;
   c->amg_valid = false;
+  c->csr_vals_valid = false;
   // SELL padding slots point at the row itself and are never written by the assembly, so they
   // must hold zeros in the k-form layout of THIS operator (the SpMV multiplies them)
   CK(hipMemsetAsync(c->vals.p, 0, sizeof(double) * size_t(c->L.nslots) * c->nks, c->stream),
@@ -2250,63 +2398,10 @@ extern "C" int pnp_jacobian_csr_device(pnp_ctx *c, pnp_csr_view *out) {
   if (!c || !out) return PNP_E_ARG;
   if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
   hipSetDevice(c->device);
-  const pnp::LocalLayout &L = c->L;
-  const int nf = c->nf, nv = c->mesh.nv, mask = c->pat & 0x1FF;
-  if (c->csr_pat != mask || c->csr_nf != nf) {  // structure of this block pattern (host, once)
-    const int n = nf * nv;
-    std::vector<int> cnt(n + 1, 0);
-    for (int i = 0; i < L.n_owned; i++) {
-      const int len = pnp::meta_len(L.rowmeta[i]);
-      for (int f = 0; f < nf; f++) {
-        int k = 0;
-        for (int g = 0; g < nf; g++) k += pnp::pat_index(mask, f, g) >= 0;
-        cnt[f * nv + L.l2g[i] + 1] += k * len;
-      }
-    }
-    for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
-    const long long nnz = cnt[n];
-    std::vector<int> col(nnz), src(nnz);
-    std::vector<unsigned char> vid(nnz);
-    struct E {
-      int col, src;
-      unsigned char v;
-    };
-    std::vector<E> tmp;
-    for (int i = 0; i < L.n_owned; i++) {
-      const int chunk = i / pnp::kRows, lane = i % pnp::kRows, len = pnp::meta_len(L.rowmeta[i]);
-      for (int f = 0; f < nf; f++) {
-        tmp.clear();
-        for (int sl = 0; sl < len; sl++) {
-          const int j = L.colidx[size_t(L.chunk_off[chunk]) + size_t(sl) * pnp::kRows + lane];
-          for (int g = 0; g < nf; g++) {
-            const int v = pnp::pat_index(mask, f, g);
-            if (v >= 0) tmp.push_back({g * nv + L.l2g[j], i << 6 | sl, (unsigned char)v});
-          }
-        }
-        std::sort(tmp.begin(), tmp.end(), [](const E &a, const E &b) { return a.col < b.col; });
-        long long q = cnt[f * nv + L.l2g[i]];
-        for (const E &e : tmp) {
-          col[q] = e.col;
-          src[q] = e.src;
-          vid[q] = e.v;
-          q++;
-        }
-      }
-    }
-    int rc;
-    if ((rc = c->upv(c->csr_rowptr, cnt, "csr rowptr")) || (rc = c->upv(c->csr_col, col, "csr col")) ||
-        (rc = c->upv(c->csr_src, src, "csr src")) || (rc = c->upv(c->csr_vidx, vid, "csr vidx")))
-      return rc;
-    CK(c->csr_val.alloc(std::max<long long>(1, nnz)), "csr values");
-    c->csr_nnz = nnz;
-    c->csr_pat = mask;
-    c->csr_nf = nf;
-  }
-  CK(pnp::launch_csr_fill(c->dl, nf, c->pat, c->vals.p, c->csr_nnz, c->csr_src.p, c->csr_vidx.p,
-                          c->csr_val.p, c->stream),
-     "csr fill");
+  int rc;
+  if ((rc = c->csr_values())) return rc;
   CK(hipStreamSynchronize(c->stream), "csr fill");
-  out->n = nf * nv;
+  out->n = c->nf * c->mesh.nv;
   out->nnz = c->csr_nnz;
   out->rowptr = c->csr_rowptr.p;
   out->col = c->csr_col.p;
@@ -2330,7 +2425,7 @@ extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const 
 }
 
 extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double *v) {
-  if (!c || !d || !v || prec < PNP_PREC_NONE || prec > PNP_PREC_AMG) return PNP_E_ARG;
+  if (!c || !d || !v || prec < PNP_PREC_NONE || prec > PNP_PREC_SSOR_NATURAL) return PNP_E_ARG;
   if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
   hipSetDevice(c->device);
   int rc;
@@ -2412,8 +2507,9 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
 
 extern "C" int pnp_amg_configure(pnp_ctx *c, const pnp_amg_opts *o) {
   if (!c || !o) return PNP_E_ARG;
-  if (o->smoother != PNP_PREC_SSOR && o->smoother != PNP_PREC_ILU0 && o->smoother != PNP_PREC_JACOBI)
-    return c->fail(PNP_E_ARG, "AMG smoother must be SSOR, ILU0 or JACOBI");
+  if (o->smoother != PNP_PREC_SSOR && o->smoother != PNP_PREC_ILU0 &&
+      o->smoother != PNP_PREC_JACOBI && o->smoother != PNP_PREC_SSOR_NATURAL)
+    return c->fail(PNP_E_ARG, "AMG smoother must be SSOR, SSOR_NATURAL, ILU0 or JACOBI");
   if (o->coarse_target < 1 || o->coarse_target > pnp::kAmgMaxCoarse || o->max_levels < 2 ||
       o->max_levels > pnp::kAmgMaxLevels || !(o->omega > 0 && o->omega <= 2) ||
       o->coarse_sweeps < 1 || o->coarse_sweeps > 8 || o->level0_presmooth < -1 ||
@@ -2510,6 +2606,8 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
   if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
   hipSetDevice(c->device);
   std::memset(res, 0, sizeof *res);
+  c->newton_its.clear();
+  c->newton_defects.clear();
   double t_start = now_s();
   int rc;
   long long n = c->nown();
@@ -2549,6 +2647,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
     double ts = now_s();
     if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
     res->linear_iterations += sr.iterations;
+    int step_its = sr.iterations;
     if (lo.prec == PNP_PREC_AMG && c->amg_fallback && (sr.breakdown || !sr.converged)) {
       // AMG fallback: the V-cycle of a non-symmetric system can fail where its level-0
       // smoother alone converges (a far-from-converged state); redo this step's solve with the
@@ -2558,6 +2657,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
          "rhs");
       if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
       res->linear_iterations += sr.iterations;
+      step_its += sr.iterations;
       res->linear_fallbacks++;
     }
     res->solve_seconds += now_s() - ts;
@@ -2608,10 +2708,24 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
       break;
     }
     res->iterations++;
+    c->newton_its.push_back(step_its);
+    c->newton_defects.push_back(defect);
   }
   res->defect = defect;
   if ((rc = c->download_ext(c->x.p, c->nf, u))) return rc;
   res->elapsed = now_s() - t_start;
+  return PNP_OK;
+}
+
+extern "C" int pnp_newton_history(pnp_ctx *c, int32_t *its, double *defects, int32_t cap,
+                                  int32_t *nsteps) {
+  if (!c || !nsteps || cap < 0) return PNP_E_ARG;
+  const int n = int(c->newton_its.size());
+  *nsteps = n;
+  for (int k = 0; k < std::min(n, int(cap)); k++) {
+    if (its) its[k] = c->newton_its[k];
+    if (defects) defects[k] = c->newton_defects[k];
+  }
   return PNP_OK;
 }
 

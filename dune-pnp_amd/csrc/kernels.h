@@ -388,6 +388,14 @@ hipError_t launch_fd_jacobian(const DevLayout &L, const AsmArgs &aa, int nf, int
 // slot), expanded and row-masked (pnp_jacobian_csr_device)
 hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *vals, long long nnz,
                            const int *src, const unsigned char *vidx, double *out, hipStream_t s);
+// ISTL SeqSSOR (k = 1, omega = 1) in the lexicographic DOF order (ssor_natural.hip): v = 0, then
+// the forward levels (lptr_f: nlev_f + 1 offsets into rows_f, host array) and the backward levels,
+// one launch per level; rowptr / col / val / diag: the external-layout CSR of the local matrix,
+// d / v external-layout vectors
+hipError_t launch_ssor_natural(int nlev_f, const int *lptr_f, const int *rows_f, int nlev_b,
+                               const int *lptr_b, const int *rows_b, const int *rowptr,
+                               const int *col, const double *val, const int *diag, const double *d,
+                               double *v, hipStream_t s);
 // read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
 hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 

@@ -7,9 +7,12 @@
 //                                                 ion current to current.dat)
 //
 // usage: pnp_main <config.cfg> [--refine k] [--mode stationary|instationary|md|pb] [--steps n]
-//                 [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec ...] [--amg-smoother s]
+//                 [--prec none|ssor|ssor_natural|jacobi|ilu0|amg] [--pb-prec ...] [--amg-smoother s]
 //                 [--device d] [--out prefix]
-//                 [--md-reduction r] [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]
+//                 [--md-reduction r]
+//                 [--linear-solver bcgs_ssork|bcgs_ssork_mc|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]
+//                 (bcgs_ssork, the reference's default: ISTL SeqSSOR in the lexicographic order,
+//                  PNP_PREC_SSOR_NATURAL; bcgs_ssork_mc: the multicolour sweep, same method, other order)
 //                 [--degree k]   (md / pb modes: PDEGREE, src/instationary_pnp_from_pb_md.hh:26-28;
 //                                 the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111)
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
@@ -32,6 +35,7 @@ using V = std::vector<double>;
 static int prec_of(const std::string &s) {
   if (s == "none" || s == "nonprec") return PNP_PREC_NONE;
   if (s == "ssor") return PNP_PREC_SSOR;
+  if (s == "ssor_natural") return PNP_PREC_SSOR_NATURAL;  // ISTL SeqSSOR in the reference's order
   if (s == "jacobi") return PNP_PREC_JACOBI;
   if (s == "ilu0") return PNP_PREC_ILU0;
   if (s == "amg") return PNP_PREC_AMG;  // level-0 smoother: --amg-smoother (PB: ssor, PNP: ilu0)
@@ -41,10 +45,11 @@ static int prec_of(const std::string &s) {
 static void usage() {
   std::printf(
       "usage: pnp_main <config.cfg> [--refine k] [--mesh-scale s] [--mode stationary|instationary|md|pb]\n"
-      "                [--steps n] [--prec none|ssor|jacobi|ilu0|amg] [--pb-prec p] [--device d]\n"
+      "                [--steps n] [--prec none|ssor|ssor_natural|jacobi|ilu0|amg] [--pb-prec p]\n"
+      "                [--device d]\n"
       "                [--amg-smoother ssor|ilu0|jacobi]\n"
       "                [--out prefix] [--md-reduction r]\n"
-      "                [--linear-solver bcgs_ssork|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
+      "                [--linear-solver bcgs_ssork|bcgs_ssork_mc|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
       "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n");
 }
 
@@ -331,8 +336,11 @@ int main(int argc, char **argv) {
       }
     } else if (mode == "md") {  // src/instationary_pnp_from_pb_md.hh:295-454
       if (!out.empty() && rank == 0) write_vector(out + "_x0.dat", u, nv);
-      int lmethod = PNP_METHOD_BICGSTAB, lprec = PNP_PREC_SSOR;
-      if (linsolver == "bcgs_noprec") lprec = PNP_PREC_NONE;
+      // BCGS_SSORk (the default of src/instationary_pnp_from_pb_md.hh:30-31, ISTLBackend_NOVLP_
+      // BCGS_SSORk(gfs, maxit, 1, verbose) at :188-191): SeqSSOR in the GFS's lexicographic order
+      int lmethod = PNP_METHOD_BICGSTAB, lprec = PNP_PREC_SSOR_NATURAL;
+      if (linsolver == "bcgs_ssork_mc") lprec = PNP_PREC_SSOR;
+      else if (linsolver == "bcgs_noprec") lprec = PNP_PREC_NONE;
       else if (linsolver == "cg_noprec") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_NONE;
       else if (linsolver == "cg_jacobi") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_JACOBI;
       else if (linsolver == "cg_amg_ssor") lmethod = PNP_METHOD_CG, lprec = PNP_PREC_AMG;

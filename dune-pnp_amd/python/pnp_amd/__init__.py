@@ -31,13 +31,13 @@ HEADER = os.path.join(REPO_ROOT, "include", "pnp_capi.h")
 OK, E_ARG, E_HIP, E_RCCL, E_BREAKDOWN, E_NOT_CONVERGED, E_IO, E_MESH, E_STATE = \
     0, -1, -2, -3, -4, -5, -6, -7, -8
 OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSON = range(6)
-PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG = range(5)
+PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG, PREC_SSOR_NATURAL = range(6)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
 (OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD, OPT_BICG_TWORED, OPT_AMG_FALLBACK,
  OPT_GRAPH) = 1, 2, 3, 4, 5, 6
 DEVICE_PTRS, JAC_FD = 1, 2
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
-                "jacobi": PREC_JACOBI, "amg": PREC_AMG}
+                "jacobi": PREC_JACOBI, "amg": PREC_AMG, "ssor_natural": PREC_SSOR_NATURAL}
 MAX_SURFACES = 64
 
 
@@ -604,6 +604,15 @@ class Context:
         r = _NewtonResult()
         self._ck(lib().pnp_newton(self.h, _ptr(u), C.byref(o), C.byref(r)))
         return u, {k: getattr(r, k) for k, _ in _NewtonResult._fields_}
+
+    def newton_history(self):
+        """Per-step record of the last newton(): (linear iterations, defect after the step)."""
+        n = C.c_int32(0)
+        self._ck(lib().pnp_newton_history(self.h, None, None, 0, C.byref(n)))
+        its = np.zeros(n.value, dtype=np.int32)
+        dfs = np.zeros(n.value)
+        self._ck(lib().pnp_newton_history(self.h, _ptr(its), _ptr(dfs), n.value, C.byref(n)))
+        return its, dfs
 
     def sync_vector(self, v, nfields=None):
         """Collective: global vector from every rank's owned entries (no-op on one GPU)."""

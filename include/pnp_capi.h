@@ -258,8 +258,16 @@ int pnp_jacobian_csr_device(pnp_ctx *ctx, pnp_csr_view *view);
 
 /* ---- linear solve (ISTL BiCGSTABSolver semantics) ----------------------------------------- */
 enum { PNP_PREC_NONE = 0, PNP_PREC_SSOR = 1, PNP_PREC_ILU0 = 2, PNP_PREC_JACOBI = 3,
-       PNP_PREC_AMG = 4 /* aggregation AMG V-cycle (ISTL Amg::AMG of LINEARSOLVER CG_AMG_SSOR,
-                            src/instationary_pnp_from_pb_md.hh:207-210); see pnp_amg_configure */ };
+       PNP_PREC_AMG = 4, /* aggregation AMG V-cycle (ISTL Amg::AMG of LINEARSOLVER CG_AMG_SSOR,
+                            src/instationary_pnp_from_pb_md.hh:207-210); see pnp_amg_configure */
+       /* ISTL SeqSSOR(A, 1, 1.0) exactly: one forward and one backward Gauss-Seidel sweep in the
+        * reference's lexicographic DOF order ([phi | c+ | c-] over the vertex order), each row's
+        * sum over its columns in ascending order -- the preconditioner of the reference's default
+        * ISTLBackend_NOVLP_BCGS_SSORk (src/instationary_pnp_from_pb_md.hh:30-31,188-191,
+        * src/stationary_pnp_from_pb.hh:168-169), so iteration counts compare with the reference's.
+        * Level-scheduled on the GPU (one launch per dependency level, ~100-300 levels): a parity
+        * mode, slower than the multicolour PNP_PREC_SSOR.  Block-Jacobi across ranks. */
+       PNP_PREC_SSOR_NATURAL = 5 };
 enum { PNP_METHOD_BICGSTAB = 0, PNP_METHOD_CG = 1 };
 typedef struct {
   int32_t prec;       /* SSOR = one multicolour symmetric Gauss-Seidel sweep (k=1, w=1) */
@@ -382,6 +390,12 @@ typedef struct {
       solves.  Off by default: a failed AMG solve ends Newton like any linear-solver failure. */
 } pnp_newton_result;
 int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
+/* per-step record of the last pnp_newton on ctx (PDELab Newton's verbose per-step output,
+ * src/stationary_pnp_from_pb.hh:355-369): for step k < min(cap, *nsteps) the linear solver's
+ * iterations and the defect after the line search; *nsteps = the number of steps (either array
+ * may be NULL) */
+int pnp_newton_history(pnp_ctx *ctx, int32_t *linear_iterations, double *defects, int32_t cap,
+                       int32_t *nsteps);
 
 /* Multi-GPU: v (host, external layout, nfields*nv) holds this rank's owned entries (as returned
  * by pnp_newton / pnp_linear_solve / pnp_residual); on return it holds the global vector on every

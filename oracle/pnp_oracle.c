@@ -1025,6 +1025,15 @@ static void prec_apply(const prec_t *P, double *v, const double *d) {
   }
 }
 
+/* one application of the preconditioner from v = 0 (test hook: the GPU's pnp_prec_apply) */
+void orc_prec_apply(const orc_csr *A, int prec, const double *d, double *v) {
+  prec_t P;
+  prec_init(&P, A, prec);
+  memset(v, 0, sizeof(double) * A->n);
+  prec_apply(&P, v, d);
+  prec_free(&P);
+}
+
 void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
                   orc_solve_result *res) {
   const double EPSILON = 1e-80;
@@ -1192,6 +1201,7 @@ void orc_newton(const orc_mesh *m, const orc_params *p, const orc_operator *op, 
     orc_solve_result sr;
     orc_bicgstab(&A, o->prec, lin_red, o->linear_maxit, z, r, &sr);
     res->linear_iterations += sr.iterations;
+    if (res->iterations < ORC_NEWTON_MAX_RECORD) res->step_linear_iterations[res->iterations] = sr.iterations;
     if (!sr.converged) { res->status = -3; break; }
     /* line_search: hackbuschReuskenAcceptBest */
     double lambda = 1.0, best_lambda = 0.0, best_defect = res->defect;

@@ -162,6 +162,9 @@ void orc_spmv(const orc_csr *A, const double *x, double *y);
 void orc_set_parallel(int on);
 void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
                   orc_solve_result *res);
+/* v = W^{-1} d, one application of preconditioner prec from v = 0 (ISTL SeqSSOR / SeqILU0 /
+ * Jacobi / Richardson as inside orc_bicgstab) */
+void orc_prec_apply(const orc_csr *A, int prec, const double *d, double *v);
 /* ISTL CGSolver (LINEARSOLVER CG_NOPREC / CG_Jacobi), see pnp_oracle.c */
 void orc_cg(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
             orc_solve_result *res);
@@ -172,9 +175,11 @@ typedef struct {
   int maxit, line_search_maxit, reassemble_threshold_zero;
   int linear_maxit, prec, fd_jacobian;
 } orc_newton_opts;
+#define ORC_NEWTON_MAX_RECORD 64
 typedef struct {
   int converged, iterations, linear_iterations, status;
   double first_defect, defect;
+  int step_linear_iterations[ORC_NEWTON_MAX_RECORD]; /* BiCGSTAB iterations of each Newton step */
 } orc_newton_result;
 /* PDELab Newton::apply on op, u in/out. status: 0 ok, -1 not converged, -2 line search,
  * -3 linear solver did not converge (NewtonLinearSolverError). */

@@ -65,7 +65,8 @@ class OrcNewtonOpts(C.Structure):
 
 class OrcNewtonResult(C.Structure):
     _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("linear_iterations", C.c_int),
-                ("status", C.c_int), ("first_defect", C.c_double), ("defect", C.c_double)]
+                ("status", C.c_int), ("first_defect", C.c_double), ("defect", C.c_double),
+                ("step_linear_iterations", C.c_int * 64)]
 
 
 def lib():
@@ -327,6 +328,27 @@ def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
 def cg(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
     """ISTL-semantics CG (CGSolver) on a scipy CSR matrix."""
     return _krylov("orc_cg", A, b, prec, reduction, maxit, x0)
+
+
+def _csr(A):
+    A = A.tocsr()
+    A.sort_indices()
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    col = np.ascontiguousarray(A.indices, dtype=np.int32)
+    val = np.ascontiguousarray(A.data, dtype=np.float64)
+    M = OrcCsr(A.shape[0], A.nnz, rp.ctypes.data_as(C.POINTER(C.c_int)),
+               col.ctypes.data_as(C.POINTER(C.c_int)), val.ctypes.data_as(C.POINTER(C.c_double)))
+    return M, (rp, col, val)
+
+
+def prec_apply(A, d, prec):
+    """v = W^{-1} d: one application of the oracle's preconditioner (ISTL SeqSSOR / SeqILU0 /
+    Jacobi) from v = 0, as inside its BiCGSTAB."""
+    M, keep = _csr(A)
+    dd = np.ascontiguousarray(d, dtype=np.float64)
+    v = np.zeros(A.shape[0])
+    lib().orc_prec_apply(C.byref(M), prec, _p(dd), _p(v))
+    return v
 
 
 def _krylov(fn, A, b, prec, reduction, maxit, x0):

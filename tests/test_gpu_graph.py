@@ -24,7 +24,8 @@ def both(fn, name="pore_small_k0"):
     return out
 
 
-@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI, P.PREC_SSOR, P.PREC_ILU0])
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_JACOBI, P.PREC_SSOR, P.PREC_ILU0,
+                                  P.PREC_SSOR_NATURAL])
 def test_graph_linear_solve_bitwise_equals_eager(prec):
     def fn(ctx, z, mesh):
         ctx.set_operator(P.OP_PNP)
