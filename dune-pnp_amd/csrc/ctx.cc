@@ -2717,6 +2717,42 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
   return PNP_OK;
 }
 
+// owner-masked dot of two external-layout vectors (this rank's owned entries), allreduced
+static int dot_ext(pnp_ctx *c, const double *a, const double *b, int nfields, int32_t flags,
+                   double *out) {
+  if (!c || !a || !b || !out || nfields < 1 || nfields > 3) return PNP_E_ARG;
+  int rc;
+  if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS))) return rc;
+  hipSetDevice(c->device);
+  const bool dev = flags & PNP_DEVICE_PTRS;
+  if ((rc = c->upload_ext(a, nfields, c->t.p, false, dev))) return rc;
+  if (b != a && (rc = c->upload_ext(b, nfields, c->y.p, false, dev))) return rc;
+  const long long n = (long long)c->L.n_owned * nfields;
+  CK(pnp::launch_dot(n, c->t.p, b != a ? c->y.p : c->t.p, 0, c->partials.p, c->stream), "dot");
+  CK(pnp::launch_reduce(c->partials.p, pnp::blas_nparts(n), 1, c->S.p + 1, c->stream), "dot");
+  if (c->dist) {
+    double *red = reinterpret_cast<double *>(reinterpret_cast<char *>(c->S.p + 1) +
+                                             offsetof(pnp::Scalars, red));
+    if ((rc = c->allreduce_dev(red, 1))) return rc;
+  }
+  CK(hipMemcpyAsync(c->hS + 1, c->S.p + 1, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, c->stream),
+     "dot readback");
+  CK(hipStreamSynchronize(c->stream), "dot readback");
+  *out = c->hS[1].red[0];
+  return PNP_OK;
+}
+
+extern "C" int pnp_dot(pnp_ctx *c, const double *a, const double *b, int32_t nfields,
+                       int32_t flags, double *out) {
+  return dot_ext(c, a, b, nfields, flags, out);
+}
+
+extern "C" int pnp_norm(pnp_ctx *c, const double *a, int32_t nfields, int32_t flags, double *out) {
+  const int rc = dot_ext(c, a, a, nfields, flags, out);
+  if (rc == PNP_OK) *out = std::sqrt(*out);
+  return rc;
+}
+
 extern "C" int pnp_newton_history(pnp_ctx *c, int32_t *its, double *defects, int32_t cap,
                                   int32_t *nsteps) {
   if (!c || !nsteps || cap < 0) return PNP_E_ARG;

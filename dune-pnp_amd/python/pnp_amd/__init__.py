@@ -605,6 +605,21 @@ class Context:
         self._ck(lib().pnp_newton(self.h, _ptr(u), C.byref(o), C.byref(r)))
         return u, {k: getattr(r, k) for k, _ in _NewtonResult._fields_}
 
+    def dot(self, a, b, nfields=None):
+        """Collective: owner-masked global scalar product of two external-layout vectors."""
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = C.c_double(0)
+        self._ck(lib().pnp_dot(self.h, _ptr(a), _ptr(b), nfields or (a.size // self.nn), 0,
+                               C.byref(out)))
+        return out.value
+
+    def norm(self, a, nfields=None):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        out = C.c_double(0)
+        self._ck(lib().pnp_norm(self.h, _ptr(a), nfields or (a.size // self.nn), 0, C.byref(out)))
+        return out.value
+
     def newton_history(self):
         """Per-step record of the last newton(): (linear iterations, defect after the step)."""
         n = C.c_int32(0)

@@ -402,6 +402,16 @@ int pnp_newton_history(pnp_ctx *ctx, int32_t *linear_iterations, double *defects
  * rank (collective; a no-op on one GPU). */
 int pnp_sync_vector(pnp_ctx *ctx, double *v, int32_t nfields);
 
+/* The NOVLP backends' parallel scalar product (ISTL's OwnerOverlapCopy-style "owner-masked local
+ * dot + allreduce", behind LS::norm at src/stationary_pnp_from_pb.hh:355-358 and the Newton
+ * defect): *out = sum over the DOFs each rank owns of a_i b_i, summed over all ranks, so every rank
+ * gets the global value whatever the other entries of its vectors hold.  a, b: external layout,
+ * nfields x nv (host, or device memory with PNP_DEVICE_PTRS); only this rank's owned entries are
+ * read.  Collective on multi-GPU.  pnp_norm = sqrt(pnp_dot(a, a)). */
+int pnp_dot(pnp_ctx *ctx, const double *a, const double *b, int32_t nfields, int32_t flags,
+            double *out);
+int pnp_norm(pnp_ctx *ctx, const double *a, int32_t nfields, int32_t flags, double *out);
+
 /* BCExtension interpolation: x0 (3*nv, external layout) from the PB potential phi_pb (nv). */
 int pnp_initial_state(pnp_ctx *ctx, const double *phi_pb, double *x0);
 

@@ -224,13 +224,25 @@ class BiCGStabBackend {
       std::printf("=== BiCGSTABSolver: rate=%g, T=%g, IT=%d\n", res_.conv_rate, res_.elapsed,
                   res_.iterations);
   }
+  // the NOVLP backend's parallel norm / scalar product: owned entries of every rank, allreduced
+  // (pnp_norm / pnp_dot); v holds nfields x nv entries in the lexicographic order
   double norm(const V &v) const {
-    double s = 0;
-    const double *p = data(v);
-    for (size_t i = 0; i < size(v); i++) s += p[i] * p[i];
-    return std::sqrt(s);
+    double out = 0;
+    check(pnp_norm(ctx_.get(), data(v), nfields(v), 0, &out), ctx_.get());
+    return out;
+  }
+  double dot(const V &a, const V &b) const {
+    double out = 0;
+    check(pnp_dot(ctx_.get(), data(a), data(b), nfields(a), 0, &out), ctx_.get());
+    return out;
   }
   const InverseOperatorResult &result() const { return res_; }
+  int nfields(const V &v) const {
+    const size_t n = size(v), nv = size_t(ctx_.nv());
+    if (nv == 0 || n % nv != 0 || n / nv < 1 || n / nv > 3)
+      throw Error(PNP_E_ARG, "pnp: vector length is not nfields x nv");
+    return int(n / nv);
+  }
   int prec() const { return prec_; }
   int maxit() const { return maxit_; }
   int method() const { return method_; }
@@ -273,6 +285,17 @@ class Newton {
     res_.defect = r.defect;
     res_.elapsed = r.elapsed;
     res_.converged = r.converged != 0;
+    if (verbose_ > 1) {  // PDELab Newton's per-step lines (verbosity 2)
+      int32_t n = 0;
+      check(pnp_newton_history(go_.context().get(), nullptr, nullptr, 0, &n), go_.context().get());
+      std::vector<int32_t> its(n);
+      std::vector<double> dfs(n);
+      check(pnp_newton_history(go_.context().get(), its.data(), dfs.data(), n, &n),
+            go_.context().get());
+      for (int k = 0; k < n; k++)
+        std::printf("  Newton iteration %3d.  New defect: %12.4e  (linear iterations %d)\n", k + 1,
+                    dfs[k], its[k]);
+    }
     if (verbose_ > 0)
       std::printf("  Newton converged=%d after %d iterations (%d linear), defect %.6e -> %.6e\n",
                   r.converged, r.iterations, r.linear_iterations, r.first_defect, r.defect);

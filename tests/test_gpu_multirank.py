@@ -319,3 +319,29 @@ def test_implicit_euler_8_ranks():
     for traj in outs:
         for a, b in zip(traj, ref):
             assert np.max(np.abs(a - b)) <= 1e-6 * np.max(np.abs(b))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_parallel_dot_and_norm_equal_single_rank(nranks):
+    """pnp_dot / pnp_norm (the NOVLP backend's norm behind Newton's defect, src/stationary_pnp_from_pb.hh:
+    355-358): every rank reads only its owned entries and gets the global value, whatever its other
+    entries hold -- here each rank's copy is garbage outside its owned rows."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    nv = mesh.nv
+    rng = np.random.default_rng(21)
+    a, b = rng.standard_normal(3 * nv), rng.standard_normal(3 * nv)
+    c1 = P.Context(mesh, par)
+    d1, n1, s1 = c1.dot(a, b), c1.norm(a), c1.norm(a[:nv], nfields=1)
+    assert abs(n1 - np.linalg.norm(a)) <= 1e-14 * n1 and abs(d1 - a @ b) <= 1e-13 * abs(a @ b)
+
+    def fn(ctx, r):
+        lay = P.Layout(mesh, r, nranks)
+        own = np.zeros(nv, dtype=bool)
+        own[lay.l2g[:lay.n_owned]] = True
+        own3 = np.tile(own, 3)
+        ga = np.where(own3, a, 1e30 * (r + 1))
+        gb = np.where(own3, b, -7.0)
+        return ctx.dot(ga, gb), ctx.norm(ga), ctx.norm(ga[:nv], nfields=1)
+    for d, n, s in run_ranks(nranks, mesh, par, fn):
+        assert abs(d - d1) <= 1e-14 * abs(d1) * 10 and abs(n - n1) <= 1e-14 * n1
+        assert abs(s - s1) <= 1e-14 * s1

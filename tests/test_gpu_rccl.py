@@ -75,3 +75,16 @@ def test_rccl_pb_then_pnp_newton_and_ion_flux_equal_plain():
         (pb1["linear_iterations"], res1["linear_iterations"])
     np.testing.assert_array_equal(u0, u1)
     np.testing.assert_array_equal(np.asarray(f0), np.asarray(f1))
+
+
+def test_rccl_dot_and_norm_equal_plain():
+    """pnp_dot / pnp_norm through the 1-rank RCCL communicator (ncclAllReduce) = the plain value."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    rng = np.random.default_rng(4)
+    a, b = rng.standard_normal(3 * mesh.nv), rng.standard_normal(3 * mesh.nv)
+    vals = []
+    for ctx in pair(mesh, par):
+        vals.append((ctx.dot(a, b), ctx.norm(a), ctx.norm(b[:mesh.nv], nfields=1)))
+        ctx.close()
+    assert vals[0] == vals[1]
+    assert abs(vals[0][1] - np.linalg.norm(a)) <= 1e-14 * vals[0][1]
