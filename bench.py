@@ -184,6 +184,27 @@ def cpu_baseline(cfg, refine, seconds):
             "mt_dofs_per_s": 3 * nv / t_mt}
 
 
+def host_cpu_info():
+    """The GPU box's host CPU as the CPU baseline ran on it: model name from /proc/cpuinfo, the
+    machine's logical CPUs (nproc --all) and the ones this process may run on (nproc)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"cpu_model": model or platform.processor() or platform.machine(),
+            "host_logical_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def measured_copy_gbs(device):
     """Device copy rate (read + write bytes / s) of a 1 GiB buffer, past the Infinity Cache."""
     import torch
@@ -282,10 +303,31 @@ def measure(ctx, mesh, args, prec, dist, world):
         ctx.assemble_state(1)
         ctx.timers(enable=False)
     tm_cold = ctx.timers()
+    # in situ: each assembly right after a BiCGSTAB block, as pnp_newton runs it (the solve's
+    # vector and matrix streams have replaced the assembly's data in the caches)
+    ctx.timers(reset=True)
+    for _ in range(args.steps):
+        ctx.bicgstab_iterations(args.bicg_iters, prec)
+        ctx.timers(enable=True)
+        ctx.assemble_state(1)
+        ctx.timers(enable=False)
+    tm_situ = ctx.timers()
     # the warm roofline's launch time: one event pair around K back-to-back launches (the per-launch
     # event pairs above add ~3 us each, r2bj: 50.2 us against rocprofv3's 47.4 us)
     ctx.assemble_state(2)
     asm_batch_s = ctx.assemble_state_timed(args.steps) / args.steps
+    # BiCGSTAB with fp64 ILU(0) factors (the default stores them in single precision)
+    t_bicg64 = None
+    if prec == P.PREC_ILU0:
+        ctx.set_option(P.OPT_ILU_F32, 0)
+        ctx.bicgstab_iterations(2, prec)
+        barrier_sync(dist, world)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.bicgstab_iterations(args.bicg_iters, prec)
+        barrier_sync(dist, world)
+        t_bicg64 = max_over_ranks(dist, world, time.perf_counter() - t0)
+        ctx.set_option(P.OPT_ILU_F32, 1)
     t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
 
     nf = 3
@@ -296,6 +338,7 @@ def measure(ctx, mesh, args, prec, dist, world):
     asm_ev_s = tm["assemble_ms"] / max(1, tm["assemble_launches"]) / 1e3
     asm_s = asm_batch_s
     asm_cold_s = tm_cold["assemble_ms"] / max(1, tm_cold["assemble_launches"]) / 1e3
+    asm_situ_s = tm_situ["assemble_ms"] / max(1, tm_situ["assemble_launches"]) / 1e3
     it_ev = (tm["spmv_ms"] + tm["prec_ms"] + tm["blas_ms"] + tm["halo_ms"] +
              tm["allreduce_ms"]) / 1e3 / args.bicg_iters
     spmv_s = tm["spmv_ms"] / max(1, tm["spmv_launches"]) / 1e3
@@ -309,12 +352,76 @@ def measure(ctx, mesh, args, prec, dist, world):
         "dofs_per_s": N_global * args.steps / t_asm,
         "iters_per_s": args.steps * args.bicg_iters / t_bicg,
         "asm_warm": rl(B["asm"], asm_s), "asm_cold": rl(B["asm"], asm_cold_s),
+        "asm_situ": rl(B["asm"], asm_situ_s),
+        "iters_per_s_f64_factors": (args.steps * args.bicg_iters / t_bicg64) if t_bicg64 else None,
         "asm_warm_per_launch_events_s": asm_ev_s,
         "it_contract": rl(B["it_contract"], it_ev), "it_stored": rl(B["it_stored"], it_ev),
         "spmv_stored": rl(B["spmv_stored"], spmv_s),
         "ilu_stored": rl(B["ilu_stored"], prec_s) if prec != P.PREC_NONE else None,
         "blas": rl(B["blas"], blas_s),
     }
+
+
+def rccl_parity(sctx, smesh, scfg, x0, rank, world, local, dist):
+    """Self-check of the multi-GPU path on the config-5 (strong) system: the global residual R(x0)
+    and the converged PNP Newton solution (reduction 1e-10; BiCGSTAB with the aggregation AMG, ILU(0)
+    smoother, block-Jacobi across ranks -- with ILU(0) alone the tight solve takes ~30 s on one GPU)
+    of the partitioned context, against a one-rank context on rank 0's GPU.  At N = 1 the "partitioned" side is a
+    context with a 1-rank RCCL communicator of its own (every reduction an ncclAllReduce, the
+    halo-split SpMV path).  Bounds: residual 1e-13 relative, solution 1e-6."""
+    s = scfg.system
+    kw = dict(reduction=1e-10, min_linear_reduction=s["newtonMinLinearReduction"],
+              prec=P.PREC_AMG, linear_maxit=int(s["linearSolverIterations"]), maxit=20)
+    t0 = time.perf_counter()
+    par = P.Params.from_config(scfg)
+    dctx = sctx if world > 1 else P.Context(smesh, par, device=local, rank=0, size=1,
+                                             unique_id=P.rccl_unique_id())
+    dctx.set_operator(P.OP_PNP)
+    dctx.amg_configure(smoother=P.PREC_ILU0)
+    dctx.timers(enable=True, reset=True)
+    r_d = dctx.sync_vector(dctx.residual(x0))
+    u_d, res_d = dctx.newton(x0, **kw)
+    u_d = dctx.sync_vector(u_d)
+    tm = dctx.timers(enable=False)
+    dinfo = dctx.info()
+    mine = {"rank": rank, "transport": dinfo["transport"], "nranks": dinfo["nranks"],
+            "nv_owned": dinfo["nv_owned"], "nv_ghost": dinfo["nv_ghost"],
+            "halo_ms": tm["halo_ms"], "allreduce_ms": tm["allreduce_ms"],
+            "spmv_launches": tm["spmv_launches"]}
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+        dctx.close()
+    out = None
+    if rank == 0:
+        c1 = P.Context(smesh, par, device=local)
+        c1.set_operator(P.OP_PNP)
+        c1.amg_configure(smoother=P.PREC_ILU0)
+        r1 = c1.residual(x0)
+        u1, res1 = c1.newton(x0, **kw)
+        c1.close()
+        er = float(np.max(np.abs(r_d - r1)) / np.max(np.abs(r1)))
+        eu = float(np.max(np.abs(u_d - u1)) / np.max(np.abs(u1)))
+        out = {"system": f"config 5 ({3 * smesh.nv} DOFs), x0 = Boltzmann initial state",
+               "ranks": world, "transport": ["plain", "local", "rccl"][allr[0]["transport"]],
+               "rccl_ranks_seen": allr[0]["nranks"],
+               "residual_rel_err": er, "solution_rel_err": eu,
+               "newton_converged": [res_d["converged"], res1["converged"]],
+               "newton_steps": [res_d["iterations"], res1["iterations"]],
+               "bicgstab_iterations": [res_d["linear_iterations"], res1["linear_iterations"]],
+               "halo_ms_max_over_ranks": max(a["halo_ms"] for a in allr),
+               "allreduce_ms_max_over_ranks": max(a["allreduce_ms"] for a in allr),
+               "ghost_vertices_per_rank": [a["nv_ghost"] for a in allr],
+               "pass": bool(er <= 1e-13 and eu <= 1e-6 and res_d["converged"] == 1 and
+                            res1["converged"] == 1),
+               "bounds": "residual <= 1e-13, solution <= 1e-6 (relative, max norm)",
+               "seconds": None}
+    barrier_sync(dist, world)
+    if out is not None:
+        out["seconds"] = time.perf_counter() - t0
+    return out
 
 
 def strong_mesh(refine):
@@ -350,6 +457,8 @@ def main():
                     help="skip the AMG-preconditioned time-to-solution leg")
     ap.add_argument("--amg-multi", action="store_true",
                     help="run the AMG time-to-solution leg at N>1 too (default: N=1 only)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the multi-GPU self-check (rccl_parity) on the config-5 system")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-refine", type=int, default=4,
                     help="refinement of the CPU sample (4: the config-3 mesh itself)")
@@ -423,11 +532,13 @@ def main():
     ctx.close()
 
     # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
-    strong = None
+    strong = parity = None
     if args.scaling == "weak" and not args.no_strong:
         scfg, smesh = strong_mesh(args.strong_refine)
-        sctx, _, spb, s_setup = make_context(smesh, scfg, rank, world, local, dist)
+        sctx, sx0, spb, s_setup = make_context(smesh, scfg, rank, world, local, dist)
         S = measure(sctx, smesh, args, prec, dist, world)
+        if not args.no_parity:
+            parity = rccl_parity(sctx, smesh, scfg, sx0, rank, world, local, dist)
         sctx.close()
         strong = {"workload": f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
                               f"natively (scale 0.85), refined k={args.strong_refine}, one mesh "
@@ -439,6 +550,7 @@ def main():
                   "bicgstab_ms_per_iter": 1e3 * S["t_bicg"] / (args.steps * args.bicg_iters),
                   "roofline_assembly_warm": S["asm_warm"], "roofline_assembly_cold": S["asm_cold"],
                   "roofline_bicgstab_stored": S["it_stored"], "spmv_stored": S["spmv_stored"],
+                  "roofline_assembly_in_situ": S["asm_situ"],
                   "ilu0_apply_stored": S["ilu_stored"], "colors": S["info"]["ncolors"],
                   "ghost_vertices": S["info"]["nv_ghost"], "setup_s": s_setup,
                   "halo_ms_per_iter": S["timers"]["halo_ms"] / args.bicg_iters,
@@ -446,6 +558,7 @@ def main():
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the contract: rank 0 at N=1 only
+        hostcpu = host_cpu_info()
         cb = cpu_baseline(cfg if args.scaling == "weak" else P.read_config(args.cfg),
                           args.cpu_refine, args.cpu_seconds)
         cpu = {"value": cb["dofs_per_s"], "unit": "assembled DOFs/s", "cores": 1, "kind": "port",
@@ -453,9 +566,10 @@ def main():
                           f"residual + PDELab forward-difference Jacobian + BCRS-style scatter) on "
                           f"pore_pnp refined k={args.cpu_refine} ({cb['dofs']} DOFs), "
                           f"{cb['assembly_s']:.3f} s per assembly, single thread on "
-                          f"{platform.processor() or platform.machine()}; ISTL BiCGSTAB NOPREC "
+                          f"{hostcpu['cpu_model']}; ISTL BiCGSTAB NOPREC "
                           f"on the same system {cb['bicgstab_nonprec_s_per_it'] * 1e3:.2f} ms/it"),
                "bicgstab_nonprec_iters_per_s_at_sample": 1.0 / cb["bicgstab_nonprec_s_per_it"],
+               "host": hostcpu,
                "gpu_vs_cpu_parity": cb["parity"]}
         cpu_all = {"value": cb["mt_dofs_per_s"], "unit": "assembled DOFs/s",
                    "cores": cb["mt_threads"], "kind": "port",
@@ -464,11 +578,13 @@ def main():
                               f"(OMP_NUM_THREADS / host), {cb['mt_assembly_s']:.4f} s per "
                               f"assembly; ISTL BiCGSTAB NOPREC row-parallel "
                               f"{cb['bicgstab_nonprec_s_per_it_mt'] * 1e3:.2f} ms/it"),
-                   "bicgstab_nonprec_iters_per_s": 1.0 / cb["bicgstab_nonprec_s_per_it_mt"]}
+                   "bicgstab_nonprec_iters_per_s": 1.0 / cb["bicgstab_nonprec_s_per_it_mt"],
+                   "host": hostcpu}
 
     if rank == 0:
         tm = M["timers"]
-        aw, ac = M["asm_warm"], M["asm_cold"]
+        aw, ac, asit = M["asm_warm"], M["asm_cold"], M["asm_situ"]
+        traffic = pmc_traffic("k_assemble_ga<0, 1, 3, 9, 6")
         if args.scaling == "weak":
             workload = (f"config 3: stationary 3-ion PNP, test/pore_pnp/pore.msh refined "
                         f"k={args.refine} x {world} mirrored copies")
@@ -498,9 +614,15 @@ def main():
                        "sell_slots": info["nslots"], "blocks": info["nblocks"]},
             "bicgstab_iters_per_s": M["iters_per_s"],
             "bicgstab_ms_per_iter": 1e3 * M["t_bicg"] / (args.steps * args.bicg_iters),
+            "bicgstab_iters_per_s_f64_factors": M["iters_per_s_f64_factors"],
             "roofline": {"bound": "hbm", "achieved": aw["achieved"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": aw["frac"],
-                         "traffic": pmc_traffic("k_assemble_ga<0, 1, 3, 9, 6"),
+                         "traffic": traffic,
+                         "achieved_is": "algorithmic (contract) bytes, SURVEY.md §8(d) B_asm, per "
+                                        "launch / launch time: an effective bandwidth on the model "
+                                        "bytes, not counted HBM bytes",
+                         "hbm_gbs_from_traffic": (traffic / aw["seconds"] / 1e9) if traffic
+                                                 else None,
                          "traffic_source": "profiles/r02/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
                                            "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
@@ -510,7 +632,16 @@ def main():
                          "avg_launch_us_per_launch_events":
                              M["asm_warm_per_launch_events_s"] * 1e6,
                          "note": "warm: back-to-back launches, the matrix write stream stays in "
-                                 "the Infinity Cache at config 3; see roofline_cold"},
+                                 "the Infinity Cache at config 3 (partly on-die bandwidth); "
+                                 "roofline_in_situ is the launch as Newton runs it, right after "
+                                 "a BiCGSTAB block; roofline_cold after a 1 GiB scrub"},
+            "roofline_in_situ": {"bound": "hbm", "achieved": asit["achieved"], "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": asit["frac"],
+                                 "bytes_per_launch": asit["bytes"],
+                                 "avg_launch_us": asit["seconds"] * 1e6,
+                                 "frac_of_measured_copy": asit["achieved"] / copy_gbs,
+                                 "timing": f"HIP event pair per launch, each launch right after "
+                                           f"{args.bicg_iters} BiCGSTAB iterations"},
             "roofline_cold": {"bound": "hbm", "achieved": ac["achieved"], "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": ac["frac"], "bytes_per_launch": ac["bytes"],
                               "avg_launch_us": ac["seconds"] * 1e6,
@@ -541,6 +672,7 @@ def main():
             "pnp_newton_time_to_solution": newton,
             "pnp_newton_time_to_solution_amg": newton_amg,
             "strong_scaling": strong,
+            "rccl_parity": parity,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

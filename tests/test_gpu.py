@@ -137,6 +137,51 @@ def test_residual_parity_full_size():
     assert np.max(np.abs(lhs - J @ d)) <= 1e-9 * np.max(np.abs(J @ d))
 
 
+def test_jacobian_parity_full_size():
+    """Config-3 mesh (2.2 M DOF, 36 M stored nonzeros): the GPU's analytic Jacobian entry by entry
+    against the oracle's analytic Jacobian, 1e-12 of max|J|."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp/pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(4)
+    par = P.Params.from_config(cfg)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    rng = np.random.default_rng(20261015)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    J = ctx.jacobian(x)
+    ctx.close()
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    Jo = orc.jacobian(op, x)
+    assert abs(J - Jo).max() <= 1e-12 * abs(Jo).max()
+
+
+def test_residual_parity_config5():
+    """Config 5 (test/pore_without_dna's .geo meshed natively, scale 0.85, refined k=6: 8.87 M DOF,
+    the north star's system): residual vs the oracle, 1e-12 of max|r|."""
+    cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
+    mesh = P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(6)
+    par = P.Params.from_config(cfg)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    rng = np.random.default_rng(5)
+    nv = mesh.nv
+    assert 3 * nv > 8_000_000
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    r = ctx.residual(x)
+    ctx.close()
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    ro = orc.residual(op, x)
+    assert np.max(np.abs(r - ro)) <= 1e-12 * np.max(np.abs(ro))
+
+
 @pytest.mark.parametrize("kind,prec", [("pnp", P.PREC_NONE), ("pnp", P.PREC_SSOR),
                                        ("pnp", P.PREC_ILU0), ("pb", P.PREC_JACOBI),
                                        ("pb", P.PREC_SSOR), ("pb", P.PREC_ILU0)])
