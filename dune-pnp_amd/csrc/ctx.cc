@@ -122,6 +122,9 @@ struct pnp_ctx {
   DBuf<uint8_t> d_rowcolor;
   DBuf<uint64_t> d_rowmeta;
   DBuf<int> d_uptr, d_ulist;   // LDS-staged SpMV lists (PNP_SPMV_LDS, DevLayout::uptr)
+  DBuf<int> d_lsx_ptr, d_lsx_list, d_usx_ptr, d_usx_list;  // LDS-staged sweeps (DevLayout lsx_*)
+  DBuf<uint16_t> d_lsx_idx, d_usx_idx;
+  DBuf<uint8_t> d_lperm, d_uperm, d_lpinv, d_upinv, d_llen, d_ulen, d_ldl;  // split lane order
   DBuf<uint16_t> d_lidx;
   DBuf<double> d_xy;
 
@@ -1781,22 +1784,63 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     return PNP_OK;
   };
   int rc;
-  // triangular split of the owned-column pattern (DevLayout l*/u*)
+  // triangular split of the owned-column pattern (DevLayout l*/u*).  Lane order (PNP_SPLIT_SORT,
+  // default on): inside each 64-row chunk, and inside each colour's segment of it, the rows are
+  // stored longest-first in each of L and U, so a slot plane's padding is a tail of lanes that
+  // issue no loads (config 3: 17.8 % of the split slots are padding); position p = 64 ch + lane
+  // holds row 64 ch + lperm[p] in L and 64 ch + uperm[p] in U.  A row's own arithmetic and slot
+  // order are unchanged, so every result is bitwise the identity order's.
+  const int no = L.n_owned, npos = 64 * L.nchunks;
+  std::vector<int> nlr(npos, 0), nur(npos, 1);
+  for (int row = 0; row < no; row++) {
+    const int ch = row / 64, ln = row % 64, len = int(L.rowmeta[row] & 63);
+    for (int sl = 1; sl < len; sl++) {
+      const int j = L.colidx[size_t(L.chunk_off[ch]) + 64 * sl + ln];
+      // ghost and same-colour columns are outside the sweeps (mesh.cc absorb_top)
+      if (j >= no || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
+      (j < row ? nlr[row] : nur[row])++;
+    }
+  }
+  std::vector<uint8_t> lperm(npos), uperm(npos), lpinv(npos), upinv(npos), llen8(npos, 0),
+      ulen8(npos, 0), ldl(npos);
+  const bool sort_lanes = [] {
+    const char *e = getenv("PNP_SPLIT_SORT");
+    return !(e && e[0] == '0');
+  }();
+  for (int ch = 0; ch < L.nchunks; ch++) {
+    for (int ln = 0; ln < 64; ln++) lperm[64 * ch + ln] = uperm[64 * ch + ln] = uint8_t(ln);
+    for (int a0 = 64 * ch; a0 < std::min(no, 64 * ch + 64);) {  // colour segments
+      int a1 = a0 + 1;
+      while (a1 < std::min(no, 64 * ch + 64) && L.rowcolor[a1] == L.rowcolor[a0]) a1++;
+      if (sort_lanes) {
+        std::vector<int> ord(a1 - a0);
+        for (int k = 0; k < a1 - a0; k++) ord[k] = a0 + k;
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return nlr[x] > nlr[y]; });
+        for (int k = 0; k < a1 - a0; k++) lperm[a0 + k] = uint8_t(ord[k] - 64 * ch);
+        for (int k = 0; k < a1 - a0; k++) ord[k] = a0 + k;
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return nur[x] > nur[y]; });
+        for (int k = 0; k < a1 - a0; k++) uperm[a0 + k] = uint8_t(ord[k] - 64 * ch);
+      }
+      a0 = a1;
+    }
+  }
+  auto rowL = [&](int pos) { return 64 * (pos / 64) + lperm[pos]; };
+  auto rowU = [&](int pos) { return 64 * (pos / 64) + uperm[pos]; };
+  for (int pos = 0; pos < npos; pos++) {
+    lpinv[rowL(pos)] = uint8_t(pos % 64);
+    upinv[rowU(pos)] = uint8_t(pos % 64);
+  }
+  for (int pos = 0; pos < npos; pos++) {
+    llen8[pos] = uint8_t(nlr[rowL(pos)]);
+    ulen8[pos] = uint8_t(nur[rowU(pos)]);
+    ldl[pos] = upinv[rowL(pos)];
+  }
   std::vector<int> lcl(L.nchunks), lco(L.nchunks + 1, 0), ucl(L.nchunks), uco(L.nchunks + 1, 0);
   for (int ch = 0; ch < L.nchunks; ch++) {
     int ml = 0, mu = 1;
-    for (int ln = 0; ln < 64; ln++) {
-      int row = 64 * ch + ln;
-      if (row >= L.n_owned) break;
-      int len = int(L.rowmeta[row] & 63), nl = 0, nu = 1;
-      for (int sl = 1; sl < len; sl++) {
-        int j = L.colidx[size_t(L.chunk_off[ch]) + 64 * sl + ln];
-        // ghost and same-colour columns are outside the sweeps (mesh.cc absorb_top)
-        if (j >= L.n_owned || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
-        (j < row ? nl : nu)++;
-      }
-      ml = std::max(ml, nl);
-      mu = std::max(mu, nu);
+    for (int row = 64 * ch; row < std::min(no, 64 * ch + 64); row++) {
+      ml = std::max(ml, nlr[row]);
+      mu = std::max(mu, nur[row]);
     }
     lcl[ch] = ml;
     ucl[ch] = mu;
@@ -1807,33 +1851,117 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       usrc(uco[L.nchunks], -1);
   for (int ch = 0; ch < L.nchunks; ch++)
     for (int ln = 0; ln < 64; ln++) {
-      int row = 64 * ch + ln;
-      for (int sl = 0; sl < lcl[ch]; sl++) lcol[size_t(lco[ch]) + 64 * sl + ln] = row;
-      for (int sl = 0; sl < ucl[ch]; sl++) ucol[size_t(uco[ch]) + 64 * sl + ln] = row;
-      if (row >= L.n_owned) continue;
-      int len = int(L.rowmeta[row] & 63), kl = 0, ku = 1;
-      usrc[size_t(uco[ch]) + ln] = row << 6;  // slot 0: the diagonal block
-      for (int sl = 1; sl < len; sl++) {
-        int pos = L.chunk_off[ch] + 64 * sl + ln;
-        int j = L.colidx[pos];
-        if (j >= L.n_owned || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
-        if (j < row) {
-          lcol[size_t(lco[ch]) + 64 * kl + ln] = j;
-          lsrc[size_t(lco[ch]) + 64 * kl + ln] = row << 6 | sl;
-          kl++;
-        } else {
-          ucol[size_t(uco[ch]) + 64 * ku + ln] = j;
-          usrc[size_t(uco[ch]) + 64 * ku + ln] = row << 6 | sl;
-          ku++;
+      const int p = 64 * ch + ln, rl = rowL(p), ru = rowU(p);
+      for (int sl = 0; sl < lcl[ch]; sl++) lcol[size_t(lco[ch]) + 64 * sl + ln] = rl;
+      for (int sl = 0; sl < ucl[ch]; sl++) ucol[size_t(uco[ch]) + 64 * sl + ln] = ru;
+      if (p >= no) continue;
+      for (int side = 0; side < 2; side++) {  // 0: L at this position (row rl), 1: U (row ru)
+        const int row = side ? ru : rl, rch = row / 64, rln = row % 64;
+        const int len = int(L.rowmeta[row] & 63);
+        int kl = 0, ku = 1;
+        if (side) usrc[size_t(uco[ch]) + ln] = row << 6;  // slot 0: the diagonal block
+        for (int sl = 1; sl < len; sl++) {
+          const int j = L.colidx[size_t(L.chunk_off[rch]) + 64 * sl + rln];
+          if (j >= no || j == row || L.rowcolor[j] == L.rowcolor[row]) continue;
+          if (j < row) {
+            if (!side) {
+              lcol[size_t(lco[ch]) + 64 * kl + ln] = j;
+              lsrc[size_t(lco[ch]) + 64 * kl + ln] = row << 6 | sl;
+            }
+            kl++;
+          } else {
+            if (side) {
+              ucol[size_t(uco[ch]) + 64 * ku + ln] = j;
+              usrc[size_t(uco[ch]) + 64 * ku + ln] = row << 6 | sl;
+            }
+            ku++;
+          }
         }
       }
     }
+  if ((rc = up(c->d_lperm, lperm, "lperm")) || (rc = up(c->d_uperm, uperm, "uperm")) ||
+      (rc = up(c->d_lpinv, lpinv, "lpinv")) || (rc = up(c->d_upinv, upinv, "upinv")) ||
+      (rc = up(c->d_llen, llen8, "llen")) || (rc = up(c->d_ulen, ulen8, "ulen")) ||
+      (rc = up(c->d_ldl, ldl, "ldl"))) {
+    g_err = c->err;
+    return rc;
+  }
+  c->dl.lperm = c->d_lperm.p;
+  c->dl.uperm = c->d_uperm.p;
+  c->dl.lpinv = c->d_lpinv.p;
+  c->dl.upinv = c->d_upinv.p;
+  c->dl.llen = c->d_llen.p;
+  c->dl.ulen = c->d_ulen.p;
+  c->dl.ldl = c->d_ldl.p;
   if ((rc = up(c->d_lchunk_len, lcl, "lchunk_len")) || (rc = up(c->d_lchunk_off, lco, "lchunk_off")) ||
       (rc = up(c->d_lcolidx, lcol, "lcolidx")) || (rc = up(c->d_lsrc, lsrc, "lsrc")) ||
       (rc = up(c->d_uchunk_len, ucl, "uchunk_len")) || (rc = up(c->d_uchunk_off, uco, "uchunk_off")) ||
       (rc = up(c->d_ucolidx, ucol, "ucolidx")) || (rc = up(c->d_usrc, usrc, "usrc"))) {
     g_err = c->err;
     return rc;
+  }
+  {  // LDS-staged sweep lists (DevLayout lsx_* / usx_*): per colour, per 256-row block of the
+     // colour, the distinct rows its L / U split slots couple to; per split position its list
+     // position (0xFFFF for padding and the U diagonal slot)
+    const int nc = int(L.color_ptr.size()) - 1;
+    auto lists = [&](const std::vector<int> &cl, const std::vector<int> &co,
+                     const std::vector<int> &cc, int s0, auto rowat, std::vector<int> &ptr,
+                     std::vector<int> &lst, std::vector<uint16_t> &idx) -> bool {
+      idx.assign(cc.size(), 0xFFFF);
+      ptr.assign(1, 0);
+      lst.clear();
+      std::vector<int> cols;
+      for (int c = 0; c < nc; c++) {
+        const int a = L.color_ptr[c], b = L.color_ptr[c + 1];
+        for (int r0 = a; r0 < b; r0 += 256) {
+          const int r1 = std::min(b, r0 + 256);
+          cols.clear();
+          for (int p = r0; p < r1; p++) {  // positions; the row at p is rowat(p)
+            const int ch = p / 64, ln = p % 64, row = rowat(p);
+            for (int sl = s0; sl < cl[ch]; sl++) {
+              const int j = cc[size_t(co[ch]) + 64 * sl + ln];
+              if (j != row) cols.push_back(j);
+            }
+          }
+          std::sort(cols.begin(), cols.end());
+          cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+          if (cols.size() >= 0xFFFF) return false;
+          for (int p = r0; p < r1; p++) {
+            const int ch = p / 64, ln = p % 64, row = rowat(p);
+            for (int sl = s0; sl < cl[ch]; sl++) {
+              const size_t pos = size_t(co[ch]) + 64 * sl + ln;
+              if (cc[pos] != row)
+                idx[pos] = uint16_t(std::lower_bound(cols.begin(), cols.end(), cc[pos]) - cols.begin());
+            }
+          }
+          lst.insert(lst.end(), cols.begin(), cols.end());
+          ptr.push_back(int(lst.size()));
+        }
+      }
+      return true;
+    };
+    std::vector<int> lp, ll, up2, ul;
+    std::vector<uint16_t> li, ui;
+    const bool ok = lists(lcl, lco, lcol, 0, rowL, lp, ll, li) &&
+                    lists(ucl, uco, ucol, 1, rowU, up2, ul, ui);
+    int mx = 0;
+    for (size_t k = 0; ok && k + 1 < lp.size(); k++) mx = std::max(mx, lp[k + 1] - lp[k]);
+    for (size_t k = 0; ok && k + 1 < up2.size(); k++) mx = std::max(mx, up2[k + 1] - up2[k]);
+    if (ok && nc <= 256 && size_t(mx) * 3 * 8 <= 64 * 1024) {
+      if ((rc = up(c->d_lsx_ptr, lp, "lsx ptr")) || (rc = up(c->d_lsx_list, ll, "lsx list")) ||
+          (rc = up(c->d_lsx_idx, li, "lsx idx")) || (rc = up(c->d_usx_ptr, up2, "usx ptr")) ||
+          (rc = up(c->d_usx_list, ul, "usx list")) || (rc = up(c->d_usx_idx, ui, "usx idx"))) {
+        g_err = c->err;
+        return rc;
+      }
+      c->dl.lsx_ptr = c->d_lsx_ptr.p;
+      c->dl.lsx_list = c->d_lsx_list.p;
+      c->dl.lsx_idx = c->d_lsx_idx.p;
+      c->dl.usx_ptr = c->d_usx_ptr.p;
+      c->dl.usx_list = c->d_usx_list.p;
+      c->dl.usx_idx = c->d_usx_idx.p;
+      c->dl.sx_max = mx;
+    }
   }
   {  // row-contiguous block offsets and columns of the owned rows (fused ILU(0) factorisation)
     std::vector<int> ro(L.n_owned + 1, 0), rcol;

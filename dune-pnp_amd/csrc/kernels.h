@@ -237,6 +237,20 @@ struct DevLayout {
   const int *uptr = nullptr, *ulist = nullptr;
   const uint16_t *lidx = nullptr;
   int umax = 0;
+  // LDS-staged ILU(0) sweeps (k_ilu0_solve_lds): per (colour, 256-row block of the colour) -- blocks
+  // numbered colour by colour -- the distinct neighbour rows of its L (forward) / U (backward) split
+  // slots (lsx_list[lsx_ptr[b] ..), usx_*), and per split-storage position (the indexing of lcolidx
+  // / ucolidx) the neighbour's position in its block's list (0xFFFF: padding or the diagonal slot);
+  // sx_max = the longest list
+  const int *lsx_ptr = nullptr, *lsx_list = nullptr, *usx_ptr = nullptr, *usx_list = nullptr;
+  // lane order of the split storage (ctx.cc, PNP_SPLIT_SORT): position p = 64 chunk + lane holds
+  // row 64 chunk + lperm[p] in L, 64 chunk + uperm[p] in U (rows of one colour segment of the
+  // chunk, longest first); lpinv / upinv: the lane of a row; llen / ulen: a position's own slot
+  // count (U: with the diagonal slot); ldl[p]: the U lane of L position p's row (its diagonal block)
+  const uint8_t *lperm = nullptr, *uperm = nullptr, *lpinv = nullptr, *upinv = nullptr;
+  const uint8_t *llen = nullptr, *ulen = nullptr, *ldl = nullptr;
+  const uint16_t *lsx_idx = nullptr, *usx_idx = nullptr;
+  int sx_max = 0;
 };
 
 template <int NF>

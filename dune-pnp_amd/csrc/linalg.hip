@@ -364,33 +364,36 @@ __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int l
   }
 }
 
-// Row setup shared by the split sweeps: the row's slots in the L (FWD) or U (!FWD) storage.
+// Row setup shared by the split sweeps: the slots of split position pos in the L (FWD) or U (!FWD)
+// storage, the row stored there (DevLayout lperm / uperm) and the lane of its diagonal block
 template <typename VT>
 struct SplitRow {
   const int *cix;
   const VT *vc;  // chunk base of the L or U values: slot s at vc + s * slot_vals * kRows
   const VT *dg;  // U chunk base: slot 0 = diagonal block
-  int len, lane;
+  int len, lane, dlane, row;
 };
 
 template <int NV, int FWD, typename VT = double>
 __device__ __forceinline__ SplitRow<VT> split_row(const DevLayout &L, const VT *lv, const VT *uv,
-                                                  int row, bool live) {
+                                                  int pos, bool live) {
   constexpr int NS = slot_vals<NV, VT>();
-  const int chunk = row / kRows, lane = row % kRows;
+  const int chunk = pos / kRows, lane = pos % kRows;
   const int uoff = L.uchunk_off[chunk];
   SplitRow<VT> r;
   r.lane = lane;
+  r.row = L.lperm ? chunk * kRows + int(FWD ? L.lperm[pos] : L.uperm[pos]) : pos;
+  r.dlane = (FWD && L.ldl) ? int(L.ldl[pos]) : lane;
   r.dg = uv + size_t(uoff) * NS;
   if (FWD) {
     const int off = L.lchunk_off[chunk];
     r.cix = L.lcolidx + off + lane;
     r.vc = lv + size_t(off) * NS;
-    r.len = live ? L.lchunk_len[chunk] : 0;
+    r.len = live ? (L.llen ? int(L.llen[pos]) : L.lchunk_len[chunk]) : 0;
   } else {
     r.cix = L.ucolidx + uoff + lane;
     r.vc = r.dg;
-    r.len = live ? L.uchunk_len[chunk] : 0;
+    r.len = live ? (L.ulen ? int(L.ulen[pos]) : L.uchunk_len[chunk]) : 0;
   }
   return r;
 }
@@ -475,14 +478,15 @@ __global__ __launch_bounds__(kBlock) void k_sgs_color(DevLayout L, int k0, int n
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
   const int k = gt / LPR, q = gt % LPR;
   const bool live = k < nk;
-  const int row = k0 + (live ? k : 0);  // colour-major order: the colour's rows are [k0, k0+nk)
-  const SplitRow<double> R = split_row<NV, FWD>(L, lv, uv, row, live);
+  // colour-major order: the colour's rows are the split positions [k0, k0+nk)
+  const SplitRow<double> R = split_row<NV, FWD>(L, lv, uv, k0 + (live ? k : 0), live);
+  const int row = R.row;
   // the row's own data and diagonal block do not depend on the neighbours: issued before the
   // neighbour loop so that they share its memory round trips (after the loop they cost one more)
   double rhs[NF], vi[NF], Dg[NV];
   load_nf<NF>(FWD ? d : t, size_t(row), rhs);
   if (!FWD) load_nf<NF>(v, size_t(row), vi);
-  load_vals<NV>(R.dg, R.lane, Dg);
+  load_vals<NV>(R.dg, R.dlane, Dg);
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B, NT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
@@ -775,14 +779,16 @@ __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, i
   }
   // 3) the split storage: slot 0 and the owned upper columns (slot order) to U, the lower
   // columns (slot order) to L, ghost columns dropped -- the order ctx.cc builds lsrc / usrc in
+  const int lla = L.lpinv ? int(L.lpinv[row]) : li, ula = L.upinv ? int(L.upinv[row]) : li;
   auto put = [&](VT *base, int off, int k, const double (&B)[NV]) {
+    const int ln = base == lv ? lla : ula;  // the row's lane in the L / U storage
     VT *sb = base + (size_t(off) + size_t(k) * kRows) * NS;
     if constexpr (std::is_same<VT, double>::value) {
 #pragma unroll
-      for (int q = 0; q < NV; q++) sb[vin(NV, q, li)] = B[q];
+      for (int q = 0; q < NV; q++) sb[vin(NV, q, ln)] = B[q];
     } else {
 #pragma unroll
-      for (int q = 0; q < NS; q++) sb[vinf(NV, q, li)] = q < NV ? float(B[q]) : 0.0f;
+      for (int q = 0; q < NS; q++) sb[vinf(NV, q, ln)] = q < NV ? float(B[q]) : 0.0f;
     }
   };
   const int loff = L.lchunk_off[ci], uoff = L.uchunk_off[ci];
@@ -851,15 +857,125 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
   const int k = gt / LPR, q = gt % LPR;
   const bool live = r0 + k < r1;
-  const int row = live ? r0 + k : r0;
-  const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, row, live);
+  const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, live ? r0 + k : r0, live);
+  const int row = R.row;
   // own data and diagonal block first: they share the neighbour loop's round trips
   double own[NF], Dg[NV];
   load_nf<NF>(FWD ? d : v, size_t(row), own);
-  load_split_vals<NV, 0>(R.dg, R.lane, Dg);
+  load_split_vals<NV, 0>(R.dg, R.dlane, Dg);
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B, NT, VT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] += own[f];
+  if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
+  if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
+  store_nf<NF>(v, size_t(row), acc);
+  if constexpr (ADD && KIND != kIluFwd) {
+    double ad[NF];
+    load_nf<NF>(add, size_t(row), ad);
+#pragma unroll
+    for (int f = 0; f < NF; f++) ad[f] += acc[f];
+    store_nf<NF>(out, size_t(row), ad);
+  }
+}
+
+// k_ilu0_solve (one lane per row) with the neighbour gathers staged through LDS: the workgroup's
+// 256 rows (one block of one colour) first load v at the distinct rows their split slots couple to
+// (DevLayout lsx_* / usx_*: config 3 has ~1.8 slots per distinct neighbour), then every slot reads
+// its neighbour's record from LDS by a 16-bit list position.  The rows read are of other colours
+// -- earlier ones in the forward sweep, later (finished) ones in the backward sweep -- so nothing
+// staged is written during the launch.  Each row's sum runs over its slots in the order of
+// split_row_dot<.., 1, B>, so v is bitwise k_ilu0_solve's.  The row's own loads, its diagonal
+// block and its first slot batch's list positions and factor values are issued before the barrier.
+template <int NF, int PAT, int KIND, int B, int NT, int ADD = 0, typename VT = double>
+__global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, int r1, int blk0,
+                                                           const VT *__restrict__ lv,
+                                                           const VT *__restrict__ uv,
+                                                           const double *__restrict__ d,
+                                                           double *__restrict__ v,
+                                                           const double *__restrict__ add = nullptr,
+                                                           double *__restrict__ out = nullptr) {
+  constexpr int NV = popc9(PAT), NS = slot_vals<NV, VT>();
+  constexpr bool FWD = KIND != kIluBwd;
+  extern __shared__ double sx[];  // [cnt][NF]
+  const int bl = xcd_block(blockIdx.x, gridDim.x, 1);
+  const bool live = r0 + bl * kBlock + int(threadIdx.x) < r1;
+  const int pos = live ? r0 + bl * kBlock + int(threadIdx.x) : r0;
+  const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, pos, live);
+  const int row = R.row;
+  double own[NF], Dg[NV];
+  load_nf<NF>(FWD ? d : v, size_t(row), own);
+  load_split_vals<NV, 0>(R.dg, R.dlane, Dg);
+  const int chunk = pos / kRows;
+  const uint16_t *__restrict__ lix =
+      (FWD ? L.lsx_idx + L.lchunk_off[chunk] : L.usx_idx + L.uchunk_off[chunk]) + R.lane;
+  const int *__restrict__ ptr = FWD ? L.lsx_ptr : L.usx_ptr;
+  const int *__restrict__ lst = FWD ? L.lsx_list : L.usx_list;
+  const int s0 = FWD ? 0 : 1;
+  // a batch's list positions and factor values (kept as stored, float or double, until used) do
+  // not depend on the staging: the first batch is in flight with it
+  int li[B];
+  VT ar[B][NS];
+  auto fetch = [&](int sb) {
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int s = sb + b;
+      li[b] = s < R.len ? int(lix[s * kRows]) : 0xFFFF;
+      const VT *sbp = R.vc + size_t(s) * NS * kRows;
+      if (s >= R.len) {
+#pragma unroll
+        for (int qq = 0; qq < NS; qq++) ar[b][qq] = VT(0);
+      } else if constexpr (std::is_same<VT, double>::value) {
+        load_split_vals<NV, NT>(sbp, R.lane, ar[b]);
+      } else if constexpr (NV == 1) {
+        ar[b][0] = NT ? __builtin_nontemporal_load(sbp + R.lane) : sbp[R.lane];
+      } else {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int k = 0; k < NS / 4; k++) {
+          const f4v *pp = reinterpret_cast<const f4v *>(sbp + k * 4 * kRows) + R.lane;
+          const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
+#pragma unroll
+          for (int i = 0; i < 4; i++) ar[b][4 * k + i] = t[i];
+        }
+      }
+    }
+  };
+  fetch(s0);
+  const int u0 = ptr[blk0 + bl], cnt = ptr[blk0 + bl + 1] - u0;
+  for (int k = threadIdx.x; k < cnt; k += kBlock) {
+    double t[NF];
+    load_nf<NF>(v, size_t(lst[u0 + k]), t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
+  }
+  __syncthreads();
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0.0;
+  for (int sb = s0; sb < R.len; sb += B) {
+    if (sb != s0) fetch(sb);
+    // explicit fused multiply-adds: the contraction k_ilu0_solve gets from the compiler (with the
+    // operand selects the compiler would otherwise split some products into mul + add); each
+    // slot's values are converted where they are used (short live ranges: VGPRs, occupancy)
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const bool use = li[b] != 0xFFFF;  // padding: zero values, zero operand
+      double vj[NF];
+#pragma unroll
+      for (int g = 0; g < NF; g++) vj[g] = use ? sx[li[b] * NF + g] : 0.0;
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int qq = pat_index(PAT, f, g);
+          if (qq >= 0)
+            acc[f] = __builtin_fma(-(use ? double(ar[b][qq]) : 0.0), vj[g], acc[f]);
+        }
+    }
+  }
+  if (!live) return;
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] += own[f];
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
@@ -1053,7 +1169,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     if (row < c0_end) {
       double Dg[NV];
       load_split_vals<NV, 0>(uv + size_t(L.uchunk_off[row / kRows]) * slot_vals<NV, VT>(),
-                             row % kRows, Dg);
+                             L.upinv ? int(L.upinv[row]) : row % kRows, Dg);
       diag_lower_solve<NF, PAT>(Dg, d);
       store_nf<NF>(yout, size_t(row), d);
     }
@@ -1563,11 +1679,74 @@ hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *cp, int nf, i
   return f32 ? run(float()) : run(double());
 }
 
+// LDS-staged sweeps when the layout carries their lists and the sweep shape is the default one
+// lane per row (PNP_ILU_LDS=0: the direct gathers, A/B)
+static bool ilu_lds() {
+  static const bool v = [] {
+    const char *e = std::getenv("PNP_ILU_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+static bool ilu_lds_b8() {
+  static const bool v = [] {
+    const char *e = std::getenv("PNP_ILU_LDS_B");
+    return e && e[0] == '8';
+  }();
+  return v;
+}
+
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const void *lvp,
                              const void *uvp, const double *d, double *v, hipStream_t s,
                              int c_first, const double *add, double *out, int f32) {
   if (L.n_owned == 0) return hipSuccess;
   const int nc = L.ncolors;
+  if (ilu_lds() && L.lsx_ptr && sweep_cfg() == 20) {
+    // block numbering of the lists: colour by colour, 256-row blocks
+    int blk0[256 + 1];
+    if (nc > 256) return hipErrorInvalidValue;
+    blk0[0] = 0;
+    for (int c = 0; c < nc; c++) blk0[c + 1] = blk0[c] + (cp[c + 1] - cp[c] + kBlock - 1) / kBlock;
+    const size_t lds = size_t(L.sx_max) * nf * sizeof(double);
+    auto run = [&](auto vt) -> hipError_t {
+      using VT = decltype(vt);
+      const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
+      // slot batch: 4 (8-slot batches, one batch for every row seen: config 3 apply 77 -> 89 us,
+      // config 5 245 -> 288 us, profiles/r03/ab_ilu_lds_b.log)
+      constexpr int kB = 4;
+      PNP_PAT_DISPATCH(nf, pat, {
+        auto go = [&](auto kind, int c) {
+          const int n = cp[c + 1] - cp[c];
+          if (n <= 0) return;
+          constexpr int K = decltype(kind)::value;
+          auto launch = [&](auto ntc, auto bc) {
+            constexpr int NT = decltype(ntc)::value;
+            constexpr int BB = decltype(bc)::value;
+            if (add && K != kIluFwd)
+              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 1, VT>), rows_grid(n),
+                                 dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
+                                 add, out);
+            else
+              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 0, VT>), rows_grid(n),
+                                 dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
+                                 nullptr, nullptr);
+          };
+          if (ilu_lds_b8())  // A/B: 8-slot batches
+            launch(std::integral_constant<int, 1>(), std::integral_constant<int, 8>());
+          else if (sweep_nt())
+            launch(std::integral_constant<int, 1>(), std::integral_constant<int, kB>());
+          else
+            launch(std::integral_constant<int, 0>(), std::integral_constant<int, kB>());
+        };
+        for (int c = c_first; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
+        go(std::integral_constant<int, kIluLast>(), nc - 1);
+        for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
+      });
+      return hipGetLastError();
+    };
+    return f32 ? run(float()) : run(double());
+  }
   auto run = [&](auto vt) -> hipError_t {
     using VT = decltype(vt);
     const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
