@@ -280,6 +280,7 @@ struct pnp_ctx {
   // kernel arguments captured in a graph stay valid while the buffers and the layout do: anything
   // that changes an operator, an option or a buffer bumps the epoch
   long long graph_epoch = 0;
+  bool graphs_failed = false;  // a capture / instantiation failed: eager launches from then on
   struct GraphSlot {
     GraphKey key;
     hipGraphExec_t exec = nullptr;
@@ -290,15 +291,20 @@ struct pnp_ctx {
       if (g.exec) hipGraphExecDestroy(g.exec);
     graph_cache.clear();
     graph_epoch++;
+    graphs_failed = false;
   }
   // replay the launches `issue` makes on the stream as a graph (captured on first use of `key`)
+  // *captured = false when the failure happened before any launch ran (capture / instantiate):
+  // the caller can then run the same iterations eagerly
   template <typename F>
-  int graph_run(const GraphKey &key, F &&issue) {
+  int graph_run(const GraphKey &key, F &&issue, bool *captured = nullptr) {
+    if (captured) *captured = true;
     for (auto &g : graph_cache)
       if (g.key == key) {
         hipError_t e = hipGraphLaunch(g.exec, stream);
         return e == hipSuccess ? PNP_OK : hipfail(e, "graph launch");
       }
+    if (captured) *captured = false;
     hipError_t e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) return hipfail(e, "graph capture");
     const int rc = issue();
@@ -313,6 +319,7 @@ struct pnp_ctx {
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     hipGraphDestroy(graph);
     if (e != hipSuccess) return hipfail(e, "graph instantiate");
+    if (captured) *captured = true;
     if (graph_cache.size() >= 8) {
       hipGraphExecDestroy(graph_cache.front().exec);
       graph_cache.erase(graph_cache.begin());
@@ -1400,24 +1407,34 @@ struct pnp_ctx {
     // the iterations between two polls of the device scalars (every `check`): eagerly, or as one
     // hipGraph replay (small systems, where launching ~20 kernels per iteration from the host
     // costs more than running them: PNP_OPT_GRAPH)
-    const bool graphs = use_graphs() && !dist && !twored && !debug_trace && !timing &&
-                        prec != PNP_PREC_AMG;
+    bool graphs = use_graphs() && !dist && !twored && !debug_trace && !timing &&
+                  prec != PNP_PREC_AMG && !graphs_failed;
     for (int k = 0; k < maxit;) {
       const int kend = std::min(maxit, (k / check + 1) * check);  // next poll
       if (k == 0) {
         if ((rc = body(0))) return rc;
         k = 1;
       }
-      if (k < kend && graphs) {
-        const GraphKey key{kend - k, prec, fuse ? 1 : 0, nf, pat, f32_now(), zout, dl.dmask,
+      // whole graph blocks of glen iterations (one captured graph per block length, replayed as
+      // often as the poll interval holds it), the remainder eagerly; a capture or instantiation
+      // failure turns graphs off for the rest of the solve (eager launches, same results)
+      const int glen = std::min(check, 16);
+      while (graphs && glen > 1 && kend - k >= glen) {
+        const GraphKey key{glen, prec, fuse ? 1 : 0, nf, pat, f32_now(), zout, dl.dmask,
                            graph_epoch};
-        if ((rc = graph_run(key, [&]() -> int {
-               for (int i = 0; i < key.count; i++)
-                 if (int r2 = body(1)) return r2;
-               return PNP_OK;
-             })))
-          return rc;
-        k = kend;
+        bool captured = true;
+        rc = graph_run(key, [&]() -> int {
+          for (int i = 0; i < key.count; i++)
+            if (int r2 = body(1)) return r2;
+          return PNP_OK;
+        }, &captured);
+        if (rc && !captured) {  // the graph path failed before anything ran: eager from here
+          graphs_failed = true;
+          graphs = false;
+          break;
+        }
+        if (rc) return rc;
+        k += glen;
       }
       for (; k < kend; k++)
         if ((rc = body(k))) return rc;
@@ -2602,6 +2619,29 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     return PNP_OK;
   }
   return c->fail(PNP_E_ARG, "unknown option");
+}
+
+extern "C" int pnp_set_create_option(int32_t option, int64_t value) {
+  if (option == PNP_CREATE_ABSORB_THIN_COLOR) {
+    if (value < -1 || value > 1) {
+      g_err = "PNP_CREATE_ABSORB_THIN_COLOR takes -1, 0 or 1";
+      return PNP_E_ARG;
+    }
+    pnp::g_absorb_thin_color.store(int(value));
+    return PNP_OK;
+  }
+  g_err = "unknown creation option";
+  return PNP_E_ARG;
+}
+
+extern "C" int pnp_get_create_option(int32_t option, int64_t *value) {
+  if (!value) return PNP_E_ARG;
+  if (option == PNP_CREATE_ABSORB_THIN_COLOR) {
+    *value = pnp::g_absorb_thin_color.load();
+    return PNP_OK;
+  }
+  g_err = "unknown creation option";
+  return PNP_E_ARG;
 }
 
 extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {

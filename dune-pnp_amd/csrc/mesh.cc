@@ -2,6 +2,7 @@
 #include "mesh.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -513,6 +514,8 @@ static inline uint64_t morton2(uint32_t x, uint32_t y) {
   return spread(x) | (spread(y) << 1);
 }
 
+std::atomic<int> g_absorb_thin_color{-1};
+
 bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &part, int rank,
                         int nranks, LocalLayout &L, std::string &err) {
   L = LocalLayout();
@@ -660,7 +663,8 @@ bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &pa
   // the SpMV and every other consumer keep the full matrix.  Only when at most 1/1024 of the rows
   // are left (PNP_COLOR_CONFLICTS=0 keeps the extra colour).
   const char *cc_env = std::getenv("PNP_COLOR_CONFLICTS");
-  const bool allow_conflicts = !(cc_env && cc_env[0] == '0');
+  const int cc_opt = g_absorb_thin_color.load();  // pnp_set_create_option, -1: the default
+  const bool allow_conflicts = cc_opt >= 0 ? cc_opt != 0 : !(cc_env && cc_env[0] == '0');
   auto absorb_top = [&](int top) -> bool {
     int ntop = 0;
     for (int v : owned) ntop += color[v] == top;

@@ -9,6 +9,8 @@
 //   RCB partition, colouring, Morton order and the SELL-64 block layout of the local problem.
 #pragma once
 
+#include <atomic>
+
 #include <array>
 #include <cstdint>
 #include <map>
@@ -122,6 +124,9 @@ struct LocalLayout {
   std::vector<int> recv_ptr, send_ptr, send_idx;
 };
 
+// PNP_CREATE_ABSORB_THIN_COLOR (pnp_set_create_option): -1 default (on, unless the environment
+// variable PNP_COLOR_CONFLICTS=0), 0 off, 1 on -- read by build_local_layout
+extern std::atomic<int> g_absorb_thin_color;
 bool build_local_layout(const Mesh &m, const Fans &f, const std::vector<int> &part, int rank,
                         int nranks, LocalLayout &L, std::string &err);
 

@@ -22,10 +22,25 @@
 #include <cmath>
 #include <vector>
 
+#include <atomic>
+
 #include "kernels.h"
 #include "pk.h"
 
 namespace pnp {
+
+// per-device "done" flags (bit = HIP device id) for function attributes, which are set per device:
+// a second context on another device in the same process sets them again
+static bool dev_flag_test(const std::atomic<uint64_t> &m) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return false;
+  return (m.load() >> d) & 1;
+}
+static void dev_flag_set(std::atomic<uint64_t> &m) {
+  int d = 0;
+  if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < 64) m.fetch_or(uint64_t(1) << d);
+}
+
 
 namespace {
 
@@ -920,12 +935,12 @@ hipError_t jac_launch2(const DevLayout &L, const PkDev &D, const double *x, cons
                        const double *aux1, const PkArgs &a, const double *cvec_in,
                        const uint8_t *dmask, double *r, double *vals, hipStream_t s) {
   const size_t lds = size_t(L.max_slots) * kB * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<uint64_t> attr{0};  // per device: the attribute is a per-device setting
+  if (!dev_flag_test(attr)) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pk_jac_gather<K>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr = true;
+    dev_flag_set(attr);
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_pk_elem_jac<K>, dim3((D.ne + kBE - 1) / kBE), dim3(kBE), 0, s, D, L.xy, x,
@@ -955,12 +970,13 @@ hipError_t row_launch1(const DevLayout &L, const PkDev &D, const double *x, cons
                        const uint8_t *dmask, double *r, double *cvec_out, double *vals,
                        hipStream_t s) {
   const size_t lds = JAC ? size_t(L.max_slots) * kB * sizeof(double) : 0;
-  static bool attr = false;  // up to 160 KB of LDS per workgroup on gfx950 (P3: 55 slots)
-  if (JAC && !attr) {
+  // up to 160 KB of LDS per workgroup on gfx950 (P3: 55 slots); set once per device
+  static std::atomic<uint64_t> attr{0};
+  if (JAC && !dev_flag_test(attr)) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pk_row<K, JAC>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr = true;
+    dev_flag_set(attr);
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int nwg = (L.n_owned + kB - 1) / kB;

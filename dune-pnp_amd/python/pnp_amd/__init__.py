@@ -36,6 +36,7 @@ METHOD_BICGSTAB, METHOD_CG = 0, 1
 (OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD, OPT_BICG_TWORED, OPT_AMG_FALLBACK,
  OPT_GRAPH) = 1, 2, 3, 4, 5, 6
 DEVICE_PTRS, JAC_FD = 1, 2
+CREATE_ABSORB_THIN_COLOR = 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
                 "jacobi": PREC_JACOBI, "amg": PREC_AMG, "ssor_natural": PREC_SSOR_NATURAL}
 MAX_SURFACES = 64
@@ -408,6 +409,17 @@ class Layout:
 # ------------------------------------------------------------------------------------------------
 # GPU context
 # ------------------------------------------------------------------------------------------------
+def set_create_option(option, value):
+    """Process-wide option read by every later Context / Layout creation (pnp_set_create_option)."""
+    _check(lib().pnp_set_create_option(option, C.c_int64(value)))
+
+
+def get_create_option(option):
+    v = C.c_int64(0)
+    _check(lib().pnp_get_create_option(option, C.byref(v)))
+    return v.value
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(lib().pnp_rccl_unique_id(buf))

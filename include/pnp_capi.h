@@ -364,6 +364,20 @@ enum {
   PNP_OPT_GRAPH = 6
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
+
+/* ---- creation options (process-wide; read by every later pnp_create / pnp_create_pk /
+ * pnp_layout_build, since the row colouring and the layout are built at creation) ------------ */
+enum {
+  /* the thin top colour of the greedy colouring (at most 1/1024 of the rows, each coupled to all
+   * colours below) is absorbed into the colours below, and its few same-colour couplings
+   * (pnp_info.color_conflicts) are left out of the multicolour SSOR / ILU(0) sweeps: one colour
+   * -- two sweep launches per preconditioner application -- fewer.  1 on (default), 0 off (the
+   * sweeps act on the whole matrix, one colour more), -1 the default (the environment variable
+   * PNP_COLOR_CONFLICTS=0 turns it off).  DESIGN.md §4.1. */
+  PNP_CREATE_ABSORB_THIN_COLOR = 1
+};
+int pnp_set_create_option(int32_t option, int64_t value);
+int pnp_get_create_option(int32_t option, int64_t *value);
 int pnp_get_option(pnp_ctx *ctx, int32_t option, int64_t *value);
 
 /* solve J z = rhs with the last assembled Jacobian; rhs, z host, external layout */

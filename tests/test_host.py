@@ -207,3 +207,22 @@ def test_driver_builds_and_fails_loudly_without_gpu(tmp_path):
     out = subprocess.run([exe, os.path.join(DATA, "cylinder_config.cfg")], capture_output=True,
                          text=True)
     assert out.returncode == 1 and "hip" in out.stderr.lower()
+
+
+def test_create_option_absorb_thin_color():
+    """PNP_CREATE_ABSORB_THIN_COLOR (pnp_set_create_option): on pore_pnp/pore.msh the greedy +
+    Kempe colouring leaves a thin fifth colour; absorbed (default) it gives 4 colours and 2
+    same-colour couplings outside the sweeps, off it keeps 5 colours and no conflict."""
+    m = P.Mesh.read_gmsh(os.path.join(DATA, "pore_pnp", "pore.msh"))
+    assert P.get_create_option(P.CREATE_ABSORB_THIN_COLOR) == -1
+    try:
+        P.set_create_option(P.CREATE_ABSORB_THIN_COLOR, 1)
+        on = P.Layout(m)
+        P.set_create_option(P.CREATE_ABSORB_THIN_COLOR, 0)
+        off = P.Layout(m)
+    finally:
+        P.set_create_option(P.CREATE_ABSORB_THIN_COLOR, -1)
+    assert (len(on.color_ptr) - 1, on.color_conflicts) == (4, 2)
+    assert (len(off.color_ptr) - 1, off.color_conflicts) == (5, 0)
+    with pytest.raises(P.PnpError):
+        P.set_create_option(P.CREATE_ABSORB_THIN_COLOR, 2)
