@@ -689,9 +689,18 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     const char *e = getenv("PNP_ASM_LDS");
     return e ? (atoi(e) == 1 ? 1 : 0) : -1;
   }();
+  // The Jacobian assembly inside Newton follows a BiCGSTAB solve, whose matrix and vector streams
+  // have replaced the assembly's inputs in the caches: such a launch (a.cold, set by the context
+  // after a solve) is cache-cold at any size and takes the LDS-staged walk too (config 3 in situ:
+  // profiles/r03/ab_asm_cold_hint.log); PNP_ASM_COLD_HINT=0 ignores the hint (A/B)
+  static const bool cold_hint = [] {
+    const char *e = getenv("PNP_ASM_COLD_HINT");
+    return !(e && e[0] == '0');
+  }();
   const auto lds_walk = [&](int nk) {
     return lds_env == 1 ||
-           (lds_env < 0 && size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(512) << 20));
+           (lds_env < 0 && (size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(512) << 20) ||
+                            (cold_hint && a.cold)));
   };
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \

@@ -203,6 +203,7 @@ struct pnp_ctx {
   DBuf<uint8_t> dmask;
   DBuf<double> cvec, aux0, aux1;
   bool assembled = false;
+  bool after_solve = false;  // a linear solve ran since the last Jacobian assembly (AsmArgs::cold)
 
   // aggregation AMG (PNP_PREC_AMG, amg.h): the pattern hierarchy is built once per context (it
   // depends on the layout only), the coarse values after every assembly
@@ -611,6 +612,7 @@ struct pnp_ctx {
     aa.x = xdev;
     aa.jac = fd_mode ? 0 : jac;
     aa.r = r.p;
+    aa.cold = after_solve ? 1 : 0;
     hipEvent_t t0 = tb(T_ASM);
     hipError_t e;
     if (degree > 1)
@@ -628,6 +630,7 @@ struct pnp_ctx {
       split_of = 0;
       amg_valid = false;
       csr_vals_valid = false;
+      after_solve = false;
     }
     return PNP_OK;
   }
@@ -1525,6 +1528,7 @@ struct pnp_ctx {
   // the linear solver selected by o.method
   int krylov(const double *bdev, double *zout, const pnp_solve_opts &o, pnp_solve_result &res) {
     int rc;
+    after_solve = true;
     if (o.method == PNP_METHOD_CG) {
       amg_symmetric = true;
       rc = cg(bdev, zout, o, res);
@@ -3039,6 +3043,7 @@ extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_
                     c->stream),
      "rhs");
   c->amg_symmetric = false;  // as in krylov(): BiCGSTAB
+  c->after_solve = true;
   int rc = c->bicgstab(c->b.p, c->z.p, o, *res, n);
   c->amg_symmetric = true;
   return rc;

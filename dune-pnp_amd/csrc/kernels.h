@@ -273,6 +273,8 @@ struct AsmArgs {
   const uint8_t *dmask;  // Dirichlet mask [n_owned * NF]
   double *r;             // [n_owned * NF]
   double *vals;          // SELL values
+  int cold;              // 1: the launch follows a linear solve (Newton's Jacobian): its inputs are
+                         // out of the caches, and the Jacobian takes the LDS-staged walk
 };
 
 // BiCGSTAB scalar block, resident on the device (no host round trip per half step)

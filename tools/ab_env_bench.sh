@@ -16,7 +16,9 @@ import json
 d = json.loads(open("/tmp/ab_line.json").read())
 t = d["event_timers_ms"]
 n = d["pnp_newton_time_to_solution"]
-msg = (f"asm {d['roofline']['avg_launch_us']:.1f} us cold {d['roofline_cold']['avg_launch_us']:.1f} us | "
+situ = d.get("roofline_in_situ") or {}
+msg = (f"asm {d['roofline']['avg_launch_us']:.1f} us cold {d['roofline_cold']['avg_launch_us']:.1f} us "
+       f"in-situ {situ.get('avg_launch_us', float('nan')):.1f} us | "
        f"bicg {d['bicgstab_ms_per_iter']*1e3:.1f} us/it  prec/apply {t['prec_ms']/max(1,t['prec_launches'])*1e3:.1f} us "
        f"spmv {t['spmv_ms']/max(1,t['spmv_launches'])*1e3:.1f} us blas/it {t['blas_ms']/20*1e3:.1f} us")
 if n:
