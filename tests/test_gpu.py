@@ -654,6 +654,10 @@ def test_two_reduction_bicgstab_keeps_istl_counts(prec):
         ctx.set_option(P.OPT_BICG_TWORED, tr)
         out[tr] = ctx.linear_solve(b, prec=prec, reduction=1e-8, maxit=20000)
     assert out[0][1]["converged"] == 1 and out[1][1]["converged"] == 1
-    assert abs(out[0][1]["it_half"] - out[1][1]["it_half"]) <= 0.1 * out[0][1]["it_half"] + 0.5
+    # without a preconditioner the ~1,000-iteration run is chaotic in the last bits (the oracle
+    # spans 697 .. 1,282 iterations on a like system under 1e-14 perturbations, see
+    # test_bicgstab_nonprec_matches_oracle_on_long_run): 30 % there, 10 % with a preconditioner
+    tol = 0.3 if prec == P.PREC_NONE else 0.1
+    assert abs(out[0][1]["it_half"] - out[1][1]["it_half"]) <= tol * out[0][1]["it_half"] + 0.5
     for tr in (0, 1):
         assert np.linalg.norm(J @ out[tr][0] - b) <= 1.001e-8 * np.linalg.norm(b)
