@@ -46,7 +46,7 @@ import pnp_amd as P  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured copy rate is in
 #                       the line (`measured_copy_gbs`)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
 SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
 
 
@@ -54,7 +54,7 @@ def pmc_traffic(kernel_prefix):
     """Per-launch HBM-side bytes of a kernel from the committed rocprofv3 PMC summary, or None."""
     try:
         with open(PMC_SUMMARY if os.path.exists(PMC_SUMMARY)
-                  else PMC_SUMMARY.replace("r02", "r01")) as f:
+                  else PMC_SUMMARY.replace("r03", "r02")) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
@@ -623,7 +623,7 @@ def main():
                                         "bytes, not counted HBM bytes",
                          "hbm_gbs_from_traffic": (traffic / aw["seconds"] / 1e9) if traffic
                                                  else None,
-                         "traffic_source": "profiles/r02/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
+                         "traffic_source": "profiles/r03/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
                                            "+ WRITE_SIZE per launch, separate passes)",
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
                          "bytes_per_launch": aw["bytes"], "avg_launch_us": aw["seconds"] * 1e6,

@@ -226,7 +226,7 @@ struct pnp_ctx {
 
 
   // vectors (sized n_local * 3)
-  DBuf<double> x, r, rs, z, rt, p, v, t, y, b, prevu, ext, sendbuf, partials, partials2;
+  DBuf<double> x, r, rs, z, rt, p, v, t, y, y2, b, prevu, ext, sendbuf, partials, partials2;
   std::vector<int> newton_its;        // pnp_newton_history: linear iterations per Newton step
   std::vector<double> newton_defects; // and the defect after each step
   DBuf<pnp::Scalars> S;
@@ -1324,6 +1324,15 @@ struct pnp_ctx {
     // PNP_OPT_BICG_TWORED (or PNP_BICG_TWORED) 0/1 forces it off/on.  Half-step counts keep
     // ISTL's semantics.
     const bool twored = twored_opt >= 0 ? twored_opt == 1 : dist;
+    // fused ILU(0), one reduction per half step: the first half step's x += alpha y is applied by
+    // the second half's update (one read and write of x per iteration fewer; the second
+    // preconditioned vector then goes to y2).  PNP_XDEFER=0 keeps the two passes (A/B).
+    static const bool xdefer_env = [] {
+      const char *ev = std::getenv("PNP_XDEFER");
+      return !(ev && std::atoi(ev) == 0);
+    }();
+    const bool xdefer = xdefer_env && fuse && !twored;
+    double *const y2p = xdefer ? y2.p : y.p;
     int pending_np = 0;
     // one BiCGSTAB iteration; for k >= 1 (and without the two-reduction variant's host state) it
     // launches the same kernels with the same arguments every time, which is what the graph
@@ -1360,9 +1369,9 @@ struct pnp_ctx {
       // iteration (twored): also <rt, s> into partials2, for rho_new without a third reduction.
       t0 = tb(T_BLAS);
       if (fuse)
-        e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, zout, yin, rs.p, v.p, nullptr,
-                                    uvals.p, y.p, partials2.p, &npu, stream, f32_now(),
-                                    twored ? rt.p : nullptr);
+        e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, xdefer ? nullptr : zout, yin,
+                                    rs.p, v.p, nullptr, uvals.p, y2p, partials2.p, &npu, stream,
+                                    f32_now(), twored ? rt.p : nullptr);
       else
         e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, twored ? rt.p : nullptr,
                                   partials2.p, stream);
@@ -1371,8 +1380,8 @@ struct pnp_ctx {
       // y = M^{-1} r ; t = A y ; <t,r>, <t,t> (twored: and <t,rt>)
       const double *yin2 = rs.p;
       if (fuse) {
-        if ((rc = ilu_from1(rs.p, y.p))) return rc;
-        yin2 = y.p;
+        if ((rc = ilu_from1(rs.p, y2p))) return rc;
+        yin2 = y2p;
       } else if (prec != PNP_PREC_NONE) {
         if ((rc = precond(prec, rs.p, y.p))) return rc;
         yin2 = y.p;
@@ -1391,7 +1400,8 @@ struct pnp_ctx {
         if ((rc = reduce_derive2(nsp, 2, fuse ? npu : np, 1, 23))) return rc;
         // x += omega y ; r -= omega t ; ||r||, <rt, r>
         t0 = tb(T_BLAS);
-        e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream);
+        e = pnp::launch_update_xr(n, S.p, 1, zout, yin2, rs.p, t.p, rt.p, partials.p, stream,
+                                  xdefer ? yin : nullptr);
         if (e != hipSuccess) return hipfail(e, "update x r (2)");
         if ((rc = reduce_derive(np, 2, 4))) return rc;
         te(T_BLAS, t0);
@@ -2143,7 +2153,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       (rc = al(c->fluxred, 2 * 256, "flux reduce")) || (rc = al(c->x, nv3, "x")) ||
       (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
       (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
-      (rc = al(c->y, nv3, "y")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
+      (rc = al(c->y, nv3, "y")) || (rc = al(c->y2, nv3, "y2")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
       (rc = al(c->ext, 3 * size_t(c->mesh.nv), "ext")) ||
       (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
       // up to 3 partials per workgroup (SpMV mode 4) / 2 (updates with <rt, s>)
@@ -2268,7 +2278,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->transport = c->comm ? 2 : (c->lg ? 1 : 0);
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
-                        c->b.n + c->prevu.n + c->ext.n) * 8;
+                        c->y2.n + c->b.n + c->prevu.n + c->ext.n) * 8;
   b += c->d_colidx.n * 4 + c->d_rowmeta.n * 8 + c->d_xy.n * 8;
   info->device_bytes = int64_t(b);
   return PNP_OK;

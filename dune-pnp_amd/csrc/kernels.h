@@ -287,6 +287,8 @@ struct Scalars {
   int iter;              // full iterations started
   int divguard;          // 1: stop with breakdown 4 once ||r|| > 1e10 ||r0|| (AMG solves)
   int pending;           // two-reduction iteration: the second half step's test is still due
+  int xpend;             // x += alpha y of the first half step deferred to the second half's
+                         // update (set by launch_update_fwd0 with x = null, cleared by stage 4)
 };
 
 // ---- launchers (return hipError_t of the launch) ----------------------------------------------
@@ -342,7 +344,8 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int 
                              double *out = nullptr, int f32 = 0);
 // BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
 // p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
-// r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0
+// r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0.
+// which 1 with x = null: x += alpha yin is left to launch_update_xr(.., y1 = yin) (S->xpend)
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
                               const double *v, double *p, const void *uv, double *yout,
@@ -358,9 +361,13 @@ hipError_t launch_update_p(long long n, const Scalars *S, const double *r, const
 hipError_t launch_cg_update_p(long long n, const Scalars *S, const double *q, double *p,
                               hipStream_t s);
 // x += a*y; r -= a*v; partials <r,r> [, <rt, r>];  a = S->alpha (which=0) or S->omega (which=1)
+// y1 != null (which 1): first x += alpha y1, the first half step's update that
+// launch_update_fwd0 deferred, then x += omega y -- the same two roundings as two passes, one
+// read and write of x fewer; with the first half step converged (S->done, S->xpend) only the
+// former
 hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x, const double *y,
                             double *r, const double *v, const double *rt, double *partials,
-                            hipStream_t s);
+                            hipStream_t s, const double *y1 = nullptr);
 // partials of <a,b> (and <a,a> if two)
 hipError_t launch_dot(long long n, const double *a, const double *b, int two, double *partials,
                       hipStream_t s);

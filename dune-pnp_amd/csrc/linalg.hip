@@ -1089,13 +1089,25 @@ __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars
                                                       double *__restrict__ r,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ rt,
-                                                      double *__restrict__ partials) {
-  if (S->done) return;
-  const double a = which ? S->omega : S->alpha;
+                                                      double *__restrict__ partials,
+                                                      const double *__restrict__ y1) {
+  const double al = S->alpha;
+  if (S->done) {
+    if (!(y1 && S->xpend)) return;
+    // the first half step converged: its deferred x += alpha y1, as ISTL returns it
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
+         i += (long long)gridDim.x * kBlock)
+      x[i] += al * y1[i];
+    return;
+  }
+  const double a = which ? S->omega : al;
   double acc[2] = {0, 0};
   for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n;
        i += (long long)gridDim.x * kBlock) {
-    x[i] += a * y[i];
+    double xi = x[i];
+    if (y1) xi += al * y1[i];  // uniform
+    xi += a * y[i];
+    x[i] = xi;
     const double ri = r[i] - a * v[i];
     r[i] = ri;
     acc[0] += ri * ri;
@@ -1118,7 +1130,7 @@ __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars
 // row's y before the row's new y is written, by the same thread).
 template <int NF, int PAT, int WHICH, typename VT = double>
 __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
-                                                        const Scalars *__restrict__ S, int first,
+                                                        Scalars *S, int first,
                                                         double *__restrict__ x, const double *yin,
                                                         double *__restrict__ r,
                                                         const double *__restrict__ v,
@@ -1149,11 +1161,14 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     } else {
       const double a = S->alpha;
       double xi[NF], yi[NF];
-      load_nf<NF>(x, size_t(row), xi);
-      load_nf<NF>(yin, size_t(row), yi);
+      if (x) {  // uniform; null: deferred to k_update_xr (S->xpend)
+        load_nf<NF>(x, size_t(row), xi);
+        load_nf<NF>(yin, size_t(row), yi);
+#pragma unroll
+        for (int f = 0; f < NF; f++) xi[f] += a * yi[f];
+      }
 #pragma unroll
       for (int f = 0; f < NF; f++) {
-        xi[f] += a * yi[f];
         d[f] -= a * vv[f];
         ss += d[f] * d[f];
       }
@@ -1163,7 +1178,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
 #pragma unroll
         for (int f = 0; f < NF; f++) rs += ti[f] * d[f];
       }
-      store_nf<NF>(x, size_t(row), xi);
+      if (x) store_nf<NF>(x, size_t(row), xi);
       store_nf<NF>(r, size_t(row), d);
     }
     if (row < c0_end) {
@@ -1175,6 +1190,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     }
   }
   if (WHICH == 1) {
+    if (!x && blockIdx.x == 0 && threadIdx.x == 0) S->xpend = 1;  // read by k_update_xr only
     if (rt) {  // uniform over the grid
       double a2[2] = {ss, rs};
       block_sum<2>(a2, partials + 2 * blockIdx.x);
@@ -1233,7 +1249,10 @@ __global__ __launch_bounds__(kRedBlock) void k_reduce(const double *__restrict__
                                                       const double *__restrict__ pb, int npb,
                                                       Scalars *__restrict__ S, int stage) {
   // the start stages (0 BiCGSTAB, 10 CG) run on a fresh state; everything else stops once done
-  if (S->done && stage != 0 && stage != 10) return;
+  if (S->done && stage != 0 && stage != 10) {
+    if (stage == 4 && threadIdx.x == 0) S->xpend = 0;  // (derive's stage 4 clears it otherwise)
+    return;
+  }
   double acc[KA + KB];
 #pragma unroll
   for (int j = 0; j < KA + KB; j++) acc[j] = 0;
@@ -1271,6 +1290,7 @@ __device__ void derive(Scalars *S, int stage) {
     S->done = S->norm0 < 1e-30 ? 1 : 0;
     return;
   }
+  if (stage == 4) S->xpend = 0;  // the deferred x update (if any) was applied by k_update_xr
   if (S->done) return;
   if (stage == 11) {  // CG: rho = <M^{-1} r, r>
     S->rho = S->red[0];
@@ -1780,6 +1800,7 @@ hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, c
                               double *partials, int *nparts, hipStream_t s, int f32,
                               const double *rt) {
   const dim3 g = rows_grid(L.n_owned);
+  Scalars *Sw = const_cast<Scalars *>(S);  // which 1 with x = null sets S->xpend
   if (nparts) *nparts = int(g.x);
   if (L.n_owned == 0) return hipSuccess;
   auto run = [&](auto vt) -> hipError_t {
@@ -1787,10 +1808,10 @@ hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, c
     const VT *uv = static_cast<const VT *>(uvp);
     PNP_PAT_DISPATCH(nf, pat, {
       if (which == 0)
-        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT>), g, dim3(kBlock), 0, s, L, c0_end, Sw,
                            first, x, yin, r, v, p, uv, yout, partials, nullptr);
       else
-        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT>), g, dim3(kBlock), 0, s, L, c0_end, S,
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT>), g, dim3(kBlock), 0, s, L, c0_end, Sw,
                            first, x, yin, r, v, p, uv, yout, partials, rt);
     });
     return hipGetLastError();
@@ -1842,13 +1863,13 @@ hipError_t launch_cg_update_p(long long n, const Scalars *S, const double *q, do
 
 hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x, const double *y,
                             double *r, const double *v, const double *rt, double *partials,
-                            hipStream_t s) {
+                            hipStream_t s, const double *y1) {
   if (rt)
     hipLaunchKernelGGL(k_update_xr<1>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, which, x, y,
-                       r, v, rt, partials);
+                       r, v, rt, partials, y1);
   else
     hipLaunchKernelGGL(k_update_xr<0>, dim3(blas_nparts(n)), dim3(kBlock), 0, s, n, S, which, x, y,
-                       r, v, rt, partials);
+                       r, v, rt, partials, y1);
   return hipGetLastError();
 }
 

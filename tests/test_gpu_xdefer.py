@@ -1,0 +1,83 @@
+"""BiCGSTAB with the first half step's x += alpha y deferred into the second half step's update
+(launch_update_xr with y1; the default on the fused ILU(0) path with one reduction per half step)
+against the two separate x passes (PNP_XDEFER=0), -m gpu.  The deferred update performs the same
+two roundings in the same order, so iterates, half-step counts and Newton trajectories must be
+bitwise the same: on the small golden systems (graph replay on and off), for solves that end
+after a first half step (x = x + alpha y only), and at config 3 (pore_pnp refined 4x, eager
+launches).  The knob is read once per process, so each variant runs in a child process."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CHILD = r"""
+import hashlib, json, os, sys
+import numpy as np
+sys.path.insert(0, HERE)
+import conftest  # noqa: F401  (puts the package on the path)
+from test_gpu import golden
+import pnp_amd as P
+out = {}
+def h(a):
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+for name in ("pore_small_k0", "cylinder_k0"):
+    z, mesh, par, orc = golden(name)
+    x = z["newton_pnp_x0"]
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    ctx.jacobian(x, export=False)
+    rhs = ctx.residual(x)
+    for f32 in (1, 0):
+        ctx.set_option(P.OPT_ILU_F32, f32)
+        for red in (1e-10, 1e-2, 1e-3, 1e-4, 1e-6):
+            sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=red, maxit=20000)
+            out[f"{name}solve{f32}_{red}"] = [h(sol), res["iterations"], res["it_half"]]
+    ctx.set_option(P.OPT_ILU_F32, 1)
+    ctx.set_option(P.OPT_GRAPH, 0)
+    sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=1e-10, maxit=20000)
+    out[f"{name}eager"] = [h(sol), res["iterations"], res["it_half"]]
+    ctx.set_option(P.OPT_GRAPH, -1)
+    ctx.set_operator(P.OP_PB)
+    phi, rpb = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(x0, prec=P.PREC_ILU0)
+    out[f"{name}newton"] = [h(u), res["linear_iterations"], h(ctx.newton_history()[1])]
+cfg = P.read_config(os.path.join(os.path.dirname(HERE), "data", "pore_pnp", "pore.cfg"))
+mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(4)
+ctx = P.Context(mesh, P.Params.from_config(cfg))
+ctx.set_operator(P.OP_PNP)
+rng = np.random.default_rng(20261017)
+nv = mesh.nv
+x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                    0.06 * rng.uniform(0.5, 1.5, nv)])
+ctx.jacobian(x, export=False)
+rhs = ctx.residual(x)
+for red in (1e-4, 1e-3, 1e-2):
+    sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=red, maxit=400)
+    out[f"config3_{red}"] = [h(sol), res["iterations"], res["it_half"], res["converged"]]
+print("RESULT " + json.dumps(out))
+"""
+
+
+def run(**knobs):
+    env = dict(os.environ, **{k: str(v) for k, v in knobs.items()})
+    code = CHILD.replace("HERE", repr(HERE))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=HERE)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")][-1]
+    return json.loads(line[len("RESULT "):])
+
+
+def test_deferred_x_update_is_bitwise_the_two_passes():
+    ref = run(PNP_XDEFER=0)
+    got = run()
+    assert got == ref
+    # the half-step exits are exercised (a loose reduction ends some solves half way)
+    assert any(v[2] != int(v[2]) for k, v in got.items() if "solve" in k or "config3" in k)
