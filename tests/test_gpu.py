@@ -159,9 +159,10 @@ def test_jacobian_parity_full_size():
     assert abs(J - Jo).max() <= 1e-12 * abs(Jo).max()
 
 
-def test_residual_parity_config5():
+def test_residual_and_jacobian_parity_config5():
     """Config 5 (test/pore_without_dna's .geo meshed natively, scale 0.85, refined k=6: 8.87 M DOF,
-    the north star's system): residual vs the oracle, 1e-12 of max|r|."""
+    the north star's system): residual and analytic Jacobian entry by entry vs the oracle, 1e-12
+    of max|r| and of max|J|."""
     cfg = P.read_config(os.path.join(DATA, "pore_without_dna", "pore.cfg"))
     mesh = P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(6)
     par = P.Params.from_config(cfg)
@@ -176,10 +177,14 @@ def test_residual_parity_config5():
     ctx = P.Context(mesh, par)
     ctx.set_operator(P.OP_PNP)
     r = ctx.residual(x)
+    J = ctx.jacobian(x)
     ctx.close()
     op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
     ro = orc.residual(op, x)
     assert np.max(np.abs(r - ro)) <= 1e-12 * np.max(np.abs(ro))
+    Jo = orc.jacobian(op, x)
+    assert J.shape == Jo.shape == (3 * nv, 3 * nv)
+    assert abs(J - Jo).max() <= 1e-12 * abs(Jo).max()
 
 
 @pytest.mark.parametrize("kind,prec", [("pnp", P.PREC_NONE), ("pnp", P.PREC_SSOR),
