@@ -187,11 +187,26 @@ struct pnp_ctx {
   DBuf<unsigned char> csr_vidx;
   DBuf<double> csr_val;
   bool csr_vals_valid = false;  // csr_val holds the current Jacobian
-  // natural-order SSOR (PNP_PREC_SSOR_NATURAL, ssor_natural.hip): level schedule of the forward
-  // and backward sweeps over the external-layout rows (built with the CSR structure), the
-  // position of each row's diagonal, and external-layout work vectors
-  std::vector<int> nat_lptr_f, nat_lptr_b;
-  DBuf<int> nat_rows_f, nat_rows_b, nat_diag;
+  // natural-order SSOR (PNP_PREC_SSOR_NATURAL, ssor_natural.hip): level schedules of the forward
+  // and backward sweeps over the external-layout rows with each level's rows as an ELL over the
+  // CSR (pnp::NatSweep; built with the CSR structure), and external-layout work vectors
+  struct NatDir {
+    std::vector<int> lptr;
+    std::vector<long long> eoff;
+    DBuf<int4> info;
+    DBuf<int> ecol, eidx;
+    pnp::NatSweep view() const {
+      pnp::NatSweep w;
+      w.nlev = int(lptr.size()) - 1;
+      w.lptr = lptr.data();
+      w.eoff = eoff.data();
+      w.info = info.p;
+      w.ecol = ecol.p;
+      w.eidx = eidx.p;
+      return w;
+    }
+  };
+  NatDir nat_f, nat_b;
   DBuf<double> nat_d, nat_v;
   int nat_pat = -1, nat_nf = 0;
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
@@ -287,7 +302,17 @@ struct pnp_ctx {
     hipGraphExec_t exec = nullptr;
   };
   std::vector<GraphSlot> graph_cache;
+  // the natural-order SSOR's level launches (ssor_natural.hip: ~2 x 131 levels per field sweep
+  // at pore_pnp k=3) replayed as one graph: their arguments are context buffers only
+  hipGraphExec_t nat_exec = nullptr;
+  bool nat_graph_failed = false;
+  void nat_graph_clear() {
+    if (nat_exec) hipGraphExecDestroy(nat_exec);
+    nat_exec = nullptr;
+    nat_graph_failed = false;
+  }
   void graphs_clear() {
+    nat_graph_clear();
     for (auto &g : graph_cache)
       if (g.exec) hipGraphExecDestroy(g.exec);
     graph_cache.clear();
@@ -642,6 +667,7 @@ struct pnp_ctx {
   int csr_structure() {
     const int nv = mesh.nv, mask = pat & 0x1FF;
     if (csr_pat == mask && csr_nf == nf) return PNP_OK;
+    nat_graph_clear();  // its buffers are rebuilt below
     const int n = nf * nv;
     std::vector<int> cnt(n + 1, 0);
     for (int i = 0; i < L.n_owned; i++) {
@@ -700,7 +726,8 @@ struct pnp_ctx {
         if (col[k] == R) diag[R] = k;
     for (int R = 0; R < n; R++)
       if (!empty(R) && diag[R] < 0) return fail(PNP_E_STATE, "natural SSOR: row without diagonal");
-    auto schedule = [&](bool fwd, std::vector<int> &lptr, DBuf<int> &rows) -> int {
+    auto schedule = [&](bool fwd, NatDir &W) -> int {
+      std::vector<int> &lptr = W.lptr;
       std::vector<int> lev(n, -1), push(n, 0);
       int nlev = 0;
       for (int s = 0; s < n; s++) {
@@ -725,11 +752,35 @@ struct pnp_ctx {
       std::vector<int> fill(lptr.begin(), lptr.end() - 1), rl(std::max(1, lptr[nlev]));
       for (int R = 0; R < n; R++)
         if (lev[R] >= 0) rl[fill[lev[R]]++] = R;
-      return upv(rows, rl, "natural SSOR rows");
+      // per level a column-major ELL of its rows' entries (CSR order), width = its longest row,
+      // padding slots with value index -1
+      std::vector<int4> info(std::max(1, lptr[nlev]));
+      W.eoff.assign(nlev + 1, 0);
+      for (int l = 0; l < nlev; l++) {
+        int w = 0;
+        for (int t = lptr[l]; t < lptr[l + 1]; t++) w = std::max(w, cnt[rl[t] + 1] - cnt[rl[t]]);
+        W.eoff[l + 1] = W.eoff[l] + (long long)w * (lptr[l + 1] - lptr[l]);
+      }
+      std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), 0), eidx(ecol.size(), -1);
+      for (int l = 0; l < nlev; l++) {
+        const int nl = lptr[l + 1] - lptr[l];
+        for (int t = lptr[l]; t < lptr[l + 1]; t++) {
+          const int R = rl[t], len = cnt[R + 1] - cnt[R];
+          info[t] = make_int4(R, len, diag[R], 0);
+          for (int k = 0; k < len; k++) {
+            const size_t q = size_t(W.eoff[l]) + size_t(k) * nl + (t - lptr[l]);
+            ecol[q] = col[cnt[R] + k];
+            eidx[q] = cnt[R] + k;
+          }
+        }
+      }
+      int rc2;
+      if ((rc2 = upv(W.info, info, "natural SSOR rows")) ||
+          (rc2 = upv(W.ecol, ecol, "natural SSOR columns")))
+        return rc2;
+      return upv(W.eidx, eidx, "natural SSOR entries");
     };
-    if ((rc = schedule(true, nat_lptr_f, nat_rows_f)) ||
-        (rc = schedule(false, nat_lptr_b, nat_rows_b)) || (rc = upv(nat_diag, diag, "ssor diag")))
-      return rc;
+    if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
     if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess)
       return hipfail(e, "natural SSOR vectors");
     csr_nnz = nnz;
@@ -757,13 +808,46 @@ struct pnp_ctx {
     hipError_t e = hipMemsetAsync(nat_v.p, 0, sizeof(double) * nat_v.n, stream);
     if (e == hipSuccess)
       e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
-    if (e == hipSuccess)
-      e = pnp::launch_ssor_natural(int(nat_lptr_f.size()) - 1, nat_lptr_f.data(), nat_rows_f.p,
-                                   int(nat_lptr_b.size()) - 1, nat_lptr_b.data(), nat_rows_b.p,
-                                   csr_rowptr.p, csr_col.p, csr_val.p, nat_diag.p, nat_d.p,
-                                   nat_v.p, stream);
+    if (e == hipSuccess) e = ssor_natural_levels();
     if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
     return e;
+  }
+  // the level launches: one graph replay (captured on first use; PNP_NAT_GRAPH=0: eager), or eager
+  // when the stream is itself being captured (a BiCGSTAB block graph then holds them), with more
+  // than one rank, or after a failed capture
+  hipError_t ssor_natural_levels() {
+    auto issue = [&] {
+      return pnp::launch_ssor_natural(nat_f.view(), nat_b.view(), csr_val.p, nat_d.p, nat_v.p,
+                                      stream);
+    };
+    static const bool env_on = [] {
+      const char *ev = std::getenv("PNP_NAT_GRAPH");
+      return !(ev && std::atoi(ev) == 0);
+    }();
+    // not with more than one rank: in-process ranks share the device, and another rank's thread
+    // touching the legacy stream during a capture would invalidate it
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (!env_on || dist || nat_graph_failed || hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+        cs != hipStreamCaptureStatusNone)
+      return issue();
+    if (!nat_exec) {
+      hipError_t e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
+      if (e == hipSuccess) {
+        const hipError_t e1 = issue();
+        hipGraph_t g = nullptr;
+        const hipError_t e2 = hipStreamEndCapture(stream, &g);
+        e = e1 != hipSuccess ? e1 : e2;
+        if (e == hipSuccess) e = hipGraphInstantiate(&nat_exec, g, nullptr, nullptr, 0);
+        if (g) hipGraphDestroy(g);
+      }
+      if (e != hipSuccess || !nat_exec) {  // nothing of the capture ran: launch eagerly
+        (void)hipGetLastError();
+        nat_exec = nullptr;
+        nat_graph_failed = true;
+        return issue();
+      }
+    }
+    return hipGraphLaunch(nat_exec, stream);
   }
 
   // analytic (k-form) or forward-difference (expanded, kPat*FD) storage of the next Jacobian

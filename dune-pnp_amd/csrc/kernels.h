@@ -412,13 +412,21 @@ hipError_t launch_fd_jacobian(const DevLayout &L, const AsmArgs &aa, int nf, int
 hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *vals, long long nnz,
                            const int *src, const unsigned char *vidx, double *out, hipStream_t s);
 // ISTL SeqSSOR (k = 1, omega = 1) in the lexicographic DOF order (ssor_natural.hip): v = 0, then
-// the forward levels (lptr_f: nlev_f + 1 offsets into rows_f, host array) and the backward levels,
-// one launch per level; rowptr / col / val / diag: the external-layout CSR of the local matrix,
-// d / v external-layout vectors
-hipError_t launch_ssor_natural(int nlev_f, const int *lptr_f, const int *rows_f, int nlev_b,
-                               const int *lptr_b, const int *rows_b, const int *rowptr,
-                               const int *col, const double *val, const int *diag, const double *d,
-                               double *v, hipStream_t s);
+// the forward levels and the backward levels, one launch per level.  Per sweep direction
+// (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row,
+// entry count, index of the diagonal in val, 0}; the row's entries in CSR (ascending column)
+// order as a column-major ELL of the level, entry k of position t at eoff[l] + k n_l + (t -
+// lptr[l]) (eoff: host array; n_l = the level's row count): its column (ecol) and its index into
+// the external-layout CSR values val (eidx).  d / v: external-layout vectors.
+struct NatSweep {
+  int nlev = 0;
+  const int *lptr = nullptr;
+  const long long *eoff = nullptr;
+  const int4 *info = nullptr;
+  const int *ecol = nullptr, *eidx = nullptr;
+};
+hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
+                               const double *d, double *v, hipStream_t s);
 // read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
 hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 

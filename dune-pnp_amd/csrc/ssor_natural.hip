@@ -31,35 +31,64 @@ namespace pnp {
 namespace {
 constexpr int kB = 256;
 
+// A level is a short chain of dependent memory round trips per row, whatever its size, so the
+// sweep is laid out to keep that chain at two: the level's entries are a column-major ELL of its
+// rows (NatSweep: coalesced column / value-index loads that need nothing but the position, padding
+// marked by index -1), and each row is served by kL lanes, lane j loading entries j, j + kL, ...
+// (kS per pass) and forming their products.  Round trip 1: the row record and the ELL slots; round
+// trip 2: d, the diagonal and the gathered values.  The row's first lane then subtracts the
+// products in column order, taken from the other lanes by shuffles: the oracle's operations in
+// the oracle's order (only loads and products move; a padding slot contributes rhs - (+0.0), which
+// is rhs bit for bit).  One thread per row through rowptr, one entry at a time, took 14.1 ms per
+// application at config 3 (profiles/r03/ssor_natural_r3t.log).
+#ifndef NAT_KL
+#define NAT_KL 8  // lanes per row (build-flag A/B knob)
+#endif
+constexpr int kL = NAT_KL, kS = (24 + kL - 1) / kL, kC = kS * kL;  // PNP rows: <= 21 entries
 __global__ void __launch_bounds__(kB)
-    k_ssor_nat_level(const int *__restrict__ rows, int n, const int *__restrict__ rowptr,
-                     const int *__restrict__ col, const double *__restrict__ val,
-                     const int *__restrict__ diag, const double *__restrict__ d,
+    k_ssor_nat_level(const int4 *__restrict__ info, const int *__restrict__ ecol,
+                     const int *__restrict__ eidx, int n, int width,
+                     const double *__restrict__ val, const double *__restrict__ d,
                      double *__restrict__ v) {
-  const int t = blockIdx.x * kB + threadIdx.x;
-  if (t >= n) return;
-  const int R = rows[t];
-  double rhs = d[R];
-  const int k1 = rowptr[R + 1];
-  for (int k = rowptr[R]; k < k1; k++) rhs -= val[k] * v[col[k]];
-  v[R] += 1.0 * (rhs / val[diag[R]]);
+  const int g = blockIdx.x * kB + threadIdx.x, t = g / kL, j = g % kL;
+  const bool live = t < n;  // whole rows per wavefront: kL divides 64
+  const bool head = live && j == 0;
+  const int4 I = head ? info[t] : make_int4(0, 0, 0, 0);
+  const int base = (threadIdx.x % 64) - j;  // the row's first lane in the wavefront
+  double rhs = 0.0;
+  for (int kb = 0; kb < width; kb += kC) {  // uniform: width = the level's longest row
+    int c[kS], ix[kS];
+#pragma unroll
+    for (int u = 0; u < kS; u++) {
+      const int k = kb + j + u * kL;
+      const bool in = live && k < width;
+      c[u] = in ? ecol[size_t(k) * n + t] : 0;
+      ix[u] = in ? eidx[size_t(k) * n + t] : -1;
+    }
+    if (kb == 0 && head) rhs = d[I.x];
+    double pr[kS];
+#pragma unroll
+    for (int u = 0; u < kS; u++) pr[u] = ix[u] >= 0 ? val[ix[u]] * v[c[u]] : 0.0;
+#pragma unroll
+    for (int k = 0; k < kC; k++) {
+      const double p = __shfl(pr[k / kL], base + k % kL, 64);
+      if (head && kb + k < width) rhs -= p;
+    }
+  }
+  if (head) v[I.x] += 1.0 * (rhs / val[I.z]);
 }
 }  // namespace
 
-hipError_t launch_ssor_natural(int nlev_f, const int *lptr_f, const int *rows_f, int nlev_b,
-                               const int *lptr_b, const int *rows_b, const int *rowptr,
-                               const int *col, const double *val, const int *diag, const double *d,
-                               double *v, hipStream_t s) {
-  for (int l = 0; l < nlev_f; l++) {
-    const int n = lptr_f[l + 1] - lptr_f[l];
-    hipLaunchKernelGGL(k_ssor_nat_level, dim3((n + kB - 1) / kB), dim3(kB), 0, s,
-                       rows_f + lptr_f[l], n, rowptr, col, val, diag, d, v);
-  }
-  for (int l = 0; l < nlev_b; l++) {
-    const int n = lptr_b[l + 1] - lptr_b[l];
-    hipLaunchKernelGGL(k_ssor_nat_level, dim3((n + kB - 1) / kB), dim3(kB), 0, s,
-                       rows_b + lptr_b[l], n, rowptr, col, val, diag, d, v);
-  }
+hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
+                               const double *d, double *v, hipStream_t s) {
+  for (const NatSweep *W : {&fwd, &bwd})
+    for (int l = 0; l < W->nlev; l++) {
+      const int n = W->lptr[l + 1] - W->lptr[l];
+      const int width = n > 0 ? int((W->eoff[l + 1] - W->eoff[l]) / n) : 0;
+      hipLaunchKernelGGL(k_ssor_nat_level, dim3((n * kL + kB - 1) / kB), dim3(kB), 0, s,
+                         W->info + W->lptr[l], W->ecol + W->eoff[l], W->eidx + W->eoff[l], n,
+                         width, val, d, v);
+    }
   return hipGetLastError();
 }
 

@@ -206,3 +206,21 @@ def test_thin_color_absorption_tracks_iteration_drift(prec):
         assert rpb["converged"] == 1 and res["converged"] == 1
         assert np.linalg.norm(J @ sol - b) <= 1.001e-8 * np.linalg.norm(b)
     assert np.max(np.abs(out[1][4] - out[0][4])) <= 1e-6 * max(np.max(np.abs(out[0][4])), 1e-12)
+
+
+@pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("cylinder_k0", "pb")])
+def test_ssor_natural_level_graph_bitwise_equals_captured_and_eager(name, kind):
+    """The natural sweep's level launches replayed as their own graph (BiCGSTAB graphs off) equal
+    the same launches captured inside BiCGSTAB's block graphs (graphs on) bit for bit, and a
+    Newton solve repeats bitwise on the replayed graph."""
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    set_ops(z, ctx, orc, kind)
+    ctx.jacobian(z[kind + "_x"], export=False)
+    rhs = ctx.residual(z[kind + "_x"])
+    out = {}
+    for g in (1, 0, 0):
+        ctx.set_option(P.OPT_GRAPH, g)
+        sol, res = ctx.linear_solve(rhs, prec=P.PREC_SSOR_NATURAL, reduction=1e-10, maxit=5000)
+        out.setdefault(g, []).append((sol.tobytes(), res["iterations"], res["it_half"]))
+    assert out[1][0] == out[0][0] == out[0][1]
