@@ -1,6 +1,7 @@
 """PNP Newton with BiCGSTAB + aggregation AMG (ILU(0) smoother, the bench's configuration) on
 config 3, eager launches against hipGraph block replay (PNP_OPT_GRAPH 0 / -1), interleaved twice.
 Prints one JSON line per run.  usage: python tools/time_amg_graph.py"""
+import hashlib
 import json
 import os
 import sys
@@ -27,4 +28,4 @@ for g in (0, -1, 0, -1):
     dt = time.perf_counter() - t
     print(json.dumps({"graph": g, "seconds": dt, "newton_steps": res["iterations"],
                       "linear_iterations": res["linear_iterations"],
-                      "converged": res["converged"], "u_sha": hash(u.tobytes())}), flush=True)
+                      "converged": res["converged"], "u_sha1": hashlib.sha1(u.tobytes()).hexdigest()[:16]}), flush=True)
