@@ -14,7 +14,8 @@
 //
 // Schedule: a row depends on the rows it couples to (either direction of the pattern) that come
 // before it in the sweep.  Rows are grouped into levels (host, once per block pattern: the longest
-// chain of such dependencies ending in the row), and every level is one launch, one thread per row.
+// chain of such dependencies ending in the row), and every level is one launch (kL lanes per row,
+// below).
 // A row therefore reads its earlier neighbours' new values and its later neighbours' values before
 // they are touched -- zero in the forward sweep, the forward result in the backward sweep -- i.e.
 // exactly the sequential sweep's operands.  Each row's sum runs over its CSR row in ascending column
