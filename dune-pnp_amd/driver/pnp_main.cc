@@ -15,6 +15,11 @@
 //                  PNP_PREC_SSOR_NATURAL; bcgs_ssork_mc: the multicolour sweep, same method, other order)
 //                 [--degree k]   (md / pb modes: PDEGREE, src/instationary_pnp_from_pb_md.hh:26-28;
 //                                 the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111)
+//                 [--reference-solvers]  (stationary / pb / instationary: the reference's own
+//                                 choices, src/stationary_pnp_from_pb.hh:168-169,329-331 -- PB with
+//                                 ISTLBackend_NOVLP_BCGS_SSORk = --pb-prec ssor_natural, PNP with
+//                                 ISTLBackend_NOVLP_BCGS_NOPREC = --prec none; the defaults are the
+//                                 multicolour SSOR for both, same methods' faster relatives)
 // Multi-GPU: run one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment and
 // PNP_RCCL_ID_FILE pointing to a shared path (rank 0 writes the RCCL unique id there).
 #include <algorithm>
@@ -50,7 +55,8 @@ static void usage() {
       "                [--amg-smoother ssor|ilu0|jacobi]\n"
       "                [--out prefix] [--md-reduction r]\n"
       "                [--linear-solver bcgs_ssork|bcgs_ssork_mc|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
-      "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n");
+      "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n"
+      "                [--reference-solvers]  (PB: ISTL SeqSSOR in DOF order, PNP: no preconditioner)\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -202,6 +208,10 @@ int main(int argc, char **argv) {
     else if (a == "--linear-solver") linsolver = next();
     else if (a == "--abs-limit") abs_limit = std::atof(next().c_str());
     else if (a == "--degree") degree = std::atoi(next().c_str());
+    else if (a == "--reference-solvers") {
+      pb_prec = "ssor_natural";
+      prec = "none";
+    }
     else if (a == "--dump-steps") {
       std::string l = next();
       for (size_t p = 0; p < l.size();) {

@@ -358,6 +358,34 @@ def test_cpp_driver_matches_python_api(tmp_path):
     assert np.max(np.abs(u_drv - u)) <= 1e-8 * np.max(np.abs(u))
 
 
+def test_cpp_driver_reference_solvers(tmp_path):
+    """pnp_main --reference-solvers: the stationary driver with the reference's own linear solvers
+    (src/stationary_pnp_from_pb.hh:168-169 PB with BCGS_SSORk, :329-331 PNP with BCGS_NOPREC) --
+    PNP_PREC_SSOR_NATURAL for PB and no preconditioner for PNP -- equals the same sequence through
+    the Python mirror of the C ABI."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    out = subprocess.run([exe, cfgp, "--reference-solvers", "--out", str(tmp_path / "cyl")],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    u_drv = np.loadtxt(tmp_path / "cyl_pnp.dat").T.ravel()
+    cfg = P.read_config(cfgp)
+    mesh = P.Mesh.read_gmsh(cfg.meshfile)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    s = cfg.system
+    ctx.set_operator(P.OP_PB)
+    phi, rpb = ctx.newton(np.zeros(mesh.nv), reduction=s["newtonReduction"],
+                          min_linear_reduction=s["newtonMinLinearReduction"],
+                          prec=P.PREC_SSOR_NATURAL)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    u, res = ctx.newton(x0, reduction=s["newtonReduction"],
+                        min_linear_reduction=s["newtonMinLinearReduction"], prec=P.PREC_NONE)
+    assert res["converged"] == 1
+    assert np.max(np.abs(u_drv - u)) <= 1e-8 * np.max(np.abs(u))
+
+
 # ---- multicolour ILU(0) --------------------------------------------------------------------------
 # stored block patterns (dune-pnp_amd/csrc/kernels.h kPatPnp / kPatPnpIE): PnpOperator has no
 # c+/c- coupling; PnpTOperator's c- mass term lands in the c+ rows (quirk Q2) -> (1,2) present
