@@ -888,6 +888,9 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
 // staged is written during the launch.  Each row's sum runs over its slots in the order of
 // split_row_dot<.., 1, B>, so v is bitwise k_ilu0_solve's.  The row's own loads, its diagonal
 // block and its first slot batch's list positions and factor values are issued before the barrier.
+#ifndef ILU_SU
+#define ILU_SU 4  // staged list entries per thread issued together (build-flag A/B knob)
+#endif
 template <int NF, int PAT, int KIND, int B, int NT, int ADD = 0, typename VT = double>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, int r1, int blk0,
                                                            const VT *__restrict__ lv,
@@ -902,6 +905,11 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   const int bl = xcd_block(blockIdx.x, gridDim.x, 1);
   const bool live = r0 + bl * kBlock + int(threadIdx.x) < r1;
   const int pos = live ? r0 + bl * kBlock + int(threadIdx.x) : r0;
+  // the staging list's bounds first: they depend on nothing, so their round trip is the row
+  // metadata's (split_row) instead of one more in the chain before the barrier
+  const int *__restrict__ ptr = FWD ? L.lsx_ptr : L.usx_ptr;
+  const int *__restrict__ lst = FWD ? L.lsx_list : L.usx_list;
+  const int u0 = ptr[blk0 + bl], u1 = ptr[blk0 + bl + 1];
   const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, pos, live);
   const int row = R.row;
   double own[NF], Dg[NV];
@@ -910,8 +918,6 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   const int chunk = pos / kRows;
   const uint16_t *__restrict__ lix =
       (FWD ? L.lsx_idx + L.lchunk_off[chunk] : L.usx_idx + L.uchunk_off[chunk]) + R.lane;
-  const int *__restrict__ ptr = FWD ? L.lsx_ptr : L.usx_ptr;
-  const int *__restrict__ lst = FWD ? L.lsx_list : L.usx_list;
   const int s0 = FWD ? 0 : 1;
   // a batch's list positions and factor values (kept as stored, float or double, until used) do
   // not depend on the staging: the first batch is in flight with it
@@ -943,8 +949,30 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
     }
   };
   fetch(s0);
-  const int u0 = ptr[blk0 + bl], cnt = ptr[blk0 + bl + 1] - u0;
-  for (int k = threadIdx.x; k < cnt; k += kBlock) {
+  // the staging: up to kSU list entries per thread, their list loads, then their gathers, then the
+  // LDS stores (two round trips, not two per entry)
+  const int cnt = u1 - u0;
+  {
+    constexpr int kSU = ILU_SU;
+    int jj[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; u++) {
+      const int k = int(threadIdx.x) + u * kBlock;
+      jj[u] = k < cnt ? lst[u0 + k] : -1;
+    }
+    double t[kSU][NF];
+#pragma unroll
+    for (int u = 0; u < kSU; u++)
+      if (jj[u] >= 0) load_nf<NF>(v, size_t(jj[u]), t[u]);
+#pragma unroll
+    for (int u = 0; u < kSU; u++) {
+      const int k = int(threadIdx.x) + u * kBlock;
+      if (jj[u] >= 0)
+#pragma unroll
+        for (int f = 0; f < NF; f++) sx[k * NF + f] = t[u][f];
+    }
+  }
+  for (int k = int(threadIdx.x) + ILU_SU * kBlock; k < cnt; k += kBlock) {  // longer lists
     double t[NF];
     load_nf<NF>(v, size_t(lst[u0 + k]), t);
 #pragma unroll
