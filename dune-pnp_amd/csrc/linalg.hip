@@ -182,6 +182,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
 // (two lanes per row, even / odd slots, combined at the end; dot partials per 128 rows with the
 // same trees), so results and partials are bitwise those of k_spmv: the BiCGSTAB iterates and
 // iteration counts do not move (they are sensitive to the last bit on the pore system).
+#ifndef SPMV_SU
+#define SPMV_SU 4  // staged list entries per thread issued together (build-flag A/B knob)
+#endif
 template <int NF, int PAT, int MODE, int SB, int NT>
 __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *__restrict__ vals,
                                                      const double *__restrict__ x,
@@ -197,23 +200,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
   const int chunk = row / kRows, lane = row % kRows;
   const int off = live ? L.chunk_off[chunk] : 0, len = live ? L.chunk_len[chunk] : 0;
   const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
-  for (int k = threadIdx.x; k < cnt; k += kBlock) {
-    double t[NF];
-    load_nf<NF>(x, size_t(L.ulist[u0 + k]), t);
-#pragma unroll
-    for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
-  }
-  __syncthreads();
-  static_assert(SB == 2, "slot pairs: even slots into acc2[0], odd into acc2[1]");
-  double d[3] = {0, 0, 0};
-  double acc2[2][NF];
-#pragma unroll
-  for (int f = 0; f < NF; f++) acc2[0][f] = acc2[1][f] = 0;
   const uint16_t *__restrict__ lix = L.lidx + off + lane;
   const double *__restrict__ vc = vals + size_t(off) * NK;
-  for (int s0 = 0; s0 < len; s0 += SB) {
-    int li[SB];
-    double k[SB][NK];
+  // one slot pair's list positions and values (issuing the first pair before the staging barrier
+  // was measured: config 5 BiCGSTAB +2.5 %, profiles/r03/ab_spmv_staging.log)
+  auto fetch = [&](int s0, int (&li)[SB], double (&k)[SB][NK]) {
 #pragma unroll
     for (int b = 0; b < SB; b++) {
       const int sl = s0 + b;
@@ -228,6 +219,42 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
         for (int qq = 0; qq < NK; qq++) k[b][qq] = 0.0;
       }
     }
+  };
+  {  // up to SPMV_SU list entries per thread: list loads, then gathers, then LDS stores
+    int jj[SPMV_SU];
+#pragma unroll
+    for (int u = 0; u < SPMV_SU; u++) {
+      const int k = int(threadIdx.x) + u * kBlock;
+      jj[u] = k < cnt ? L.ulist[u0 + k] : -1;
+    }
+    double t[SPMV_SU][NF];
+#pragma unroll
+    for (int u = 0; u < SPMV_SU; u++)
+      if (jj[u] >= 0) load_nf<NF>(x, size_t(jj[u]), t[u]);
+#pragma unroll
+    for (int u = 0; u < SPMV_SU; u++) {
+      const int k = int(threadIdx.x) + u * kBlock;
+      if (jj[u] >= 0)
+#pragma unroll
+        for (int f = 0; f < NF; f++) sx[k * NF + f] = t[u][f];
+    }
+  }
+  for (int k = int(threadIdx.x) + SPMV_SU * kBlock; k < cnt; k += kBlock) {  // longer lists
+    double t[NF];
+    load_nf<NF>(x, size_t(L.ulist[u0 + k]), t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
+  }
+  __syncthreads();
+  static_assert(SB == 2, "slot pairs: even slots into acc2[0], odd into acc2[1]");
+  double d[3] = {0, 0, 0};
+  double acc2[2][NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc2[0][f] = acc2[1][f] = 0;
+  for (int s0 = 0; s0 < len; s0 += SB) {
+    int li[SB];
+    double k[SB][NK];
+    fetch(s0, li, k);
 #pragma unroll
     for (int b = 0; b < SB; b++) {
       double a[NV], xj[NF];
