@@ -238,8 +238,8 @@ def byte_models(info, nf, N_local, T_local, prec):
     spmv = info["nslots"] * (8 * info["nks"] + 4) + 8 * n_loc + 16 * N_local
     # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
     # written, re-read by the backward sweep (gathers counted once), v written
-    vb = 4 * ((info["nvb"] + 3) // 4 * 4 if info["nvb"] > 1 else 1) if info["ilu_f32"] else \
-        8 * info["nvb"]  # bytes per block of the stored factors (float: quads)
+    vb = 4 * info["nvb"] if info["ilu_f32"] else \
+        8 * info["nvb"]  # bytes per block of the stored factors (float: quads + the remainder)
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
     blas = 192 * N_local  # ~24 vector passes per iteration (the contract's figure)
     return {"asm": B_asm, "it_contract": B_it, "spmv_stored": spmv, "ilu_stored": ilu,

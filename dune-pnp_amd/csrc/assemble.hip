@@ -387,6 +387,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
 // LDSG: the fan neighbours' coordinates, dofs and frozen fields come from LDS, where the
 // workgroup first gathered them once per distinct column of its 256 rows (DevLayout::uptr /
 // ulist / lidx, as the LDS-staged SpMV): half the scattered gathers of the direct walk.
+#ifndef ASM_SU
+#define ASM_SU 4  // staged list entries per thread issued together (build-flag A/B knob)
+#endif
 template <int OP>
 __host__ __device__ constexpr int asm_lds_rec() {  // doubles per staged column
   return 2 + OpTraits<OP>::NF + (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) +
@@ -433,7 +436,35 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   if constexpr (AUX1) aq = a.aux1[row];
   if constexpr (LDSG) {
     const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
-    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+    // up to ASM_SU list entries per thread: their list loads, then their gathers, then the LDS
+    // stores (two round trips, not two per entry; ~1,000 distinct columns per block at config 3)
+    constexpr int kSU = ASM_SU;
+    int jj[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; u++) {
+      const int k = int(threadIdx.x) + u * 256;
+      jj[u] = k < cnt ? L.ulist[u0 + k] : -1;
+    }
+    double t[kSU][RW];
+#pragma unroll
+    for (int u = 0; u < kSU; u++)
+      if (jj[u] >= 0) {
+        const double2 p = reinterpret_cast<const double2 *>(L.xy)[jj[u]];
+        t[u][0] = p.x;
+        t[u][1] = p.y;
+        double uu[NF];
+        load_nf<NF>(a.x, size_t(jj[u]), uu);
+#pragma unroll
+        for (int f = 0; f < NF; f++) t[u][2 + f] = uu[f];
+        if constexpr (AUX0) t[u][2 + NF] = a.aux0[jj[u]];
+        if constexpr (AUX1) t[u][3 + NF] = a.aux1[jj[u]];
+      }
+#pragma unroll
+    for (int u = 0; u < kSU; u++)
+      if (jj[u] >= 0)
+#pragma unroll
+        for (int w = 0; w < RW; w++) srec[size_t(int(threadIdx.x) + u * 256) * RW + w] = t[u][w];
+    for (int k = int(threadIdx.x) + kSU * 256; k < cnt; k += blockDim.x) {
       const int j = L.ulist[u0 + k];
       const double2 p = reinterpret_cast<const double2 *>(L.xy)[j];
       double u[NF];

@@ -359,10 +359,46 @@ __global__ __launch_bounds__(kBlock) void k_jacobi(DevLayout L, const double *__
 // stores them in single precision (PNP_ILU_F32; the arithmetic stays fp64).  float slots hold NVP
 // = NV rounded up to 4 values per row, quad-interleaved (one dwordx4 per lane moves 4 values):
 // value q of lane l at (q >> 2) * 4 * kRows + 4 l + (q & 3); NV == 1 is row-contiguous.
+// ILU_F32_PACK (default): NV values exactly, the full quads as above and the last NV % 4 values
+// as one record of that many floats per lane (NV = 7: a dwordx4 and a dwordx3 per lane, 28 B per
+// block instead of 32)
+#ifndef ILU_F32_PACK
+#define ILU_F32_PACK 1
+#endif
 template <int NV>
-__host__ __device__ constexpr int nvp_f() { return NV == 1 ? 1 : ((NV + 3) & ~3); }
+__host__ __device__ constexpr int nvp_f() {
+  return NV == 1 ? 1 : ILU_F32_PACK ? NV : ((NV + 3) & ~3);
+}
 __host__ __device__ constexpr int vinf(int nv, int q, int lane) {
-  return nv == 1 ? lane : (q >> 2) * 4 * kRows + 4 * lane + (q & 3);
+  if (nv == 1) return lane;
+  const int nq = ILU_F32_PACK ? (nv >> 2) : ((nv + 3) >> 2), rem = nv - 4 * nq;
+  return q < 4 * nq ? (q >> 2) * 4 * kRows + 4 * lane + (q & 3)
+                    : 4 * nq * kRows + rem * lane + (q - 4 * nq);
+}
+// the values of a float slot-lane (quad-interleaved as vinf) into B[0 .. NV) as doubles
+template <int NV, int NT, typename T = double>
+__device__ __forceinline__ void load_f32_slot(const float *__restrict__ sb, int lane, T *B) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  constexpr int NQ = ILU_F32_PACK ? (NV >> 2) : ((NV + 3) >> 2), REM = ILU_F32_PACK ? NV - 4 * NQ : 0;
+#pragma unroll
+  for (int k = 0; k < NQ; k++) {
+    const f4v *pp = reinterpret_cast<const f4v *>(sb + k * 4 * kRows) + lane;
+    const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * k + i < NV) B[4 * k + i] = T(t[i]);
+  }
+  const float *pr = sb + NQ * 4 * kRows + REM * lane;
+  if constexpr (REM == 2) {
+    const f2v t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2v *>(pr))
+                     : *reinterpret_cast<const f2v *>(pr);
+    B[4 * NQ] = T(t[0]);
+    B[4 * NQ + 1] = T(t[1]);
+  } else if constexpr (REM != 0) {
+#pragma unroll
+    for (int i = 0; i < REM; i++) B[4 * NQ + i] = T(NT ? __builtin_nontemporal_load(pr + i) : pr[i]);
+  }
 }
 template <int NV, typename VT>
 __host__ __device__ constexpr int slot_vals() {
@@ -379,15 +415,7 @@ __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int l
   } else if constexpr (NV == 1) {
     B[0] = NT ? __builtin_nontemporal_load(sb + lane) : sb[lane];
   } else {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int k = 0; k < nvp_f<NV>() / 4; k++) {
-      const f4v *pp = reinterpret_cast<const f4v *>(sb + k * 4 * kRows) + lane;
-      const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (4 * k + i < NV) B[4 * k + i] = double(t[i]);
-    }
+    load_f32_slot<NV, NT>(sb, lane, B);
   }
 }
 
@@ -964,14 +992,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
       } else if constexpr (NV == 1) {
         ar[b][0] = NT ? __builtin_nontemporal_load(sbp + R.lane) : sbp[R.lane];
       } else {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int k = 0; k < NS / 4; k++) {
-          const f4v *pp = reinterpret_cast<const f4v *>(sbp + k * 4 * kRows) + R.lane;
-          const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
-#pragma unroll
-          for (int i = 0; i < 4; i++) ar[b][4 * k + i] = t[i];
-        }
+        load_f32_slot<NV, NT, float>(sbp, R.lane, ar[b]);
       }
     }
   };
