@@ -241,6 +241,8 @@ def byte_models(info, nf, N_local, T_local, prec):
     vb = 4 * info["nvb"] if info["ilu_f32"] else \
         8 * info["nvb"]  # bytes per block of the stored factors (float: quads + the remainder)
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
+    if info["ilu_f32"] and info["nvb"] == 7:
+        ilu -= 16 * V  # the forward steps read only the 12-B lower tail of each diagonal block
     blas = 192 * N_local  # ~24 vector passes per iteration (the contract's figure)
     return {"asm": B_asm, "it_contract": B_it, "spmv_stored": spmv, "ilu_stored": ilu,
             "blas": blas, "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}

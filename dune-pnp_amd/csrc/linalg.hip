@@ -369,35 +369,54 @@ template <int NV>
 __host__ __device__ constexpr int nvp_f() {
   return NV == 1 ? 1 : ILU_F32_PACK ? NV : ((NV + 3) & ~3);
 }
-__host__ __device__ constexpr int vinf(int nv, int q, int lane) {
+// ILU_F32_LOWTAIL (default, packed NV = 7 only): values 3 and 4 trade places in storage, so that
+// the remainder record holds (1,0), (2,0) and (2,2) of the PNP pattern: the strictly lower entries
+// of a diagonal block, all a forward step needs of it (one dwordx3 instead of 28 B)
+#ifndef ILU_F32_LOWTAIL
+#define ILU_F32_LOWTAIL 1
+#endif
+__host__ __device__ constexpr int fperm(int nv, int q) {
+  return (ILU_F32_PACK && ILU_F32_LOWTAIL && nv == 7 && (q == 3 || q == 4)) ? 7 - q : q;
+}
+__host__ __device__ constexpr int vinf(int nv, int q0, int lane) {
   if (nv == 1) return lane;
+  const int q = fperm(nv, q0);
   const int nq = ILU_F32_PACK ? (nv >> 2) : ((nv + 3) >> 2), rem = nv - 4 * nq;
   return q < 4 * nq ? (q >> 2) * 4 * kRows + 4 * lane + (q & 3)
                     : 4 * nq * kRows + rem * lane + (q - 4 * nq);
 }
 // the values of a float slot-lane (quad-interleaved as vinf) into B[0 .. NV) as doubles
-template <int NV, int NT, typename T = double>
+// LOWER: only what a forward step reads of a diagonal block (the remainder record when it holds
+// all strictly lower entries, see fperm; the other values are zero then)
+template <int NV, int NT, typename T = double, int LOWER = 0>
 __device__ __forceinline__ void load_f32_slot(const float *__restrict__ sb, int lane, T *B) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   typedef float f2v __attribute__((ext_vector_type(2)));
   constexpr int NQ = ILU_F32_PACK ? (NV >> 2) : ((NV + 3) >> 2), REM = ILU_F32_PACK ? NV - 4 * NQ : 0;
+  constexpr bool TAIL = LOWER && fperm(NV, 3) != 3;  // the remainder holds the lower entries
 #pragma unroll
   for (int k = 0; k < NQ; k++) {
+    if (TAIL) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) B[fperm(NV, 4 * k + i)] = T(0);
+      continue;
+    }
     const f4v *pp = reinterpret_cast<const f4v *>(sb + k * 4 * kRows) + lane;
     const f4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (4 * k + i < NV) B[4 * k + i] = T(t[i]);
+      if (4 * k + i < NV) B[fperm(NV, 4 * k + i)] = T(t[i]);
   }
   const float *pr = sb + NQ * 4 * kRows + REM * lane;
   if constexpr (REM == 2) {
     const f2v t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f2v *>(pr))
                      : *reinterpret_cast<const f2v *>(pr);
-    B[4 * NQ] = T(t[0]);
-    B[4 * NQ + 1] = T(t[1]);
+    B[fperm(NV, 4 * NQ)] = T(t[0]);
+    B[fperm(NV, 4 * NQ + 1)] = T(t[1]);
   } else if constexpr (REM != 0) {
 #pragma unroll
-    for (int i = 0; i < REM; i++) B[4 * NQ + i] = T(NT ? __builtin_nontemporal_load(pr + i) : pr[i]);
+    for (int i = 0; i < REM; i++)
+      B[fperm(NV, 4 * NQ + i)] = T(NT ? __builtin_nontemporal_load(pr + i) : pr[i]);
   }
 }
 template <int NV, typename VT>
@@ -405,7 +424,7 @@ __host__ __device__ constexpr int slot_vals() {
   return std::is_same<VT, float>::value ? nvp_f<NV>() : NV;
 }
 
-template <int NV, int NT, typename VT>
+template <int NV, int NT, typename VT, int LOWER = 0>
 __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int lane, double *B) {
   if constexpr (std::is_same<VT, double>::value) {
     if (NT)
@@ -415,7 +434,7 @@ __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int l
   } else if constexpr (NV == 1) {
     B[0] = NT ? __builtin_nontemporal_load(sb + lane) : sb[lane];
   } else {
-    load_f32_slot<NV, NT>(sb, lane, B);
+    load_f32_slot<NV, NT, double, LOWER>(sb, lane, B);
   }
 }
 
@@ -917,7 +936,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   // own data and diagonal block first: they share the neighbour loop's round trips
   double own[NF], Dg[NV];
   load_nf<NF>(FWD ? d : v, size_t(row), own);
-  load_split_vals<NV, 0>(R.dg, R.dlane, Dg);
+  load_split_vals<NV, 0, VT, KIND == kIluFwd>(R.dg, R.dlane, Dg);
   double acc[NF];
   split_row_dot<NF, PAT, LPR, B, NT, VT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
@@ -969,7 +988,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   const int row = R.row;
   double own[NF], Dg[NV];
   load_nf<NF>(FWD ? d : v, size_t(row), own);
-  load_split_vals<NV, 0>(R.dg, R.dlane, Dg);
+  load_split_vals<NV, 0, VT, KIND == kIluFwd>(R.dg, R.dlane, Dg);
   const int chunk = pos / kRows;
   const uint16_t *__restrict__ lix =
       (FWD ? L.lsx_idx + L.lchunk_off[chunk] : L.usx_idx + L.uchunk_off[chunk]) + R.lane;
@@ -1259,7 +1278,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
     }
     if (row < c0_end) {
       double Dg[NV];
-      load_split_vals<NV, 0>(uv + size_t(L.uchunk_off[row / kRows]) * slot_vals<NV, VT>(),
+      load_split_vals<NV, 0, VT, 1>(uv + size_t(L.uchunk_off[row / kRows]) * slot_vals<NV, VT>(),
                              L.upinv ? int(L.upinv[row]) : row % kRows, Dg);
       diag_lower_solve<NF, PAT>(Dg, d);
       store_nf<NF>(yout, size_t(row), d);
