@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   if constexpr (AUX0) ai = a.aux0[row];
   if constexpr (AUX1) aq = a.aux1[row];
   if constexpr (LDSG) {
-    const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
+    const int u0 = L.uptr[blk], cnt = L.uown[blk];  // the fan neighbours (own rows come after)
     // up to ASM_SU list entries per thread: their list loads, then their gathers, then the LDS
     // stores (two round trips, not two per entry; ~1,000 distinct columns per block at config 3)
     constexpr int kSU = ASM_SU;
@@ -739,10 +739,10 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
     else if (!fanr)                                                                \
       hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
-    else if (!a.jac && fanr == 9 && ga && lds_env == 1 && L.uptr &&                 \
-             size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
+    else if (!a.jac && fanr == 9 && ga && lds_env == 1 && L.uown &&                 \
+             size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9, 9, 0, 1>), grid, block,         \
-                         size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
+                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
     else if (!a.jac && fanr == 9 && ga)                                            \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9>), grid, block, 0, s, L, a);  \
     else if (!a.jac)                                                               \
@@ -753,10 +753,10 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
-    else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uptr &&       \
-             size_t(L.umax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
+    else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uown &&       \
+             size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \
-                         size_t(L.umax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
+                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
     else if (ga == 4 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, L, a); \
     else if (ga == 5 && fanr == 9)                                                 \

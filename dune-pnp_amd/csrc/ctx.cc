@@ -122,6 +122,7 @@ struct pnp_ctx {
   DBuf<uint8_t> d_rowcolor;
   DBuf<uint64_t> d_rowmeta;
   DBuf<int> d_uptr, d_ulist;   // LDS-staged SpMV lists (PNP_SPMV_LDS, DevLayout::uptr)
+  DBuf<int> d_uown;            // per block: list entries before its own rows (DevLayout::uown)
   DBuf<int> d_lsx_ptr, d_lsx_list, d_usx_ptr, d_usx_list;  // LDS-staged sweeps (DevLayout lsx_*)
   DBuf<uint16_t> d_lsx_idx, d_usx_idx;
   DBuf<uint8_t> d_lperm, d_uperm, d_lpinv, d_upinv, d_llen, d_ulen, d_ldl;  // split lane order
@@ -2182,9 +2183,13 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     const int nblk = (L.n_owned + 255) / 256;
     std::vector<int> uptr(nblk + 1, 0), ulist;
     std::vector<uint16_t> lidx(size_t(L.nslots), 0);
-    std::vector<int> cols;
-    int umax = 0;
+    std::vector<int> cols, uown(nblk, 0);
+    int umax = 0, unmax = 0;
     bool fits = true;
+    const bool own_last = [] {
+      const char *e = getenv("PNP_LIST_OWN_LAST");
+      return !(e && e[0] == '0');
+    }();
     for (int b = 0; b < nblk && fits; b++) {
       cols.clear();
       const int r1 = std::min(L.n_owned, 256 * b + 256);
@@ -2197,19 +2202,47 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
       if (cols.size() > 65535) fits = false;
       umax = std::max(umax, int(cols.size()));
+      // columns that are only a row's own slot 0 last (PNP_LIST_OWN_LAST, default): the assembly
+      // walk stages only the first uown[b] entries, the columns of slots >= 1 (fan neighbours; a
+      // block's rows are mostly of one colour, so its own rows are rarely among them); the SpMV
+      // stages all
+      std::vector<int> npos(cols.size());
+      int nn = 0;
+      if (own_last) {
+        std::vector<char> nb(cols.size(), 0);
+        for (int i = 256 * b; i < r1; i++) {
+          const int ch = i / pnp::kRows, ln = i % pnp::kRows;
+          for (int sl = 1; sl < L.chunk_len[ch]; sl++) {
+            const int j = L.colidx[size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln];
+            if (j != i) nb[std::lower_bound(cols.begin(), cols.end(), j) - cols.begin()] = 1;
+          }
+        }
+        for (size_t k = 0; k < cols.size(); k++)
+          if (nb[k]) npos[k] = nn++;
+        int no = nn;
+        for (size_t k = 0; k < cols.size(); k++)
+          if (!nb[k]) npos[k] = no++;
+      } else {
+        for (size_t k = 0; k < cols.size(); k++) npos[k] = int(k);
+        nn = int(cols.size());
+      }
+      uown[b] = nn;
+      unmax = std::max(unmax, nn);
       for (int i = 256 * b; i < r1; i++) {
         const int ch = i / pnp::kRows, ln = i % pnp::kRows;
         for (int sl = 0; sl < L.chunk_len[ch]; sl++) {
           const size_t pos = size_t(L.chunk_off[ch]) + 64 * size_t(sl) + ln;
-          lidx[pos] = uint16_t(std::lower_bound(cols.begin(), cols.end(), L.colidx[pos]) - cols.begin());
+          lidx[pos] = uint16_t(npos[std::lower_bound(cols.begin(), cols.end(), L.colidx[pos]) - cols.begin()]);
         }
       }
-      ulist.insert(ulist.end(), cols.begin(), cols.end());
+      std::vector<int> reord(cols.size());
+      for (size_t k = 0; k < cols.size(); k++) reord[npos[k]] = cols[k];
+      ulist.insert(ulist.end(), reord.begin(), reord.end());
       uptr[b + 1] = int(ulist.size());
     }
     if (fits && size_t(umax) * 3 * 8 <= 64 * 1024) {
       if ((rc = up(c->d_uptr, uptr, "uptr")) || (rc = up(c->d_ulist, ulist, "ulist")) ||
-          (rc = up(c->d_lidx, lidx, "lidx"))) {
+          (rc = up(c->d_lidx, lidx, "lidx")) || (rc = up(c->d_uown, uown, "uown"))) {
         g_err = c->err;
         return rc;
       }
@@ -2217,6 +2250,8 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       c->dl.ulist = c->d_ulist.p;
       c->dl.lidx = c->d_lidx.p;
       c->dl.umax = umax;
+      c->dl.uown = c->d_uown.p;
+      c->dl.unmax = unmax;
     }
   }
   c->dl.xy = c->d_xy.p;

@@ -237,6 +237,10 @@ struct DevLayout {
   const int *uptr = nullptr, *ulist = nullptr;
   const uint16_t *lidx = nullptr;
   int umax = 0;
+  // per block the number of list entries that are not its own rows (they come first): the
+  // assembly walk stages only those; unmax = the largest
+  const int *uown = nullptr;
+  int unmax = 0;
   // LDS-staged ILU(0) sweeps (k_ilu0_solve_lds): per (colour, 256-row block of the colour) -- blocks
   // numbered colour by colour -- the distinct neighbour rows of its L (forward) / U (backward) split
   // slots (lsx_list[lsx_ptr[b] ..), usx_*), and per split-storage position (the indexing of lcolidx
