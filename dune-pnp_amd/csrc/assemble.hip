@@ -422,7 +422,10 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   if constexpr (LDSG) {
     const uint16_t *__restrict__ lix = L.lidx + off + lane;
 #pragma unroll
-    for (int k = 1; k < NS; k++) cj[k] = lix[(k < len ? k : 0) * kRows];
+    for (int k = 1; k < NS; k++) {  // past the fan: entry 0 (slot 0's own row is not staged)
+      const int t = lix[(k < len ? k : 0) * kRows];
+      cj[k] = k < len ? t : 0;
+    }
   } else {
     const int *__restrict__ cix = L.colidx + off + lane;
 #pragma unroll
