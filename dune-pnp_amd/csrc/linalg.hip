@@ -185,6 +185,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv(DevLayout L, const double *__re
 #ifndef SPMV_SU
 #define SPMV_SU 4  // staged list entries per thread issued together (build-flag A/B knob)
 #endif
+#ifndef SPMV_OWN_DIRECT
+#define SPMV_OWN_DIRECT 1
+#endif
 template <int NF, int PAT, int MODE, int SB, int NT>
 __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *__restrict__ vals,
                                                      const double *__restrict__ x,
@@ -199,9 +202,19 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
   const bool live = row < L.n_owned;
   const int chunk = row / kRows, lane = row % kRows;
   const int off = live ? L.chunk_off[chunk] : 0, len = live ? L.chunk_len[chunk] : 0;
-  const int u0 = L.uptr[blk], cnt = L.uptr[blk + 1] - u0;
+  // SPMV_OWN_DIRECT (default): the entries past uown[blk] -- columns that are only a row's own
+  // slot 0 (and its padding slots) -- are not staged; a slot whose column is the row itself takes
+  // x[row] from a direct, coalesced load instead (the same value, so bitwise the staged form)
+  const int u0 = L.uptr[blk];
+  const int cnt = (SPMV_OWN_DIRECT && L.uown) ? L.uown[blk] : L.uptr[blk + 1] - u0;
   const uint16_t *__restrict__ lix = L.lidx + off + lane;
   const double *__restrict__ vc = vals + size_t(off) * NK;
+  double xo[NF];
+  int lown = -1;
+  if (SPMV_OWN_DIRECT && L.uown && live) {
+    load_nf<NF>(x, size_t(row), xo);
+    lown = lix[0];
+  }
   // one slot pair's list positions and values (issuing the first pair before the staging barrier
   // was measured: config 5 BiCGSTAB +2.5 %, profiles/r03/ab_spmv_staging.log)
   auto fetch = [&](int s0, int (&li)[SB], double (&k)[SB][NK]) {
@@ -258,8 +271,13 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lds(DevLayout L, const double *
 #pragma unroll
     for (int b = 0; b < SB; b++) {
       double a[NV], xj[NF];
+      const bool me = SPMV_OWN_DIRECT && li[b] == lown;
+      const int lj = me ? 0 : li[b];
 #pragma unroll
-      for (int g = 0; g < NF; g++) xj[g] = sx[li[b] * NF + g];
+      for (int g = 0; g < NF; g++) {
+        const double t = sx[lj * NF + g];
+        xj[g] = me ? xo[g] : t;
+      }
       expand_k<PAT>(k[b], a);
 #pragma unroll
       for (int f = 0; f < NF; f++)
@@ -1610,7 +1628,7 @@ static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double 
                      0, s, L, vals, x, y, w, partials, w2)
   const int b = spmv_batch(), l = spmv_lpr();
   if (spmv_uses_lds(L)) {
-    const size_t lds = size_t(L.umax) * NF * sizeof(double);
+    const size_t lds = size_t(SPMV_OWN_DIRECT && L.uown ? L.unmax : L.umax) * NF * sizeof(double);
     hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
                        w, partials, w2);
     return;
