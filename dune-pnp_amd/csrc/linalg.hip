@@ -1822,10 +1822,12 @@ static bool ilu_lds() {
   return v;
 }
 
-static bool ilu_lds_b8() {
-  static const bool v = [] {
+// PNP_ILU_LDS_B: force the LDS sweeps' slot batch (2, 3, 4 or 8; 0 / unset: by size)
+static int ilu_lds_bsel() {
+  static const int v = [] {
     const char *e = std::getenv("PNP_ILU_LDS_B");
-    return e && e[0] == '8';
+    const int b = e ? atoi(e) : 0;
+    return (b == 2 || b == 3 || b == 4 || b == 8) ? b : 0;
   }();
   return v;
 }
@@ -1845,9 +1847,11 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     auto run = [&](auto vt) -> hipError_t {
       using VT = decltype(vt);
       const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
-      // slot batch: 4 (8-slot batches, one batch for every row seen: config 3 apply 77 -> 89 us,
-      // config 5 245 -> 288 us, profiles/r03/ab_ilu_lds_b.log)
-      constexpr int kB = 4;
+      // slot batch (the sums run over the slots in order whatever the batch, so bitwise alike):
+      // 2 below 1.5 M rows, 3 above -- config 3 apply 69.5 -> 66.8 us with 2, config 5 215 ->
+      // 207 us with 3 (profiles/r03/ab_ilu_lds_batch_r5n.log); 4 before; 8 lost (config 3 77 ->
+      // 89 us, ab_ilu_lds_b.log).  PNP_ILU_LDS_B = 2 / 3 / 4 / 8 forces one
+      const int kBsel = ilu_lds_bsel() ? ilu_lds_bsel() : (L.n_owned > 1500000 ? 3 : 2);
       PNP_PAT_DISPATCH(nf, pat, {
         auto go = [&](auto kind, int c) {
           const int n = cp[c + 1] - cp[c];
@@ -1865,12 +1869,20 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
                                  dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
                                  nullptr, nullptr);
           };
-          if (ilu_lds_b8())  // A/B: 8-slot batches
-            launch(std::integral_constant<int, 1>(), std::integral_constant<int, 8>());
-          else if (sweep_nt())
-            launch(std::integral_constant<int, 1>(), std::integral_constant<int, kB>());
+          auto batch = [&](auto ntc) {
+            if (kBsel == 8)
+              launch(ntc, std::integral_constant<int, 8>());
+            else if (kBsel == 4)
+              launch(ntc, std::integral_constant<int, 4>());
+            else if (kBsel == 3)
+              launch(ntc, std::integral_constant<int, 3>());
+            else
+              launch(ntc, std::integral_constant<int, 2>());
+          };
+          if (sweep_nt())
+            batch(std::integral_constant<int, 1>());
           else
-            launch(std::integral_constant<int, 0>(), std::integral_constant<int, kB>());
+            batch(std::integral_constant<int, 0>());
         };
         for (int c = c_first; c < nc - 1; c++) go(std::integral_constant<int, kIluFwd>(), c);
         go(std::integral_constant<int, kIluLast>(), nc - 1);
