@@ -208,7 +208,29 @@ struct pnp_ctx {
     }
   };
   NatDir nat_f, nat_b;
-  DBuf<double> nat_d, nat_v;
+  DBuf<double> nat_d, nat_v, nat_vf;
+  // the one-launch dataflow sweep (launch_ssor_natural_flow): units, forward units first
+  std::vector<int4> nat_units;
+  DBuf<int4> d_nat_units;
+  int nat_units_f = 0;
+  bool nat_units_ok = false;
+  DBuf<unsigned> nat_abort;  // [0]: set by a sweep whose operand wait timed out (sticky)
+  DBuf<int> csr_diag;        // index of each CSR-view row's diagonal entry
+  // ---- reference-order mode (PNP_OPT_SEQ_ORDER, seq_order.hip) -----------------------------
+  int seq_opt = 0;
+  bool seq_built = false, seq_op_valid = false;
+  DBuf<int> seq_tri, seq_vptr, seq_vinc;
+  DBuf<double> seq_xy;
+  // the operator's data as the reference holds it: constrained rows (external layout), frozen
+  // fields, x_old, implicit-Euler dt / valency (host copies taken by pnp_set_operator)
+  std::vector<uint8_t> seq_mask_h;
+  std::vector<double> seq_phi_h, seq_cp_h, seq_cm_h, seq_xold_h;
+  double seq_dt = 0, seq_z = 0;
+  bool seq_cextra = false;
+  DBuf<unsigned char> seq_mask;
+  DBuf<int> seq_bptr;
+  DBuf<double> seq_bval, seq_phi, seq_cp, seq_cm, seq_xold;
+  DBuf<double> seq_rl, seq_rlo, seq_jl, seq_vec, seq_dotv;
   int nat_pat = -1, nat_nf = 0;
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
   // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
@@ -668,7 +690,9 @@ struct pnp_ctx {
   int csr_structure() {
     const int nv = mesh.nv, mask = pat & 0x1FF;
     if (csr_pat == mask && csr_nf == nf) return PNP_OK;
-    nat_graph_clear();  // its buffers are rebuilt below
+    // the BiCGSTAB block graphs captured with SSOR_NATURAL hold csr_val, nat_d / nat_v and the level
+    // buffers, all rebuilt below: drop every graph (bumps graph_epoch, part of GraphKey)
+    graphs_clear();
     const int n = nf * nv;
     std::vector<int> cnt(n + 1, 0);
     for (int i = 0; i < L.n_owned; i++) {
@@ -727,6 +751,7 @@ struct pnp_ctx {
         if (col[k] == R) diag[R] = k;
     for (int R = 0; R < n; R++)
       if (!empty(R) && diag[R] < 0) return fail(PNP_E_STATE, "natural SSOR: row without diagonal");
+    if ((rc = upv(csr_diag, diag, "csr diagonal"))) return rc;
     auto schedule = [&](bool fwd, NatDir &W) -> int {
       std::vector<int> &lptr = W.lptr;
       std::vector<int> lev(n, -1), push(n, 0);
@@ -762,7 +787,10 @@ struct pnp_ctx {
         for (int t = lptr[l]; t < lptr[l + 1]; t++) w = std::max(w, cnt[rl[t] + 1] - cnt[rl[t]]);
         W.eoff[l + 1] = W.eoff[l] + (long long)w * (lptr[l + 1] - lptr[l]);
       }
-      std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), 0), eidx(ecol.size(), -1);
+      // operand codes (NatSweep): the forward sweep reads the new value of an earlier row (C < R)
+      // and zero for the row itself and later rows; the backward sweep reads the forward value of
+      // rows C <= R and the new backward value of later rows; rows of other ranks read zero
+      std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), -1), eidx(ecol.size(), -1);
       for (int l = 0; l < nlev; l++) {
         const int nl = lptr[l + 1] - lptr[l];
         for (int t = lptr[l]; t < lptr[l + 1]; t++) {
@@ -770,19 +798,42 @@ struct pnp_ctx {
           info[t] = make_int4(R, len, diag[R], 0);
           for (int k = 0; k < len; k++) {
             const size_t q = size_t(W.eoff[l]) + size_t(k) * nl + (t - lptr[l]);
-            ecol[q] = col[cnt[R] + k];
+            const int C = col[cnt[R] + k];
+            ecol[q] = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
             eidx[q] = cnt[R] + k;
           }
         }
       }
+      // dataflow units for the one-launch sweep: up to kNatUnit consecutive rows of one level,
+      // {first sweep position, rows | width << 8, the level's row count, ELL index of the unit's
+      // first row}; forward units in level order, then backward units in level order
+      for (int l = 0; l < nlev && nat_units_ok; l++) {
+        const int nl = lptr[l + 1] - lptr[l];
+        const long long w = nl > 0 ? (W.eoff[l + 1] - W.eoff[l]) / nl : 0;
+        for (int t0 = lptr[l]; t0 < lptr[l + 1]; t0 += pnp::kNatUnit) {
+          const long long e0 = W.eoff[l] + (t0 - lptr[l]);
+          if (w > 255 || W.eoff[l + 1] > INT32_MAX) {
+            nat_units_ok = false;
+            break;
+          }
+          const int rows = std::min(pnp::kNatUnit, lptr[l + 1] - t0);
+          nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), nl, int(e0)));
+        }
+      }
+      if (fwd) nat_units_f = int(nat_units.size());
       int rc2;
       if ((rc2 = upv(W.info, info, "natural SSOR rows")) ||
           (rc2 = upv(W.ecol, ecol, "natural SSOR columns")))
         return rc2;
       return upv(W.eidx, eidx, "natural SSOR entries");
     };
+    nat_units.clear();
+    nat_units_ok = true;
     if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
-    if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess)
+    if (nat_units_ok && (rc = upv(d_nat_units, nat_units, "natural SSOR units"))) return rc;
+    if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess ||
+        (e = nat_vf.alloc(std::max(1, n))) != hipSuccess || (e = nat_abort.alloc(4)) != hipSuccess ||
+        (e = hipMemset(nat_abort.p, 0, 16)) != hipSuccess)
       return hipfail(e, "natural SSOR vectors");
     csr_nnz = nnz;
     csr_pat = mask;
@@ -806,20 +857,55 @@ struct pnp_ctx {
   // v = SSOR_natural^{-1} d on internal-layout owned rows (ssor_natural.hip); csr_values() first
   hipError_t ssor_natural(const double *d, double *vout) {
     const int nv = mesh.nv;
-    hipError_t e = hipMemsetAsync(nat_v.p, 0, sizeof(double) * nat_v.n, stream);
-    if (e == hipSuccess)
-      e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
-    if (e == hipSuccess) e = ssor_natural_levels();
+    hipError_t e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
+    if (e == hipSuccess) e = use_nat_flow() ? ssor_natural_flow() : ssor_natural_levels();
     if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
     return e;
+  }
+  // one launch for both sweeps (ssor_natural.hip, launch_ssor_natural_flow): one rank only (in-process
+  // ranks share the device, and the dataflow needs every workgroup of its grid resident);
+  // PNP_NAT_FLOW=0 keeps the level launches
+  bool use_nat_flow() const {
+    static const bool env_on = [] {
+      const char *ev = std::getenv("PNP_NAT_FLOW");
+      return !(ev && std::atoi(ev) == 0);
+    }();
+    return env_on && !dist && nat_units_ok;
+  }
+  hipError_t ssor_natural_flow() {
+    pnp::NatFlow F;
+    F.units = d_nat_units.p;
+    F.nunits = int(nat_units.size());
+    F.nunits_f = nat_units_f;
+    F.fwd = nat_f.view();
+    F.bwd = nat_b.view();
+    F.abort_word = nat_abort.p;
+    return pnp::launch_ssor_natural_flow(F, nf * mesh.nv, csr_val.p, nat_d.p, nat_vf.p, nat_v.p,
+                                         stream);
+  }
+  // a dataflow sweep that timed out (never expected: every unit waits only on earlier units, all
+  // resident) leaves NaN results and a sticky word; the solve reports it as an error
+  int nat_check() {
+    if (!use_nat_flow() || !nat_abort.p) return PNP_OK;
+    unsigned w = 0;
+    hipError_t e = hipMemcpyAsync(&w, nat_abort.p, 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "natural SSOR status");
+    if (w) {
+      hipMemsetAsync(nat_abort.p, 0, 16, stream);
+      return fail(PNP_E_HIP, "natural SSOR: dataflow sweep timed out waiting for an operand");
+    }
+    return PNP_OK;
   }
   // the level launches: one graph replay (captured on first use; PNP_NAT_GRAPH=0: eager), or eager
   // when the stream is itself being captured (a BiCGSTAB block graph then holds them), with more
   // than one rank, or after a failed capture
   hipError_t ssor_natural_levels() {
     auto issue = [&] {
-      return pnp::launch_ssor_natural(nat_f.view(), nat_b.view(), csr_val.p, nat_d.p, nat_v.p,
-                                      stream);
+      hipError_t e0 = hipMemsetAsync(nat_v.p, 0, sizeof(double) * nat_v.n, stream);
+      return e0 != hipSuccess ? e0
+                              : pnp::launch_ssor_natural(nat_f.view(), nat_b.view(), csr_val.p,
+                                                         nat_d.p, nat_v.p, stream);
     };
     static const bool env_on = [] {
       const char *ev = std::getenv("PNP_NAT_GRAPH");
@@ -1545,6 +1631,7 @@ struct pnp_ctx {
     e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "bicgstab result");
+    if (prec == PNP_PREC_SSOR_NATURAL && (rc = nat_check())) return rc;
     double it = std::min(double(maxit), hS->it_half);
     res.converged = hS->done == 1 ? 1 : 0;
     res.breakdown = hS->breakdown;
@@ -1609,6 +1696,7 @@ struct pnp_ctx {
     e = hipMemcpyAsync(hS, S.p, sizeof(pnp::Scalars), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "cg result");
+    if (o.prec == PNP_PREC_SSOR_NATURAL && (rc = nat_check())) return rc;
     res.converged = hS->done == 1 ? 1 : 0;
     res.breakdown = 0;
     res.iterations = hS->iter;
@@ -1618,6 +1706,325 @@ struct pnp_ctx {
     res.reduction = hS->norm0 > 0 ? hS->norm / hS->norm0 : 0.0;
     res.elapsed = now_s() - t_start;
     return PNP_OK;
+  }
+
+  // ---- reference-order mode (PNP_OPT_SEQ_ORDER) ------------------------------------------------
+  // The reference's single-rank arithmetic in its order (seq_order.hip): element-order assembly
+  // into the CSR view, ISTL's sequential mv / dot / updates, the scalar recurrences here in double.
+  // External-layout vectors throughout.  P1, one rank.
+  bool seq_on() const { return seq_opt && degree == 1 && !dist; }
+  int nseq() const { return nf * mesh.nv; }
+  enum { SQ_X = 0, SQ_R, SQ_Z, SQ_PREVU, SQ_P, SQ_V, SQ_T, SQ_Y, SQ_RT, SQ_B, SQ_N };
+  double *sq(int k) { return seq_vec.p + size_t(k) * size_t(3 * mesh.nv); }
+
+  int seq_build() {
+    if (seq_built) return PNP_OK;
+    const int nv = mesh.nv, nt = mesh.nt;
+    std::vector<int> vptr(nv + 1, 0), vinc(size_t(3) * nt);
+    for (int e = 0; e < nt; e++)
+      for (int a = 0; a < 3; a++) vptr[mesh.tri[3 * e + a] + 1]++;
+    for (int v = 0; v < nv; v++) vptr[v + 1] += vptr[v];
+    std::vector<int> fill(vptr.begin(), vptr.end() - 1);
+    for (int e = 0; e < nt; e++)  // ascending element index per vertex
+      for (int a = 0; a < 3; a++) vinc[fill[mesh.tri[3 * e + a]]++] = e << 2 | a;
+    int rc;
+    if ((rc = upv(seq_tri, mesh.tri, "seq tri")) || (rc = upv(seq_xy, mesh.xy, "seq xy")) ||
+        (rc = upv(seq_vptr, vptr, "seq vptr")) || (rc = upv(seq_vinc, vinc, "seq vinc")))
+      return rc;
+    hipError_t e;
+    if ((e = seq_vec.alloc(size_t(SQ_N) * 3 * nv)) != hipSuccess ||
+        (e = seq_dotv.alloc(2)) != hipSuccess || (e = seq_rl.alloc(size_t(9) * nt)) != hipSuccess ||
+        (e = seq_rlo.alloc(size_t(9) * nt)) != hipSuccess ||
+        (e = seq_jl.alloc(size_t(81) * nt)) != hipSuccess)
+      return hipfail(e, "seq buffers");
+    seq_built = true;
+    return PNP_OK;
+  }
+
+  // per operator: constrained rows, alpha_boundary's terms per row in the order the reference adds
+  // them (boundary intersections in segment order, 2-point Gauss, fields in order; the oracle's
+  // boundary_flux statements: r += scale * (j * psi * factor)), frozen fields
+  int seq_prepare() {
+    int rc;
+    if ((rc = seq_build())) return rc;
+    if (seq_op_valid) return PNP_OK;
+    if (seq_cextra) return fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER: pnp_op_args.c_extra is not supported");
+    const int nv = mesh.nv, n = nseq();
+    std::vector<std::vector<double>> terms(n);
+    const bool bnd = kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_PB ||
+                     kind == PNP_OP_POISSON;
+    if (bnd) {
+      const double PI = params.pi;
+      const double scale = kind == PNP_OP_PNP_IMPLICIT_EULER ? seq_dt : 1.0;
+      const double gt[2] = {0.5 - 0.5 / std::sqrt(3.0), 0.5 + 0.5 / std::sqrt(3.0)};
+      for (int b = 0; b < mesh.nb; b++) {
+        const int v0 = mesh.bseg[2 * b], v1 = mesh.bseg[2 * b + 1];
+        const pnp::Surface &S = params.surf[mesh.bgroup[b]];
+        const double dx = mesh.xy[2 * v1] - mesh.xy[2 * v0],
+                     dy = mesh.xy[2 * v1 + 1] - mesh.xy[2 * v0 + 1];
+        const double len = std::sqrt(dx * dx + dy * dy);
+        for (int q = 0; q < 2; q++) {
+          double factor = 0.5 * len;
+          const double y = mesh.xy[2 * v0 + 1] + gt[q] * dy;
+          if (params.cylindrical) factor *= y * 2 * PI;
+          const double psi[2] = {1.0 - gt[q], gt[q]};
+          for (int f = 0; f < nf; f++) {
+            if (S.btype(f) == 0) continue;  // isDirichlet
+            const double j = S.flux(f);
+            terms[size_t(f) * nv + v0].push_back(scale * (j * psi[0] * factor));
+            terms[size_t(f) * nv + v1].push_back(scale * (j * psi[1] * factor));
+          }
+        }
+      }
+    }
+    std::vector<int> bptr(n + 1, 0);
+    std::vector<double> bval;
+    for (int R = 0; R < n; R++) {
+      bptr[R + 1] = bptr[R] + int(terms[R].size());
+      bval.insert(bval.end(), terms[R].begin(), terms[R].end());
+    }
+    if ((rc = upv(seq_bptr, bptr, "seq boundary")) || (rc = upv(seq_bval, bval, "seq boundary")))
+      return rc;
+    std::vector<unsigned char> m(seq_mask_h.begin(), seq_mask_h.end());
+    if ((rc = upv(seq_mask, m, "seq mask"))) return rc;
+    if ((rc = upv(seq_phi, seq_phi_h, "seq phi")) || (rc = upv(seq_cp, seq_cp_h, "seq cp")) ||
+        (rc = upv(seq_cm, seq_cm_h, "seq cm")) || (rc = upv(seq_xold, seq_xold_h, "seq x_old")))
+      return rc;
+    seq_op_valid = true;
+    return PNP_OK;
+  }
+  pnp::SeqMesh seq_mesh() const {
+    pnp::SeqMesh M;
+    M.nv = mesh.nv;
+    M.nt = mesh.nt;
+    M.tri = seq_tri.p;
+    M.vptr = seq_vptr.p;
+    M.vinc = seq_vinc.p;
+    M.xy = seq_xy.p;
+    return M;
+  }
+  pnp::SeqOp seq_op() const {
+    pnp::SeqOp P;
+    P.kind = kind;
+    P.nf = nf;
+    P.cyl = params.cylindrical;
+    P.pi = params.pi;
+    P.l_b = params.l_b;
+    P.c0 = params.c0;
+    P.tau = params.tau;
+    P.dt = seq_dt;
+    P.z = seq_z;
+    P.phi = seq_phi_h.empty() ? nullptr : seq_phi.p;
+    P.cp = seq_cp_h.empty() ? nullptr : seq_cp.p;
+    P.cm = seq_cm_h.empty() ? nullptr : seq_cm.p;
+    P.x_old = seq_xold_h.empty() ? nullptr : seq_xold.p;
+    return P;
+  }
+  // r = R(x), both external layout on the device (GridOperator::residual + constraints)
+  int seq_residual(const double *x, double *r) {
+    int rc;
+    if ((rc = seq_prepare())) return rc;
+    const bool old = kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_DIFF_IMPLICIT_EULER;
+    hipError_t e = pnp::launch_seq_element(seq_mesh(), seq_op(), x, 0, seq_rl.p, seq_rlo.p,
+                                           seq_jl.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_seq_residual_gather(seq_mesh(), nf, old ? 1 : 0, seq_rl.p, seq_rlo.p,
+                                          seq_bptr.p, seq_bval.p, seq_mask.p, r, stream);
+    return e == hipSuccess ? PNP_OK : hipfail(e, "seq residual");
+  }
+  // the CSR view = J(x) (GridOperator::jacobian + constrained rows to identity); fd: PDELab's
+  // NumericalJacobianVolume
+  int seq_jacobian(const double *x, bool fd) {
+    int rc;
+    if ((rc = seq_prepare()) || (rc = csr_structure())) return rc;
+    hipError_t e = pnp::launch_seq_element(seq_mesh(), seq_op(), x, fd ? 2 : 1, seq_rl.p,
+                                           seq_rlo.p, seq_jl.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_seq_jacobian_gather(seq_mesh(), nf, seq_jl.p, csr_rowptr.p, csr_col.p,
+                                          seq_mask.p, csr_val.p, stream);
+    if (e != hipSuccess) return hipfail(e, "seq jacobian");
+    assembled = true;
+    csr_vals_valid = true;  // the CSR view holds this Jacobian; the k-form matrix does not
+    lu_valid = false;
+    split_of = 0;
+    amg_valid = false;
+    return PNP_OK;
+  }
+  double seq_dot(const double *a, const double *b, int &rc) {
+    rc = PNP_OK;
+    double h = 0;
+    hipError_t e = pnp::launch_seq_dot(nseq(), a, b, seq_dotv.p, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, seq_dotv.p, 8, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) rc = hipfail(e, "seq dot");
+    return h;
+  }
+  // v = M^{-1} d with v zero on entry (ISTL's preconditioners from y = 0)
+  int seq_prec(int prec, const double *d, double *v) {
+    const int n = nseq();
+    hipError_t e;
+    if (prec == PNP_PREC_NONE || prec == PNP_PREC_JACOBI) {
+      e = pnp::launch_seq_prec_diag(n, prec == PNP_PREC_JACOBI, d, csr_diag.p, csr_val.p, v, stream);
+    } else {  // SSOR_NATURAL: the natural-order sweep on the CSR view
+      e = hipMemcpyAsync(nat_d.p, d, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+      if (e == hipSuccess) e = use_nat_flow() ? ssor_natural_flow() : ssor_natural_levels();
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(v, nat_v.p, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+    }
+    return e == hipSuccess ? PNP_OK : hipfail(e, "seq preconditioner");
+  }
+  // ISTL BiCGSTABSolver::apply in the oracle's statements (oracle/pnp_oracle.c orc_bicgstab):
+  // x (zero start) and b (overwritten by the residual), external layout on the device
+  int seq_bicgstab(int prec, double reduction, int maxit, double *x, double *b,
+                   pnp_solve_result &res) {
+    const double EPSILON = 1e-80;
+    const int n = nseq();
+    double *r = b, *p = sq(SQ_P), *v = sq(SQ_V), *t = sq(SQ_T), *y = sq(SQ_Y), *rt = sq(SQ_RT);
+    int rc = PNP_OK;
+    hipError_t e = hipSuccess;
+    auto ck = [&](hipError_t ee) {
+      if (e == hipSuccess) e = ee;
+    };
+    for (double *q : {p, v, t, y}) ck(hipMemsetAsync(q, 0, sizeof(double) * n, stream));
+    std::memset(&res, 0, sizeof res);
+    ck(pnp::launch_seq_spmv(n, csr_rowptr.p, csr_col.p, csr_val.p, x, t, stream));  // r = b - A x
+    ck(pnp::launch_seq_aymx(n, 1.0, r, t, stream));
+    ck(hipMemcpyAsync(rt, r, sizeof(double) * n, hipMemcpyDeviceToDevice, stream));
+    if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+    double norm = std::sqrt(seq_dot(r, r, rc)), norm_0 = norm;
+    if (rc) return rc;
+    double rho = 1, alpha = 1, omega = 1, rho_new = 0, beta, h;
+    res.defect0 = norm_0;
+    double it = 0;
+    if (norm < reduction * norm_0 || norm < 1e-30) {
+      res.converged = 1;
+      res.defect = norm;
+      return PNP_OK;
+    }
+    for (it = 0.5; it < maxit; it += .5) {
+      rho_new = seq_dot(rt, r, rc);
+      if (rc) return rc;
+      if (std::fabs(rho) <= EPSILON) { res.breakdown = 1; break; }
+      if (std::fabs(omega) <= EPSILON) { res.breakdown = 2; break; }
+      if (it < 1) {
+        ck(hipMemcpyAsync(p, r, sizeof(double) * n, hipMemcpyDeviceToDevice, stream));
+      } else {
+        beta = (rho_new / rho) * (alpha / omega);
+        ck(pnp::launch_seq_bicg_p(n, beta, omega, p, v, r, stream));
+      }
+      ck(hipMemsetAsync(y, 0, sizeof(double) * n, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      if ((rc = seq_prec(prec, p, y))) return rc;
+      ck(pnp::launch_seq_spmv(n, csr_rowptr.p, csr_col.p, csr_val.p, y, v, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      h = seq_dot(rt, v, rc);
+      if (rc) return rc;
+      if (std::fabs(h) < EPSILON) { res.breakdown = 3; break; }
+      alpha = rho_new / h;
+      ck(pnp::launch_seq_axpy2(n, alpha, x, y, r, v, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      norm = std::sqrt(seq_dot(r, r, rc));
+      if (rc) return rc;
+      if (norm < reduction * norm_0) { res.converged = 1; break; }
+      it += .5;
+      ck(hipMemsetAsync(y, 0, sizeof(double) * n, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      if ((rc = seq_prec(prec, r, y))) return rc;
+      ck(pnp::launch_seq_spmv(n, csr_rowptr.p, csr_col.p, csr_val.p, y, t, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      const double tr = seq_dot(t, r, rc);
+      if (rc) return rc;
+      const double tt = seq_dot(t, t, rc);
+      if (rc) return rc;
+      omega = tr / tt;
+      ck(pnp::launch_seq_axpy2(n, omega, x, y, r, t, stream));
+      if (e != hipSuccess) return hipfail(e, "seq bicgstab");
+      rho = rho_new;
+      norm = std::sqrt(seq_dot(r, r, rc));
+      if (rc) return rc;
+      if (norm < reduction * norm_0 || norm < 1e-30) { res.converged = 1; break; }
+    }
+    if (it > maxit) it = maxit;
+    res.it_half = it;
+    res.iterations = int(std::ceil(it));
+    res.defect = norm;
+    res.reduction = norm / norm_0;
+    return PNP_OK;
+  }
+  // ISTL CGSolver::apply (orc_cg's statements)
+  int seq_cg(int prec, double reduction, int maxit, double *x, double *b, pnp_solve_result &res) {
+    const int n = nseq();
+    double *r = b, *p = sq(SQ_P), *q = sq(SQ_V);
+    int rc = PNP_OK;
+    hipError_t e = hipSuccess;
+    auto ck = [&](hipError_t ee) {
+      if (e == hipSuccess) e = ee;
+    };
+    ck(hipMemsetAsync(p, 0, sizeof(double) * n, stream));
+    ck(hipMemsetAsync(q, 0, sizeof(double) * n, stream));
+    std::memset(&res, 0, sizeof res);
+    ck(pnp::launch_seq_spmv(n, csr_rowptr.p, csr_col.p, csr_val.p, x, q, stream));
+    ck(pnp::launch_seq_aymx(n, 1.0, r, q, stream));
+    if (e != hipSuccess) return hipfail(e, "seq cg");
+    const double def0 = std::sqrt(seq_dot(r, r, rc));
+    if (rc) return rc;
+    double def = def0;
+    res.defect0 = def0;
+    int it = 0;
+    if (def0 < 1e-30) {
+      res.converged = 1;
+    } else {
+      if ((rc = seq_prec(prec, r, p))) return rc;
+      double rho = seq_dot(p, r, rc);
+      if (rc) return rc;
+      for (it = 1; it <= maxit; it++) {
+        ck(pnp::launch_seq_spmv(n, csr_rowptr.p, csr_col.p, csr_val.p, p, q, stream));
+        if (e != hipSuccess) return hipfail(e, "seq cg");
+        const double pq = seq_dot(p, q, rc);
+        if (rc) return rc;
+        const double lambda = rho / pq;
+        ck(pnp::launch_seq_axpy(n, lambda, x, p, stream));
+        ck(pnp::launch_seq_aymx(n, lambda, r, q, stream));
+        if (e != hipSuccess) return hipfail(e, "seq cg");
+        def = std::sqrt(seq_dot(r, r, rc));
+        if (rc) return rc;
+        if (def < reduction * def0 || def < 1e-30) {
+          res.converged = 1;
+          break;
+        }
+        ck(hipMemsetAsync(q, 0, sizeof(double) * n, stream));
+        if (e != hipSuccess) return hipfail(e, "seq cg");
+        if ((rc = seq_prec(prec, r, q))) return rc;
+        const double rho_new = seq_dot(q, r, rc);
+        if (rc) return rc;
+        const double beta = rho_new / rho;
+        ck(pnp::launch_seq_cg_p(n, beta, p, q, stream));
+        if (e != hipSuccess) return hipfail(e, "seq cg");
+        rho = rho_new;
+      }
+      if (it > maxit) it = maxit;
+    }
+    res.it_half = it;
+    res.iterations = it;
+    res.defect = def;
+    res.reduction = def0 > 0 ? def / def0 : 0.0;
+    return PNP_OK;
+  }
+  int seq_krylov(const pnp_solve_opts &o, double *x, double *b, pnp_solve_result &res) {
+    if (!assembled || !csr_vals_valid) return fail(PNP_E_STATE, "no Jacobian assembled");
+    if (o.prec != PNP_PREC_NONE && o.prec != PNP_PREC_JACOBI && o.prec != PNP_PREC_SSOR_NATURAL)
+      return fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER: preconditioner must be NONE, JACOBI or SSOR_NATURAL");
+    double t0 = now_s();
+    int rc;
+    if (o.method == PNP_METHOD_CG)
+      rc = seq_cg(o.prec, o.reduction, o.maxit, x, b, res);
+    else if (o.method == PNP_METHOD_BICGSTAB)
+      rc = seq_bicgstab(o.prec, o.reduction, o.maxit, x, b, res);
+    else
+      return fail(PNP_E_ARG, "unknown solver method");
+    if (!rc && o.prec == PNP_PREC_SSOR_NATURAL) rc = nat_check();
+    res.elapsed = now_s() - t0;
+    return rc;
   }
 
   // the linear solver selected by o.method
@@ -2410,8 +2817,9 @@ extern "C" int pnp_nfields(pnp_ctx *c) { return c ? c->nf : PNP_E_ARG; }
 
 extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   if (!c || !a) return PNP_E_ARG;
-  // no graphs_clear(): the operator's pattern and mask pointer are in the graph key, and nothing
-  // else a BiCGSTAB launch takes changes with the operator
+  // no graphs_clear() here: the operator's pattern and mask pointer are in the graph key; a change
+  // of the CSR view's pattern (SSOR_NATURAL, pnp_jacobian_csr_device) clears the graphs in
+  // csr_structure(), which rebuilds the buffers they captured
   if (a->kind < PNP_OP_PNP || a->kind > PNP_OP_POISSON)
     return c->fail(PNP_E_ARG, "unknown operator kind");
   hipSetDevice(c->device);
@@ -2473,6 +2881,23 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
       if (a->c_extra) lload[size_t(i) * nf + f] += a->c_extra[size_t(f) * m.nv + L.l2g[i]];
     }
   CK(hipMemcpy(c->dmask.p, lmask.data(), lmask.size(), hipMemcpyHostToDevice), "dmask");
+  // the reference-order mode's copies (external layout, global vertex order)
+  c->seq_op_valid = false;
+  c->seq_dt = a->dt;
+  c->seq_z = a->z;
+  c->seq_cextra = a->c_extra != nullptr;
+  c->seq_mask_h.assign(size_t(nf) * m.nv, 0);
+  if (c->degree == 1)
+    for (int g = 0; g < m.nv; g++)
+      for (int f = 0; f < nf; f++) c->seq_mask_h[size_t(f) * m.nv + g] = mask[size_t(g) * nf + f];
+  auto hcopy = [&](const double *h, size_t cnt, std::vector<double> &out) {
+    if (h) out.assign(h, h + cnt); else out.clear();
+  };
+  const bool dk = kind == PNP_OP_DIFF || kind == PNP_OP_DIFF_IMPLICIT_EULER;
+  hcopy(dk ? a->phi : nullptr, m.nv, c->seq_phi_h);
+  hcopy(kind == PNP_OP_POISSON ? a->cp : nullptr, m.nv, c->seq_cp_h);
+  hcopy(kind == PNP_OP_POISSON ? a->cm : nullptr, m.nv, c->seq_cm_h);
+  hcopy(ie ? a->x_old : nullptr, size_t(nf) * m.nv, c->seq_xold_h);
   c->dl.dmask = c->dmask.p;
   c->hmask = lmask;
   CK(hipMemcpy(c->cvec.p, lload.data(), sizeof(double) * lload.size(), hipMemcpyHostToDevice),
@@ -2518,10 +2943,37 @@ extern "C" int pnp_set_operator(pnp_ctx *c, const pnp_op_args *a) {
   return PNP_OK;
 }
 
+// reference-order mode: x / r external layout, host or device
+static int seq_residual_abi(pnp_ctx *c, const double *x, double *r, bool dev) {
+  int rc;
+  if ((rc = c->seq_build())) return rc;
+  const size_t n = c->nseq();
+  double *sx = c->sq(pnp_ctx::SQ_X), *sr = c->sq(pnp_ctx::SQ_R);
+  CK(hipMemcpyAsync(sx, x, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream),
+     "seq upload");
+  if ((rc = c->seq_residual(sx, sr))) return rc;
+  CK(hipMemcpyAsync(r, sr, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream),
+     "seq download");
+  CK(hipStreamSynchronize(c->stream), "seq residual");
+  return PNP_OK;
+}
+static int seq_jacobian_abi(pnp_ctx *c, const double *x, bool dev, bool fd) {
+  int rc;
+  if ((rc = c->seq_build())) return rc;
+  double *sx = c->sq(pnp_ctx::SQ_X);
+  CK(hipMemcpyAsync(sx, x, 8 * size_t(c->nseq()),
+                    dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream),
+     "seq upload");
+  if ((rc = c->seq_jacobian(sx, fd))) return rc;
+  CK(hipStreamSynchronize(c->stream), "seq jacobian");
+  return PNP_OK;
+}
+
 extern "C" int pnp_residual(pnp_ctx *c, const double *x, double *r) {
   if (!c || !x || !r) return PNP_E_ARG;
   if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
   hipSetDevice(c->device);
+  if (c->seq_on()) return seq_residual_abi(c, x, r, false);
   int rc;
   if ((rc = c->upload_ext(x, c->nf, c->x.p, true))) return rc;
   if ((rc = c->assemble(c->x.p, 0))) return rc;
@@ -2532,6 +2984,7 @@ extern "C" int pnp_jacobian(pnp_ctx *c, const double *x) {
   if (!c || !x) return PNP_E_ARG;
   if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
   hipSetDevice(c->device);
+  if (c->seq_on()) return seq_jacobian_abi(c, x, false, c->fd_opt != 0);
   int rc;
   if ((rc = c->upload_ext(x, c->nf, c->x.p, true))) return rc;
   if ((rc = c->assemble(c->x.p, 1))) return rc;
@@ -2543,6 +2996,15 @@ extern "C" int pnp_jacobian_export(pnp_ctx *c, int64_t *nnz, int32_t *rowptr, in
                                    double *val) {
   if (!c || !nnz) return PNP_E_ARG;
   if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
+  if (c->seq_on()) {  // the reference-order Jacobian lives in the CSR view
+    *nnz = c->csr_nnz;
+    if (!rowptr || !col || !val) return PNP_OK;
+    const size_t n = c->nseq();
+    CK(hipMemcpy(rowptr, c->csr_rowptr.p, 4 * (n + 1), hipMemcpyDeviceToHost), "export");
+    CK(hipMemcpy(col, c->csr_col.p, 4 * size_t(c->csr_nnz), hipMemcpyDeviceToHost), "export");
+    CK(hipMemcpy(val, c->csr_val.p, 8 * size_t(c->csr_nnz), hipMemcpyDeviceToHost), "export");
+    return PNP_OK;
+  }
   const pnp::LocalLayout &L = c->L;
   int nf = c->nf, NV = c->nvb, nv = c->mesh.nv;
   long long total = 0;
@@ -2615,6 +3077,7 @@ extern "C" int pnp_residual_ex(pnp_ctx *c, const double *x, double *r, int32_t f
   if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS))) return rc;
   hipSetDevice(c->device);
   const bool dev = flags & PNP_DEVICE_PTRS;
+  if (c->seq_on()) return seq_residual_abi(c, x, r, dev);
   if ((rc = c->upload_ext(x, c->nf, c->x.p, true, dev))) return rc;
   if ((rc = c->assemble(c->x.p, 0))) return rc;
   return c->download_ext(c->r.p, c->nf, r, dev);
@@ -2626,6 +3089,8 @@ extern "C" int pnp_jacobian_ex(pnp_ctx *c, const double *x, int32_t flags) {
   int rc;
   if ((rc = check_flags(c, flags, PNP_DEVICE_PTRS | PNP_JAC_FD))) return rc;
   hipSetDevice(c->device);
+  if (c->seq_on())
+    return seq_jacobian_abi(c, x, flags & PNP_DEVICE_PTRS, c->fd_opt || (flags & PNP_JAC_FD));
   if ((rc = c->upload_ext(x, c->nf, c->x.p, true, flags & PNP_DEVICE_PTRS))) return rc;
   const int keep = c->fd_opt;
   if (flags & PNP_JAC_FD) c->fd_opt = 1;
@@ -2649,6 +3114,18 @@ extern "C" int pnp_jacobian_apply(pnp_ctx *c, const double *x, const double *z, 
   } else if (!c->assembled) {
     return c->fail(PNP_E_STATE, "no Jacobian assembled (pass x)");
   }
+  if (c->seq_on()) {  // y = A z in BCRSMatrix::mv's order on the CSR view
+    const size_t n = c->nseq();
+    double *sz = c->sq(pnp_ctx::SQ_Z), *sy = c->sq(pnp_ctx::SQ_Y);
+    CK(hipMemcpyAsync(sz, z, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream),
+       "seq upload");
+    CK(pnp::launch_seq_spmv(int(n), c->csr_rowptr.p, c->csr_col.p, c->csr_val.p, sz, sy, c->stream),
+       "seq apply");
+    CK(hipMemcpyAsync(y, sy, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream),
+       "seq download");
+    CK(hipStreamSynchronize(c->stream), "seq apply");
+    return PNP_OK;
+  }
   // z with ghosts (the halo of a global vector is local: every rank holds it), y = A z
   if ((rc = c->upload_ext(z, c->nf, c->y.p, true, dev))) return rc;
   int nsp = 0;
@@ -2656,6 +3133,22 @@ extern "C" int pnp_jacobian_apply(pnp_ctx *c, const double *x, const double *z, 
                       &nsp, c->stream),
      "jacobian apply");
   return c->download_ext(c->t.p, c->nf, y, dev);
+}
+
+static int seq_solve_abi(pnp_ctx *c, const double *rhs, double *z, const pnp_solve_opts &o,
+                         pnp_solve_result &res, bool dev) {
+  int rc;
+  if ((rc = c->seq_build())) return rc;
+  const size_t n = c->nseq();
+  double *sb = c->sq(pnp_ctx::SQ_B), *sz = c->sq(pnp_ctx::SQ_Z);
+  CK(hipMemcpyAsync(sb, rhs, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream),
+     "seq upload");
+  CK(hipMemsetAsync(sz, 0, 8 * n, c->stream), "seq upload");
+  if ((rc = c->seq_krylov(o, sz, sb, res))) return rc;
+  CK(hipMemcpyAsync(z, sz, 8 * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream),
+     "seq download");
+  CK(hipStreamSynchronize(c->stream), "seq solve");
+  return res.breakdown ? PNP_E_BREAKDOWN : PNP_OK;
 }
 
 extern "C" int pnp_linear_solve_ex(pnp_ctx *c, const double *rhs, double *z,
@@ -2666,6 +3159,7 @@ extern "C" int pnp_linear_solve_ex(pnp_ctx *c, const double *rhs, double *z,
   hipSetDevice(c->device);
   std::memset(res, 0, sizeof *res);
   const bool dev = flags & PNP_DEVICE_PTRS;
+  if (c->seq_on()) return seq_solve_abi(c, rhs, z, *o, *res, dev);
   if ((rc = c->upload_ext(rhs, c->nf, c->b.p, false, dev))) return rc;
   if ((rc = c->krylov(c->b.p, c->z.p, *o, *res))) return rc;
   if ((rc = c->download_ext(c->z.p, c->nf, z, dev))) return rc;
@@ -2695,6 +3189,7 @@ extern "C" int pnp_linear_solve(pnp_ctx *c, const double *rhs, double *z, const 
   if (!c || !rhs || !z || !o || !res) return PNP_E_ARG;
   hipSetDevice(c->device);
   std::memset(res, 0, sizeof *res);
+  if (c->seq_on()) return seq_solve_abi(c, rhs, z, *o, *res, false);
   int rc;
   if ((rc = c->upload_ext(rhs, c->nf, c->b.p, false))) return rc;
   if ((rc = c->krylov(c->b.p, c->z.p, *o, *res))) return rc;
@@ -2707,9 +3202,23 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
   if (!c->assembled) return c->fail(PNP_E_STATE, "no Jacobian assembled");
   hipSetDevice(c->device);
   int rc;
+  if (c->seq_on()) {
+    if (prec != PNP_PREC_NONE && prec != PNP_PREC_JACOBI && prec != PNP_PREC_SSOR_NATURAL)
+      return c->fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER: preconditioner must be NONE, JACOBI or SSOR_NATURAL");
+    const size_t n = c->nseq();
+    double *sb = c->sq(pnp_ctx::SQ_B), *sz = c->sq(pnp_ctx::SQ_Z);
+    CK(hipMemcpyAsync(sb, d, 8 * n, hipMemcpyHostToDevice, c->stream), "seq upload");
+    CK(hipMemsetAsync(sz, 0, 8 * n, c->stream), "seq upload");
+    if ((rc = c->seq_prec(prec, sb, sz))) return rc;
+    if (prec == PNP_PREC_SSOR_NATURAL && (rc = c->nat_check())) return rc;
+    CK(hipMemcpyAsync(v, sz, 8 * n, hipMemcpyDeviceToHost, c->stream), "seq download");
+    CK(hipStreamSynchronize(c->stream), "seq prec");
+    return PNP_OK;
+  }
   if ((rc = c->upload_ext(d, c->nf, c->b.p, false))) return rc;
   if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
   if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
+  if (prec == PNP_PREC_SSOR_NATURAL && (rc = c->nat_check())) return rc;
   return c->download_ext(c->z.p, c->nf, v);
 }
 
@@ -2737,6 +3246,17 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
   if (option == PNP_OPT_BICG_TWORED) {
     if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_BICG_TWORED takes -1, 0 or 1");
     c->twored_opt = int(value);
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_SEQ_ORDER) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER takes 0 or 1");
+    if (value && (c->degree > 1 || c->dist))
+      return c->fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER: P1 contexts of one rank only");
+    if (c->seq_opt != int(value)) {
+      c->seq_opt = int(value);
+      c->assembled = false;  // the next Jacobian is assembled in the newly selected form
+      c->csr_vals_valid = false;
+    }
     return PNP_OK;
   }
   if (option == PNP_OPT_JAC_FD) {
@@ -2801,6 +3321,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_AMG_FALLBACK) {
     *value = c->amg_fallback;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_SEQ_ORDER) {
+    *value = c->seq_opt;
     return PNP_OK;
   }
   return c->fail(PNP_E_ARG, "unknown option");
@@ -2902,6 +3426,110 @@ extern "C" int pnp_ion_flux(pnp_ctx *c, const double *x, int32_t nsurf, double *
   return PNP_OK;
 }
 
+// PDELab Newton in the reference's order (PNP_OPT_SEQ_ORDER; the oracle's orc_newton statements):
+// external layout, GridOperator residual / Jacobian in element order, ISTL solves in their order,
+// defect = sqrt(<r, r>) summed sequentially, u -= lambda z
+static int seq_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_newton_result *res) {
+  int rc;
+  if ((rc = c->seq_build())) return rc;
+  double t_start = now_s();
+  const size_t n = c->nseq();
+  double *x = c->sq(pnp_ctx::SQ_X), *r = c->sq(pnp_ctx::SQ_R), *z = c->sq(pnp_ctx::SQ_Z),
+         *prevu = c->sq(pnp_ctx::SQ_PREVU);
+  CK(hipMemcpyAsync(x, u, 8 * n, hipMemcpyHostToDevice, c->stream), "seq upload");
+  double ta = now_s();
+  if ((rc = c->seq_residual(x, r))) return rc;
+  double defect = std::sqrt(c->seq_dot(r, r, rc));
+  if (rc) return rc;
+  res->assemble_seconds += now_s() - ta;
+  res->first_defect = defect;
+  double prev_defect = defect;
+  res->status = PNP_OK;
+  const bool fd = c->fd_opt != 0;
+  for (;;) {
+    res->converged = (defect < o->abs_limit || defect < res->first_defect * o->reduction) ? 1 : 0;
+    if (res->converged) break;
+    if (res->iterations >= o->maxit) {
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    ta = now_s();
+    if ((rc = c->seq_jacobian(x, fd))) return rc;
+    CK(hipStreamSynchronize(c->stream), "seq jacobian");
+    res->assemble_seconds += now_s() - ta;
+    const double stop_defect = std::max(res->first_defect * o->reduction, o->abs_limit);
+    double lin_red;
+    if (stop_defect / (10 * defect) > defect * defect / (prev_defect * prev_defect))
+      lin_red = stop_defect / (10 * defect);
+    else
+      lin_red = std::min(o->min_linear_reduction, defect * defect / (prev_defect * prev_defect));
+    prev_defect = defect;
+    CK(hipMemsetAsync(z, 0, 8 * n, c->stream), "seq z");
+    pnp_solve_opts lo = o->linear;
+    lo.reduction = lin_red;
+    pnp_solve_result sr{};
+    double ts = now_s();
+    if ((rc = c->seq_krylov(lo, z, r, sr))) return rc;  // r: overwritten by the solve's residual
+    res->solve_seconds += now_s() - ts;
+    res->linear_iterations += sr.iterations;
+    const int step_its = sr.iterations;
+    if (sr.breakdown) {
+      res->status = PNP_E_BREAKDOWN;
+      break;
+    }
+    if (!sr.converged) {
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    // hackbuschReuskenAcceptBest
+    double lambda = 1.0, best_lambda = 0.0, best_defect = defect;
+    CK(hipMemcpyAsync(prevu, x, 8 * n, hipMemcpyDeviceToDevice, c->stream), "seq prevu");
+    int i = 0;
+    bool ls_fail = false;
+    for (;;) {
+      CK(pnp::launch_seq_aymx(int(n), lambda, x, z, c->stream), "seq update");
+      ta = now_s();
+      if ((rc = c->seq_residual(x, r))) return rc;
+      defect = std::sqrt(c->seq_dot(r, r, rc));
+      if (rc) return rc;
+      res->assemble_seconds += now_s() - ta;
+      if (defect <= (1.0 - lambda / 4) * prev_defect) break;
+      if (defect < best_defect) {
+        best_defect = defect;
+        best_lambda = lambda;
+      }
+      if (++i >= o->line_search_maxit) {
+        if (best_lambda == 0.0) {
+          ls_fail = true;
+          break;
+        }
+        if (best_lambda != lambda) {
+          CK(hipMemcpyAsync(x, prevu, 8 * n, hipMemcpyDeviceToDevice, c->stream), "seq prevu");
+          CK(pnp::launch_seq_aymx(int(n), best_lambda, x, z, c->stream), "seq update");
+          if ((rc = c->seq_residual(x, r))) return rc;
+          defect = std::sqrt(c->seq_dot(r, r, rc));
+          if (rc) return rc;
+        }
+        break;
+      }
+      lambda *= 0.5;
+      CK(hipMemcpyAsync(x, prevu, 8 * n, hipMemcpyDeviceToDevice, c->stream), "seq prevu");
+    }
+    if (ls_fail) {
+      res->status = PNP_E_NOT_CONVERGED;
+      break;
+    }
+    res->iterations++;
+    c->newton_its.push_back(step_its);
+    c->newton_defects.push_back(defect);
+  }
+  res->defect = defect;
+  CK(hipMemcpyAsync(u, x, 8 * n, hipMemcpyDeviceToHost, c->stream), "seq download");
+  CK(hipStreamSynchronize(c->stream), "seq newton");
+  res->elapsed = now_s() - t_start;
+  return PNP_OK;
+}
+
 extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_newton_result *res) {
   if (!c || !u || !o || !res) return PNP_E_ARG;
   if (c->kind < 0) return c->fail(PNP_E_STATE, "no operator set");
@@ -2909,6 +3537,7 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
   std::memset(res, 0, sizeof *res);
   c->newton_its.clear();
   c->newton_defects.clear();
+  if (c->seq_on()) return seq_newton(c, u, o, res);
   double t_start = now_s();
   int rc;
   long long n = c->nown();

@@ -431,6 +431,57 @@ struct NatSweep {
 };
 hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
                                const double *d, double *v, hipStream_t s);
+// The same two sweeps as ONE launch (dataflow): units of up to kNatUnit rows of one level, int4
+// {first sweep position, rows | width << 8 | backward << 16, the level's row count, ELL index of
+// the unit's first row}, forward units (nunits_f) then backward ones, each in level order.  An
+// operand code in ecol (both forms): c >= 0 the forward value of row c, c == -1 zero, c <= -2 the
+// backward value of row -(c + 2).  vf / vb (n each): forward / backward results; abort_word[0]
+// is set when an operand wait times out.
+constexpr int kNatUnit = 8;
+struct NatFlow {
+  const int4 *units = nullptr;
+  int nunits = 0, nunits_f = 0;
+  NatSweep fwd, bwd;
+  unsigned *abort_word = nullptr;
+};
+hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
+                                    double *vf, double *vb, hipStream_t s);
+// ---- reference-order mode (PNP_OPT_SEQ_ORDER, seq_order.hip) ----------------------------------
+// the global mesh in its own element order (external layout): tri [nt][3], xy [nv][2]; per vertex
+// v its incident elements in ascending order, vinc[vptr[v] .. vptr[v+1]) = e << 2 | local index
+struct SeqMesh {
+  int nv = 0, nt = 0;
+  const int *tri = nullptr, *vptr = nullptr, *vinc = nullptr;
+  const double *xy = nullptr;
+};
+// the operator: kind (OP_*), nfields, parameters, frozen fields (global vertex order) and x_old
+// (external layout)
+struct SeqOp {
+  int kind = 0, nf = 1, cyl = 0;
+  double pi = 3.1415, l_b = 1, c0 = 0, tau = 1, dt = 0, z = 0;
+  const double *phi = nullptr, *cp = nullptr, *cm = nullptr, *x_old = nullptr;
+};
+hipError_t launch_seq_element(const SeqMesh &M, const SeqOp &P, const double *x, int mode,
+                              double *RL, double *RLO, double *JL, hipStream_t s);
+hipError_t launch_seq_residual_gather(const SeqMesh &M, int nf, int has_old, const double *RL,
+                                      const double *RLO, const int *bptr, const double *bval,
+                                      const unsigned char *mask, double *r, hipStream_t s);
+hipError_t launch_seq_jacobian_gather(const SeqMesh &M, int nf, const double *JL,
+                                      const int *rowptr, const int *col,
+                                      const unsigned char *mask, double *val, hipStream_t s);
+hipError_t launch_seq_spmv(int n, const int *rowptr, const int *col, const double *val,
+                           const double *x, double *y, hipStream_t s);
+hipError_t launch_seq_dot(int n, const double *a, const double *b, double *out, hipStream_t s);
+hipError_t launch_seq_bicg_p(int n, double beta, double omega, double *p, const double *v,
+                             const double *r, hipStream_t s);
+hipError_t launch_seq_axpy2(int n, double a, double *x, const double *y, double *r,
+                            const double *v, hipStream_t s);
+hipError_t launch_seq_prec_diag(int n, int jacobi, const double *d, const int *diag,
+                                const double *val, double *v, hipStream_t s);
+hipError_t launch_seq_axpy(int n, double a, double *x, const double *y, hipStream_t s);
+hipError_t launch_seq_aymx(int n, double a, double *x, const double *y, hipStream_t s);
+hipError_t launch_seq_cg_p(int n, double beta, double *p, const double *q, hipStream_t s);
+
 // read n doubles of buf (cache scrub before a cache-cold timing; sink is never written)
 hipError_t launch_scrub(const double *buf, long long n, double *sink, hipStream_t s);
 

@@ -1392,6 +1392,7 @@ __device__ void derive(Scalars *S, int stage) {
     S->it_half = 0;
     S->iter = 0;
     S->breakdown = 0;
+    S->xpend = 0;  // a solve that ended between k_update_fwd0 and stage 4 must not leak it
     S->done = (S->norm < S->reduction * S->norm0 || S->norm < 1e-30) ? 1 : 0;
     return;
   }
@@ -1400,6 +1401,7 @@ __device__ void derive(Scalars *S, int stage) {
     S->it_half = 0;
     S->iter = 0;
     S->breakdown = 0;
+    S->xpend = 0;
     S->done = S->norm0 < 1e-30 ? 1 : 0;
     return;
   }

@@ -27,6 +27,9 @@
 // across ranks, as the reference's NOVLP SSOR acts on the local matrix only).
 #include "kernels.h"
 
+#include <cstdlib>
+#include <algorithm>
+
 namespace pnp {
 
 namespace {
@@ -63,13 +66,18 @@ __global__ void __launch_bounds__(kB)
     for (int u = 0; u < kS; u++) {
       const int k = kb + j + u * kL;
       const bool in = live && k < width;
-      c[u] = in ? ecol[size_t(k) * n + t] : 0;
+      c[u] = in ? ecol[size_t(k) * n + t] : -1;
       ix[u] = in ? eidx[size_t(k) * n + t] : -1;
     }
     if (kb == 0 && head) rhs = d[I.x];
     double pr[kS];
 #pragma unroll
-    for (int u = 0; u < kS; u++) pr[u] = ix[u] >= 0 ? val[ix[u]] * v[c[u]] : 0.0;
+    for (int u = 0; u < kS; u++) {
+      // in place, every operand code reads v: a zero operand (-1) is a row not yet swept or
+      // another rank's, both 0.0 in v
+      const double o = c[u] == -1 ? 0.0 : v[c[u] >= 0 ? c[u] : -(c[u] + 2)];
+      pr[u] = ix[u] >= 0 ? val[ix[u]] * o : 0.0;
+    }
 #pragma unroll
     for (int k = 0; k < kC; k++) {
       const double p = __shfl(pr[k / kL], base + k % kL, 64);
@@ -78,7 +86,146 @@ __global__ void __launch_bounds__(kB)
   }
   if (head) v[I.x] += 1.0 * (rhs / val[I.z]);
 }
+
+// ---- one launch for both sweeps: a dataflow over the level-ordered units ------------------------
+// The level launches above cost two round trips plus a dispatch per level (~680 levels at
+// config 3).  Here every wave of a resident grid takes units w, w + G, w + 2G, ... (G waves) in
+// the level order, loads its rows' entries and operands at once, and waits only for the operands
+// that are not there yet: each forward / backward result is written exactly once, as one 8-byte
+// agent-scope (write-through) store, into a vector that was set to the all-ones pattern (a NaN no
+// arithmetic produces here) before the launch, so a value that is not all-ones is final.  That is
+// the data-tagged granule hand-off of cdna_hip_programming.md Guideline 16 (R2) with the value as
+// its own tag: relaxed agent-scope atomic loads poll it, no fence is needed.  The critical path is
+// the chain of row dependencies (the level count), each hop one store-to-poll latency instead of
+// a launch.
+// Progress: a unit depends only on units earlier in the order.  The earliest unfinished unit's
+// wave has finished all its own earlier units, so it is working on that unit, whose operands are
+// all final: some wave always advances, provided every wave of the grid is resident (the grid is
+// sized from the occupancy query, and one context runs one stream).  Every wait is bounded: a
+// wave that waits longer than kNatTimeout sets abort_word, and every wave that sees it stops
+// waiting and takes NaN operands, so the grid always drains.
+// The arithmetic is the level kernel's: same products, same shuffle-ordered subtraction, the
+// forward result 0.0 + 1.0 * (rhs / a_RR), the backward one v_R + 1.0 * (rhs / a_RR).
+constexpr unsigned long long kNatPending = ~0ull;
+constexpr unsigned long long kNatTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
+
+__device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(kB)
+    k_ssor_nat_flow(const int4 *__restrict__ units, int nunits, int nunits_f,
+                    const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
+                    const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
+                    const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
+                    const double *__restrict__ val, const double *__restrict__ d,
+                    unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
+  const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
+  const int G = gridDim.x * (kB / 64);
+  for (int u = blockIdx.x * (kB / 64) + threadIdx.x / 64; u < nunits; u += G) {
+    const int4 U = units[u];
+    const bool bwd = u >= nunits_f;  // uniform
+    const int rows = U.y & 255, width = (U.y >> 8) & 255;
+    const int4 *info = bwd ? info_b : info_f;
+    const int *ecol = bwd ? ecol_b : ecol_f, *eidx = bwd ? eidx_b : eidx_f;
+    const bool live = t < rows;
+    const bool head = live && j == 0;
+    const int4 I = live ? info[U.x + t] : make_int4(0, 0, 0, 0);
+    double rhs = 0.0;
+    for (int kb = 0; kb < width; kb += kC) {
+      int c[kS], ix[kS];
+#pragma unroll
+      for (int q = 0; q < kS; q++) {
+        const int k = kb + j + q * kL;
+        const bool in = live && k < width;
+        const size_t at = size_t(U.w) + size_t(k) * U.z + t;
+        c[q] = in ? ecol[at] : -1;
+        ix[q] = in ? eidx[at] : -1;
+      }
+      if (kb == 0 && head) rhs = d[I.x];
+      unsigned long long b[kS];
+      double a[kS];
+#pragma unroll
+      for (int q = 0; q < kS; q++) {
+        a[q] = ix[q] >= 0 ? val[ix[q]] : 0.0;
+        b[q] = c[q] == -1 ? 0ull : nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+      }
+      bool pend = false;
+#pragma unroll
+      for (int q = 0; q < kS; q++) pend |= b[q] == kNatPending;
+      if (__any(pend)) {
+        const unsigned long long t0 = wall_clock64();
+        while (true) {
+          __builtin_amdgcn_s_sleep(1);
+          pend = false;
+#pragma unroll
+          for (int q = 0; q < kS; q++)
+            if (b[q] == kNatPending) {
+              b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+              pend |= b[q] == kNatPending;
+            }
+          if (!__any(pend)) break;
+          const bool late = wall_clock64() - t0 > kNatTimeout;
+          if (late && lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+          if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+            for (int q = 0; q < kS; q++)
+              if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;  // NaN: drain the grid
+            break;
+          }
+        }
+      }
+      double pr[kS];
+#pragma unroll
+      for (int q = 0; q < kS; q++) pr[q] = ix[q] >= 0 ? a[q] * __longlong_as_double(b[q]) : 0.0;
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const double p = __shfl(pr[k / kL], base + k % kL, 64);
+        if (head && kb + k < width) rhs -= p;
+      }
+    }
+    if (head) {
+      // the row's own forward value is final: its diagonal entry's operand was waited for above
+      double own = 0.0;
+      if (bwd) {
+        unsigned long long w;
+        while ((w = nat_ld(vf + I.x)) == kNatPending &&
+               !__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        }
+        own = __longlong_as_double(w);
+      }
+      const double out = own + 1.0 * (rhs / val[I.z]);
+      __hip_atomic_store(bwd ? vb + I.x : vf + I.x,
+                         (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 }  // namespace
+
+hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
+                                    double *vf, double *vb, hipStream_t s) {
+  static int grid = [] {
+    int dev = 0, cus = 0, per = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_flow, kB, 0);
+    const char *ev = std::getenv("PNP_NAT_FLOW_WG_PER_CU");  // A/B knob, capped at the occupancy
+    if (ev && std::atoi(ev) > 0) per = std::min(per, std::atoi(ev));
+    return std::max(1, cus * std::max(1, per));
+  }();
+  hipError_t e = hipMemsetAsync(vf, 0xFF, sizeof(double) * size_t(n), s);
+  if (e == hipSuccess) e = hipMemsetAsync(vb, 0xFF, sizeof(double) * size_t(n), s);
+  if (e != hipSuccess) return e;
+  const int blocks = std::min(grid, (F.nunits + kB / 64 - 1) / (kB / 64));
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ssor_nat_flow, dim3(blocks), dim3(kB), 0, s, F.units, F.nunits, F.nunits_f,
+                     F.fwd.info, F.fwd.ecol, F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val,
+                     d, reinterpret_cast<unsigned long long *>(vf),
+                     reinterpret_cast<unsigned long long *>(vb), F.abort_word);
+  return hipGetLastError();
+}
 
 hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
                                const double *d, double *v, hipStream_t s) {

@@ -361,7 +361,15 @@ enum {
    * it saves the host's per-kernel launch cost where the kernels are shorter than it.  -1
    * (default): on for contexts of up to 131,072 owned rows; 0 off; 1 on (the environment
    * variable PNP_GRAPH=0/1 sets the default).  Not used with AMG, timers or more than one rank. */
-  PNP_OPT_GRAPH = 6
+  PNP_OPT_GRAPH = 6,
+  /* 1: reference-order mode.  pnp_residual / pnp_jacobian / pnp_jacobian_apply / pnp_linear_solve /
+   * pnp_prec_apply / pnp_newton then perform the reference's single-rank arithmetic in its order
+   * (element-order GridOperator assembly into the CSR view, ISTL's sequential mv / dot / vector
+   * updates, PDELab Newton's defect as a sequential sum), so iterates and iteration counts are
+   * the reference program's even where BiCGSTAB is chaotic in the last bits.  A parity mode, far
+   * slower than the default.  Preconditioners NONE, JACOBI, SSOR_NATURAL; P1 contexts of one rank;
+   * pnp_op_args.c_extra unsupported.  0 (default): the GPU's own summation orders. */
+  PNP_OPT_SEQ_ORDER = 7
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 

@@ -1,0 +1,173 @@
+"""Reference-order mode (PNP_OPT_SEQ_ORDER, -m gpu): the reference's single-rank arithmetic in its
+order on the GPU (dune-pnp_amd/csrc/seq_order.hip).  The oracle (oracle/pnp_oracle.c) restates the
+same statements on the CPU, so everything here is compared BIT FOR BIT:
+  * GridOperator::residual / ::jacobian (analytic and PDELab's forward-difference Jacobian,
+    src/pnp_operator.hh:22-27) in element order (src/stationary_pnp_from_pb.hh:165,315-321);
+  * ISTL BiCGSTAB with NOPREC / SeqSSOR (the reference's BCGS_NOPREC and BCGS_SSORk,
+    src/stationary_pnp_from_pb.hh:168-169,329-331; src/instationary_pnp_from_pb_md.hh:188-191) and
+    CG with Jacobi (src/instationary_pnp_from_pb_md.hh:198-206): the same ISTL half-step counts,
+    including the chaotic first PNP Newton system of pore_small (227 vs 133.5 half steps in the
+    default GPU order);
+  * PDELab Newton (src/stationary_pnp_from_pb.hh:355-369): the same per-step linear iteration
+    counts and the same solution.
+PB's sinh / cosh come from the device math library, whose last bit may differ from the host's
+libm: the PB cases allow 1e-15 relative there and compare step counts only."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import pnp_amd as P
+from test_gpu import CASES, golden, set_ops
+
+pytestmark = pytest.mark.gpu
+
+EXACT = [c for c in CASES if c[1] != "pb"]
+PB = [c for c in CASES if c[1] == "pb"]
+
+
+def _ctx(mesh, par):
+    ctx = P.Context(mesh, par)
+    ctx.set_option(P.OPT_SEQ_ORDER, 1)
+    return ctx
+
+
+def _state(z, kind):
+    return z[kind + "_x"]
+
+
+@pytest.mark.parametrize("name,kind", EXACT)
+def test_seq_residual_is_the_oracle_bitwise(name, kind):
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    op = set_ops(z, ctx, orc, kind)
+    x = _state(z, kind)
+    np.testing.assert_array_equal(ctx.residual(x), orc.residual(op, x))
+
+
+@pytest.mark.parametrize("fd", [False, True])
+@pytest.mark.parametrize("name,kind", EXACT)
+def test_seq_jacobian_is_the_oracle_bitwise(name, kind, fd):
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    op = set_ops(z, ctx, orc, kind)
+    x = _state(z, kind)
+    Jg = ctx.jacobian(x, fd=fd).tocsr()
+    Jo = orc.jacobian(op, x, fd=fd).tocsr()
+    D = (Jg - Jo).tocsr()
+    D.eliminate_zeros()
+    assert D.nnz == 0, f"{D.nnz} entries differ, max {abs(D).max()}"
+    # the oracle's full pattern holds only exact zeros outside the GPU's pattern
+    assert Jg.nnz <= Jo.nnz
+
+
+@pytest.mark.parametrize("name,kind", PB)
+def test_seq_pb_residual_and_jacobian_to_libm_rounding(name, kind):
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    op = set_ops(z, ctx, orc, kind)
+    x = _state(z, kind)
+    r, ro = ctx.residual(x), orc.residual(op, x)
+    assert np.max(np.abs(r - ro)) <= 1e-15 * np.max(np.abs(ro))
+    Jg, Jo = ctx.jacobian(x).tocsr(), orc.jacobian(op, x).tocsr()
+    assert abs(Jg - Jo).max() <= 1e-15 * abs(Jo).max()
+
+
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_SSOR_NATURAL])
+@pytest.mark.parametrize("name", ["pore_small_k0", "cylinder_k0"])
+def test_seq_bicgstab_first_pnp_newton_system_half_steps_exact(name, prec):
+    """The chaotic system of test_gpu_ssor_natural.py: in the reference's order the GPU takes the
+    oracle's half steps exactly and returns the oracle's solution bit for bit."""
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    op = set_ops(z, ctx, orc, "pnp")
+    x = z["newton_pnp_x0"]
+    J = ctx.jacobian(x)
+    rhs = ctx.residual(x)
+    np.testing.assert_array_equal(rhs, orc.residual(op, x))
+    sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-8, maxit=20000)
+    oprec = O.PREC_NONE if prec == P.PREC_NONE else O.PREC_SSOR
+    xo, ro = O.bicgstab(orc.jacobian(op, x), rhs, prec=oprec, reduction=1e-8, maxit=20000)
+    print(f"{name} prec {prec}: GPU {res['it_half']} half steps, oracle {ro.it_half}")
+    assert res["it_half"] == ro.it_half
+    assert res["converged"] == ro.converged
+    np.testing.assert_array_equal(sol, xo)
+
+
+def test_seq_cg_jacobi_matches_oracle():
+    """ISTL CGSolver + Jacobi (LINEARSOLVER CG_Jacobi) on the implicit-Euler diffusion system."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    nv = mesh.nv
+    phi = np.ascontiguousarray(z["diff_phi"])
+    xo_ = np.ascontiguousarray(z["pnp_ie_x_old"][nv:2 * nv])
+    ctx = _ctx(mesh, par)
+    ctx.set_operator(P.OP_DIFF_IMPLICIT_EULER, dt=1e-3, z=1.0, field=1, phi=phi, x_old=xo_)
+    op = orc.operator(O.OP_DIFF_IE, flux=orc.flux(),
+                      mask=np.ascontiguousarray(orc.mask(3)[nv:2 * nv]), dt=1e-3, z=1.0, phi=phi,
+                      x_old=xo_)
+    ctx.jacobian(xo_)
+    rhs = ctx.residual(xo_) + 0.01
+    for prec, oprec in ((P.PREC_JACOBI, O.PREC_JACOBI), (P.PREC_NONE, O.PREC_NONE)):
+        sol, res = ctx.linear_solve(rhs, prec=prec, reduction=1e-10, maxit=2000,
+                                    method=P.METHOD_CG)
+        xo, ro = O.cg(orc.jacobian(op, xo_), rhs, prec=oprec, reduction=1e-10, maxit=2000)
+        assert res["iterations"] == ro.iterations
+        np.testing.assert_array_equal(sol, xo)
+
+
+@pytest.mark.parametrize("fd", [False, True])
+@pytest.mark.parametrize("prec", [P.PREC_NONE, P.PREC_SSOR_NATURAL])
+@pytest.mark.parametrize("name", ["pore_small_k0", "cylinder_k0"])
+def test_seq_pnp_newton_is_the_oracle_newton(name, prec, fd):
+    """Stationary PNP Newton as the reference's driver runs it (BCGS_NOPREC / BCGS_SSORk, the
+    analytic or the forward-difference Jacobian): every step's BiCGSTAB count equal, the same number
+    of Newton steps, the same solution bit for bit."""
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    ctx.set_option(P.OPT_JAC_FD, int(fd))
+    u, res = ctx.newton(z["newton_pnp_x0"], prec=prec, linear_maxit=20000)
+    its, _ = ctx.newton_history()
+    op = orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3))
+    oprec = O.PREC_NONE if prec == P.PREC_NONE else O.PREC_SSOR
+    uo, ro = orc.newton(op, z["newton_pnp_x0"], prec=oprec, fd=fd)
+    its_o = list(ro.step_linear_iterations[:ro.iterations])
+    print(f"{name} prec {prec} fd {fd}: GPU {list(its)} oracle {its_o}")
+    assert res["iterations"] == ro.iterations and res["converged"] == ro.converged
+    assert list(its) == its_o
+    np.testing.assert_array_equal(u, uo)
+
+
+def test_seq_pnp_ie_newton_steps_match_oracle():
+    """One implicit-Euler step (PnpOperator + PnpTOperator, quirk Q2) with BCGS_SSORk."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    ctx = _ctx(mesh, par)
+    op = set_ops(z, ctx, orc, "pnp_ie")
+    x0 = np.ascontiguousarray(z["pnp_ie_x_old"])
+    u, res = ctx.newton(x0, prec=P.PREC_SSOR_NATURAL)
+    its, _ = ctx.newton_history()
+    uo, ro = orc.newton(op, x0, prec=O.PREC_SSOR)
+    assert list(its) == list(ro.step_linear_iterations[:ro.iterations])
+    np.testing.assert_array_equal(u, uo)
+
+
+@pytest.mark.parametrize("name", ["sphere_k0", "pore_small_k0"])
+def test_seq_pb_newton_step_counts_match_oracle(name):
+    z, mesh, par, orc = golden(name)
+    ctx = _ctx(mesh, par)
+    ctx.set_operator(P.OP_PB)
+    u, res = ctx.newton(np.zeros(mesh.nv), prec=P.PREC_SSOR_NATURAL)
+    its, _ = ctx.newton_history()
+    op = orc.operator(O.OP_PB, flux=orc.flux(), mask=orc.mask(1))
+    uo, ro = orc.newton(op, np.zeros(mesh.nv), prec=O.PREC_SSOR)
+    assert list(its) == list(ro.step_linear_iterations[:ro.iterations])
+    assert np.max(np.abs(u - uo)) <= 1e-12 * max(np.max(np.abs(uo)), 1e-300)
+
+
+def test_seq_mode_rejects_other_preconditioners():
+    z, mesh, par, orc = golden("cylinder_k0")
+    ctx = _ctx(mesh, par)
+    set_ops(z, ctx, orc, "pnp")
+    x = z["pnp_x"]
+    ctx.jacobian(x)
+    with pytest.raises(P.PnpError):
+        ctx.linear_solve(ctx.residual(x), prec=P.PREC_ILU0)

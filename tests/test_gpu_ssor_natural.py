@@ -224,3 +224,36 @@ def test_ssor_natural_level_graph_bitwise_equals_captured_and_eager(name, kind):
         sol, res = ctx.linear_solve(rhs, prec=P.PREC_SSOR_NATURAL, reduction=1e-10, maxit=5000)
         out.setdefault(g, []).append((sol.tobytes(), res["iterations"], res["it_half"]))
     assert out[1][0] == out[0][0] == out[0][1]
+
+
+def test_graph_cache_survives_csr_pattern_switch():
+    """a BiCGSTAB block graph captured with SSOR_NATURAL holds the CSR view's
+    buffers; switching PB -> PNP -> PB rebuilds them.  With graphs forced on, every solve must equal
+    the same solve on a fresh context (graphs off), bit for bit."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    nv = mesh.nv
+
+    def pb_solve(ctx):
+        ctx.set_operator(P.OP_PB)
+        J = ctx.jacobian(np.zeros(nv))
+        rhs = np.random.default_rng(5).standard_normal(nv)
+        return ctx.linear_solve(rhs, prec=P.PREC_SSOR_NATURAL, reduction=1e-8, maxit=500,
+                                check_every=4)
+
+    def pnp_solve(ctx):
+        set_ops(z, ctx, orc, "pnp")
+        ctx.jacobian(z["newton_pnp_x0"])
+        rhs = ctx.residual(z["newton_pnp_x0"])
+        return ctx.linear_solve(rhs, prec=P.PREC_SSOR_NATURAL, reduction=1e-4, maxit=500,
+                                check_every=4)
+
+    ctx = P.Context(mesh, par)
+    ctx.set_option(P.OPT_GRAPH, 1)
+    got = [pb_solve(ctx), pnp_solve(ctx), pb_solve(ctx)]
+    for k, f in enumerate([pb_solve, pnp_solve, pb_solve]):
+        ref = P.Context(mesh, par)
+        ref.set_option(P.OPT_GRAPH, 0)
+        want = f(ref)
+        np.testing.assert_array_equal(got[k][0], want[0])
+        assert got[k][1]["it_half"] == want[1]["it_half"]
+        ref.close()
