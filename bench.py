@@ -510,7 +510,23 @@ def main():
                   "first_defect": nres["first_defect"], "defect": nres["defect"],
                   "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                   "reduction": nt_red, "min_linear_reduction": nt_linred,
-                  "preconditioner": args.prec}
+                  "preconditioner": args.prec + (", f32 factors" if prec == P.PREC_ILU0 else "")}
+    # the same with fp64 ILU(0) factors (the default stores them in single precision): the f32
+    # choice's effect on time to solution, linear iterations and seconds side by side
+    newton_f64 = None
+    if not args.no_solve and prec == P.PREC_ILU0:
+        ctx.set_option(P.OPT_ILU_F32, 0)
+        barrier_sync(dist, world)
+        t0 = time.perf_counter()
+        _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=prec,
+                             linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
+        barrier_sync(dist, world)
+        newton_f64 = {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
+                      "iterations": nres["iterations"],
+                      "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
+                      "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
+                      "preconditioner": "ilu0, fp64 factors"}
+        ctx.set_option(P.OPT_ILU_F32, 1)
     # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB
     newton_amg = None
     if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
@@ -575,9 +591,12 @@ def main():
                "gpu_vs_cpu_parity": cb["parity"]}
         cpu_all = {"value": cb["mt_dofs_per_s"], "unit": "assembled DOFs/s",
                    "cores": cb["mt_threads"], "kind": "port",
+                   "label": f"{cb['mt_threads']} threads (not all {hostcpu['host_logical_cpus']} "
+                            f"host CPUs: the GPU box gives one GPU's job a 16-CPU share and sets "
+                            f"OMP_NUM_THREADS={hostcpu['omp_num_threads']})",
                    "sample": (f"the same assembly on the same sample with OpenMP over element "
                               f"colours (orc_assemble_mt), {cb['mt_threads']} threads "
-                              f"(OMP_NUM_THREADS / host), {cb['mt_assembly_s']:.4f} s per "
+                              f"(OMP_NUM_THREADS), {cb['mt_assembly_s']:.4f} s per "
                               f"assembly; ISTL BiCGSTAB NOPREC row-parallel "
                               f"{cb['bicgstab_nonprec_s_per_it_mt'] * 1e3:.2f} ms/it"),
                    "bicgstab_nonprec_iters_per_s": 1.0 / cb["bicgstab_nonprec_s_per_it_mt"],
@@ -659,19 +678,26 @@ def main():
                                                 "slot, split ILU(0) factors, vectors)",
                                   "ilu_factor_precision": "f32" if info["ilu_f32"] else "f64",
                                   "contract_bytes_per_iter": M["it_contract"]["bytes"],
-                                  "contract_achieved": M["it_contract"]["achieved"],
-                                  "contract_frac": M["it_contract"]["frac"],
+                                  "contract_model_gbs": M["it_contract"]["achieved"],
+                                  "contract_model_ratio": M["it_contract"]["frac"],
+                                  "contract_model_note": "SURVEY.md §8(d)'s fp64-CSR byte count "
+                                                         "/ iteration time / 8 TB/s: a ratio of "
+                                                         "the contract model, NOT a bandwidth "
+                                                         "(the k-form SELL values and the f32 "
+                                                         "factors move fewer bytes than the "
+                                                         "fp64 CSR the contract counts)",
                                   "kernels": {"spmv": M["spmv_stored"],
                                               "ilu0_apply": M["ilu_stored"],
                                               "blas_per_iter": M["blas"]}},
             "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_all,
+            "cpu_baseline_multithread": cpu_all,
             "setup_s": t_setup,
             "pb_newton": {"iterations": pb_res["iterations"],
                           "linear_iterations": pb_res["linear_iterations"],
                           "converged": pb_res["converged"]},
             "event_timers_ms": tm,
             "pnp_newton_time_to_solution": newton,
+            "pnp_newton_time_to_solution_f64_factors": newton_f64,
             "pnp_newton_time_to_solution_amg": newton_amg,
             "strong_scaling": strong,
             "rccl_parity": parity,

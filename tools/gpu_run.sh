@@ -27,6 +27,11 @@ for step in "$@"; do
               timeout -k 10 600 rocprofv3 --pmc $set GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_$tag" -o run -- python3 tools/prof_target.py 4 10 10 ilu0 > "$OUT/pmcmem.log" 2>&1; rc=$?
               fatal $rc && break
             done ;;
+    calib)  rc=0
+            timeout -k 10 120 tools/micro/fetch_calib 2 > "$OUT/calib_stdout.txt" 2> "$OUT/calib.log"; rc=$?
+            fatal $rc || [ $rc -ne 0 ] || { timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/calib_fetch" -o run -- tools/micro/fetch_calib 2 >> "$OUT/calib.log" 2>&1; rc=$?; }
+            fatal $rc || [ $rc -ne 0 ] || { timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/calib_write" -o run -- tools/micro/fetch_calib 2 >> "$OUT/calib.log" 2>&1; rc=$?; }
+            fatal $rc || [ $rc -ne 0 ] || { timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace --output-format csv -d "$OUT/calib_req" -o run -- tools/micro/fetch_calib 2 >> "$OUT/calib.log" 2>&1; rc=$?; } ;;
     ab)     : > "$OUT/ab.log"; rc=0
             for i in 1 2 3; do
               timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
