@@ -216,6 +216,24 @@ struct pnp_ctx {
   bool nat_units_ok = false;
   DBuf<unsigned> nat_abort;  // [0]: set by a sweep whose operand wait timed out (sticky)
   DBuf<int> csr_diag;        // index of each CSR-view row's diagonal entry
+  // ILU(0) application as one dataflow launch (PNP_OPT_ILU_FLOW, linalg.hip k_ilu0_flow): per
+  // c_first (0: every colour in the launch, 1: colour 0's forward step done by the update kernel)
+  // the unit table and dependency lists, built on first use from the staging lists (host copies
+  // kept from the layout build: rows at each L / U split position, lsx / usx lists)
+  int ilu_flow_opt = [] {
+    const char *e = std::getenv("PNP_ILU_FLOW");
+    return (e && std::atoi(e) != 0) ? 1 : 0;
+  }();
+  std::vector<int> h_posrowL, h_posrowU, h_lsx_ptr, h_lsx_list, h_usx_ptr, h_usx_list;
+  struct IluFlowDev {
+    bool built = false, ok = false;
+    pnp::IluFlow F;
+    DBuf<int> dep_ptr, dep_list;
+    DBuf<unsigned> flags;
+  };
+  IluFlowDev ilu_flow[2];
+  DBuf<unsigned> ilu_flow_abort;
+  bool ilu_flow_used = false;  // a flow launch ran since the last check
   // ---- reference-order mode (PNP_OPT_SEQ_ORDER, seq_order.hip) -----------------------------
   int seq_opt = 0;
   bool seq_built = false, seq_op_valid = false;
@@ -897,6 +915,163 @@ struct pnp_ctx {
     }
     return PNP_OK;
   }
+  // ---- ILU(0) application as one dataflow launch (PNP_OPT_ILU_FLOW) -----------------------------
+  // Units in the colour launches' order (forward colours c_first .. nc-2, the last colour, backward
+  // colours nc-2 .. 0), one per 256-position block of the colour.  A unit's dependencies (all
+  // earlier in the order): forward / last -- the forward units of the rows in its L staging list;
+  // backward -- the backward (or last-colour) units of the rows in its U list, the forward units of
+  // its own rows (their forward values are its input) and every forward unit whose L list holds one
+  // of its rows (which must have read that row's forward value before it is overwritten).
+  int ilu_flow_build(int c_first, IluFlowDev &D) {
+    D.built = true;
+    D.ok = false;
+    const int nc = int(L.color_ptr.size()) - 1;
+    const std::vector<int> &cp = L.color_ptr;
+    if (!dl.lsx_ptr || nc < 2 || h_posrowL.empty()) return PNP_OK;
+    std::vector<int> nb(nc), blk0(nc + 1, 0);
+    for (int c = 0; c < nc; c++) {
+      nb[c] = (cp[c + 1] - cp[c] + 255) / 256;
+      blk0[c + 1] = blk0[c] + nb[c];
+    }
+    std::vector<std::pair<int, int>> stages;  // {kind, colour}
+    for (int c = c_first; c < nc - 1; c++) stages.push_back({0, c});
+    stages.push_back({2, nc - 1});
+    for (int c = nc - 2; c >= 0; c--) stages.push_back({1, c});
+    if (int(stages.size()) > pnp::kIluFlowMaxStages) return PNP_OK;
+    pnp::IluFlow F;
+    F.nstages = int(stages.size());
+    int nu = 0;
+    for (int s = 0; s < F.nstages; s++) {
+      const int c = stages[s].second;
+      F.unit0[s] = nu;
+      F.kind[s] = stages[s].first;
+      F.r0[s] = cp[c];
+      F.r1[s] = cp[c + 1];
+      F.blk0[s] = blk0[c];
+      nu += nb[c];
+    }
+    F.unit0[F.nstages] = nu;
+    F.nunits = nu;
+    const int no = L.n_owned;
+    std::vector<int> fwdu(no, -1), bwdu(no, -1);
+    for (int s = 0; s < F.nstages; s++) {
+      const int c = stages[s].second, kind = stages[s].first;
+      for (int p = cp[c]; p < cp[c + 1]; p++) {
+        const int u = F.unit0[s] + (p - cp[c]) / 256;
+        if (kind != 1) fwdu[h_posrowL[p]] = u;
+        if (kind != 0) bwdu[h_posrowU[p]] = u;
+      }
+    }
+    // readers[r]: forward / last units whose L list holds row r (CSR)
+    std::vector<int> rptr(no + 1, 0), rdr;
+    auto lblock = [&](int s, int u) { return F.blk0[s] + (u - F.unit0[s]); };
+    for (int pass = 0; pass < 2; pass++) {
+      for (int s = 0; s < F.nstages; s++) {
+        if (F.kind[s] == 1) continue;
+        for (int u = F.unit0[s]; u < F.unit0[s + 1]; u++) {
+          const int b = lblock(s, u);
+          for (int k = h_lsx_ptr[b]; k < h_lsx_ptr[b + 1]; k++) {
+            const int j = h_lsx_list[k];
+            if (pass == 0)
+              rptr[j + 1]++;
+            else
+              rdr[rptr[j]++] = u;
+          }
+        }
+      }
+      if (pass == 0) {
+        for (int r = 0; r < no; r++) rptr[r + 1] += rptr[r];
+        rdr.assign(rptr[no], 0);
+      } else {
+        for (int r = no; r > 0; r--) rptr[r] = rptr[r - 1];
+        rptr[0] = 0;
+      }
+    }
+    std::vector<int> dptr(nu + 1, 0), dlist, dep;
+    for (int s = 0; s < F.nstages; s++) {
+      const int c = stages[s].second;
+      for (int u = F.unit0[s]; u < F.unit0[s + 1]; u++) {
+        const int b = lblock(s, u);
+        dep.clear();
+        if (F.kind[s] != 1) {
+          for (int k = h_lsx_ptr[b]; k < h_lsx_ptr[b + 1]; k++)
+            if (fwdu[h_lsx_list[k]] >= 0) dep.push_back(fwdu[h_lsx_list[k]]);
+        } else {
+          for (int k = h_usx_ptr[b]; k < h_usx_ptr[b + 1]; k++)
+            if (bwdu[h_usx_list[k]] >= 0) dep.push_back(bwdu[h_usx_list[k]]);
+          const int p0 = cp[c] + 256 * (u - F.unit0[s]), p1 = std::min(cp[c + 1], p0 + 256);
+          for (int p = p0; p < p1; p++) {
+            const int r = h_posrowU[p];
+            if (fwdu[r] >= 0) dep.push_back(fwdu[r]);
+            for (int k = rptr[r]; k < rptr[r + 1]; k++) dep.push_back(rdr[k]);
+          }
+        }
+        std::sort(dep.begin(), dep.end());
+        dep.erase(std::unique(dep.begin(), dep.end()), dep.end());
+        for (int w : dep)
+          if (w >= u) return fail(PNP_E_STATE, "ILU(0) dataflow: a unit depends on a later one");
+        dlist.insert(dlist.end(), dep.begin(), dep.end());
+        dptr[u + 1] = int(dlist.size());
+      }
+    }
+    if (dlist.empty()) dlist.push_back(0);
+    auto upv = [&](auto &buf, const auto &vec, const char *what) -> int {
+      hipError_t e2 = buf.alloc(vec.size());
+      if (e2 == hipSuccess)
+        e2 = hipMemcpy(buf.p, vec.data(), sizeof(vec[0]) * vec.size(), hipMemcpyHostToDevice);
+      return e2 == hipSuccess ? PNP_OK : hipfail(e2, what);
+    };
+    int rc;
+    if ((rc = upv(D.dep_ptr, dptr, "ILU(0) dataflow deps")) ||
+        (rc = upv(D.dep_list, dlist, "ILU(0) dataflow deps")))
+      return rc;
+    hipError_t e = D.flags.alloc(size_t(nu + 1 + 3) & ~size_t(3));
+    if (e == hipSuccess && !ilu_flow_abort.p) {
+      e = ilu_flow_abort.alloc(4);
+      if (e == hipSuccess) e = hipMemset(ilu_flow_abort.p, 0, 16);
+    }
+    if (e != hipSuccess) return hipfail(e, "ILU(0) dataflow flags");
+    F.dep_ptr = D.dep_ptr.p;
+    F.dep_list = D.dep_list.p;
+    F.flags = D.flags.p;
+    F.abort_word = ilu_flow_abort.p;
+    D.F = F;
+    D.ok = true;
+    return PNP_OK;
+  }
+  // v = ILU(0)^-1 d over the owned rows, colours from c_first (launch_ilu0_apply's contract): one
+  // dataflow launch when PNP_OPT_ILU_FLOW is on and d and v are distinct, else the colour launches
+  int ilu_apply(const double *d, double *vout, int c_first, const char *what) {
+    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1)) {
+      IluFlowDev &D = ilu_flow[c_first];
+      int rc;
+      if (!D.built && (rc = ilu_flow_build(c_first, D))) return rc;
+      if (D.ok) {
+        hipError_t e = pnp::launch_ilu0_flow(dl, D.F, nf, pat, lvals.p, uvals.p, d, vout, stream,
+                                             f32_now());
+        if (e != hipSuccess) return hipfail(e, what);
+        ilu_flow_used = true;
+        return PNP_OK;
+      }
+    }
+    hipError_t e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d,
+                                          vout, stream, c_first, nullptr, nullptr, f32_now());
+    return e == hipSuccess ? PNP_OK : hipfail(e, what);
+  }
+  // a dataflow application that timed out (never expected) leaves void results and a sticky word
+  int ilu_flow_check() {
+    if (!ilu_flow_used || !ilu_flow_abort.p) return PNP_OK;
+    ilu_flow_used = false;
+    unsigned w = 0;
+    hipError_t e = hipMemcpyAsync(&w, ilu_flow_abort.p, 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "ILU(0) dataflow status");
+    if (w) {
+      hipMemsetAsync(ilu_flow_abort.p, 0, 16, stream);
+      return fail(PNP_E_HIP, "ILU(0) dataflow application timed out waiting for a unit");
+    }
+    return PNP_OK;
+  }
   // the level launches: one graph replay (captured on first use; PNP_NAT_GRAPH=0: eager), or eager
   // when the stream is itself being captured (a BiCGSTAB block graph then holds them), with more
   // than one rank, or after a failed capture
@@ -1402,8 +1577,7 @@ struct pnp_ctx {
       e = pnp::launch_sgs(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout, tsgs.p,
                           stream);
     } else if (prec == PNP_PREC_ILU0) {
-      e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d, vout,
-                                 stream, 0, nullptr, nullptr, f32_now());
+      return ilu_apply(d, vout, 0, "preconditioner");
     } else if (prec == PNP_PREC_SSOR_NATURAL) {
       e = ssor_natural(d, vout);
     } else {
@@ -1483,9 +1657,8 @@ struct pnp_ctx {
     const int c0_end = L.color_ptr.size() > 1 ? L.color_ptr[1] : 0;
     auto ilu_from1 = [&](const double *d, double *out) -> int {
       hipEvent_t tp = tb(T_PREC);
-      hipError_t ee = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p,
-                                             d, out, stream, 1, nullptr, nullptr, f32_now());
-      if (ee != hipSuccess) return hipfail(ee, "preconditioner");
+      const int rc1 = ilu_apply(d, out, 1, "preconditioner");
+      if (rc1) return rc1;
       te(T_PREC, tp);
       return PNP_OK;
     };
@@ -1632,6 +1805,7 @@ struct pnp_ctx {
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hipfail(e, "bicgstab result");
     if (prec == PNP_PREC_SSOR_NATURAL && (rc = nat_check())) return rc;
+    if (prec == PNP_PREC_ILU0 && (rc = ilu_flow_check())) return rc;
     double it = std::min(double(maxit), hS->it_half);
     res.converged = hS->done == 1 ? 1 : 0;
     res.breakdown = hS->breakdown;
@@ -2484,6 +2658,18 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       c->dl.usx_list = c->d_usx_list.p;
       c->dl.usx_idx = c->d_usx_idx.p;
       c->dl.sx_max = mx;
+      // host copies for the one-launch ILU(0) application's dependency lists (ilu_flow_build)
+      c->h_posrowL.resize(npos);
+      c->h_posrowU.resize(npos);
+      for (int pos = 0; pos < npos; pos++) {
+        c->h_posrowL[pos] = rowL(pos);
+        c->h_posrowU[pos] = rowU(pos);
+      }
+      c->h_lsx_ptr = lp;
+      c->h_lsx_list = ll;
+      c->h_usx_ptr = up2;
+      c->h_usx_list = ul;
+      c->ilu_flow[0].built = c->ilu_flow[1].built = false;
     }
   }
   {  // row-contiguous block offsets and columns of the owned rows (fused ILU(0) factorisation)
@@ -3219,6 +3405,7 @@ extern "C" int pnp_prec_apply(pnp_ctx *c, int32_t prec, const double *d, double 
   if (prec == PNP_PREC_ILU0 && (rc = c->ilu_factor())) return rc;
   if ((rc = c->precond(prec, c->b.p, c->z.p))) return rc;
   if (prec == PNP_PREC_SSOR_NATURAL && (rc = c->nat_check())) return rc;
+  if (prec == PNP_PREC_ILU0 && (rc = c->ilu_flow_check())) return rc;
   return c->download_ext(c->z.p, c->nf, v);
 }
 
@@ -3236,6 +3423,11 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
       c->ilu_f32 = int(value);
       if (c->split_of == 2) c->split_of = 0;  // re-split the factors in the new precision
     }
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_ILU_FLOW) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_FLOW takes 0 or 1");
+    c->ilu_flow_opt = int(value);
     return PNP_OK;
   }
   if (option == PNP_OPT_AMG_FALLBACK) {
@@ -3317,6 +3509,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_BICG_TWORED) {
     *value = c->twored_opt;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_ILU_FLOW) {
+    *value = c->ilu_flow_opt;
     return PNP_OK;
   }
   if (option == PNP_OPT_AMG_FALLBACK) {

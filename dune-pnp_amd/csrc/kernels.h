@@ -346,6 +346,26 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int 
                              const void *lv, const void *uv, const double *d, double *v,
                              hipStream_t s, int c_first = 0, const double *add = nullptr,
                              double *out = nullptr, int f32 = 0);
+// The same application as ONE dataflow launch (k_ilu0_flow, PNP_ILU_FLOW): the colour launches'
+// 256-row blocks become units in the launches' order (forward colours c_first .. nc-2, the last
+// colour, backward colours nc-2 .. 0); a workgroup takes the next unit by an atomic ticket, waits
+// for the units it reads from (dep_list[dep_ptr[u] .. dep_ptr[u+1]), all earlier in the order) to
+// raise their flags, runs the colour launch's arithmetic on its block, stores its rows write-through
+// and raises its own flag.  flags[0 .. nunits) and the ticket flags[nunits] are zeroed before every
+// launch; abort_word is set when a wait times out (never expected).
+constexpr int kIluFlowMaxStages = 32;
+struct IluFlow {
+  int nstages = 0, nunits = 0;
+  int unit0[kIluFlowMaxStages + 1] = {};  // first unit of each stage
+  int kind[kIluFlowMaxStages] = {};       // kIluFwd 0 / kIluBwd 1 / kIluLast 2
+  int r0[kIluFlowMaxStages] = {}, r1[kIluFlowMaxStages] = {};  // the stage colour's positions
+  int blk0[kIluFlowMaxStages] = {};       // the colour's first block in the staging-list numbering
+  const int *dep_ptr = nullptr, *dep_list = nullptr;
+  unsigned *flags = nullptr;              // [nunits + 1], padded to 16 B
+  unsigned *abort_word = nullptr;
+};
+hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pat, const void *lv,
+                            const void *uv, const double *d, double *v, hipStream_t s, int f32);
 // BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
 // p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
 // r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0.

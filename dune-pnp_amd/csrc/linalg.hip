@@ -1103,6 +1103,233 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   }
 }
 
+// ---- the whole application as one dataflow launch (k_ilu0_flow, kernels.h IluFlow) -------------
+// A colour launch is a short chain of dependent round trips per block whatever it moves (10-16 us
+// at config 3), and the next colour cannot start before the slowest block of this
+// one has finished.  Here each 256-row block of each colour launch is a unit: a workgroup takes the
+// next unit in the launches' order by an atomic ticket, issues everything that does not depend on
+// this application (row metadata, factor values, staging lists, d) at once, waits only for the
+// units whose rows it reads, and runs the LDS kernel's arithmetic on its block.  A block of colour
+// c + 1 can thus start while other blocks of colour c are still running.
+// Progress: a unit waits only on units with smaller tickets, which were claimed by workgroups that
+// are running; the smallest unfinished ticket therefore never waits, whatever the residency.  Every
+// wait is bounded (kIluFlowTimeout) and sets abort_word, so the grid always drains.
+// Visibility (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md § visibility): every store
+// of v in the launch is write-through (buffer_store ... sc1), every storing wave drains it
+// (s_waitcnt vmcnt(0)) before the workgroup barrier, after which one lane stores the unit's flag
+// with an agent-scope atomic; consumers poll flags with relaxed agent-scope loads (sc1) and read
+// v only by sc1 loads, which bypass the per-CU L1 that another CU's stores never refresh.  d and
+// the factors are not written in the launch and are read plainly.
+// Dependencies (host, ctx.cc ilu_flow_build): a forward unit waits for the forward units of the
+// rows in its L staging list; a backward unit for the backward units of the rows in its U list,
+// the forward units of its own rows (their forward values are its `own`), and every forward unit
+// that reads one of its rows (their forward values must be read before it overwrites them).
+constexpr unsigned long long kIluFlowTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double *p) {
+  // range 2^31 - 16 bytes: offsets are 32-bit (vectors of up to 268 M doubles)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, 0x7FFFFFF0, 0x00020000);
+}
+constexpr int kSc1 = 16;  // cache-policy bits of a buffer access: sc1 (write-through / L1 bypass)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <int NF>
+__device__ __forceinline__ void load_nf_sc1(__amdgpu_buffer_rsrc_t r, int j, double (&o)[NF]) {
+  const int off = j * NF * 8;
+  int f = 0;
+#pragma unroll
+  for (; f + 1 < NF; f += 2) {
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, off + 8 * f, 0, kSc1);
+    o[f] = __hiloint2double(int(a.y), int(a.x));
+    o[f + 1] = __hiloint2double(int(a.w), int(a.z));
+  }
+  if (f < NF) {
+    const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * f, 0, kSc1);
+    o[f] = __hiloint2double(int(a.y), int(a.x));
+  }
+}
+template <int NF>
+__device__ __forceinline__ void store_nf_sc1(__amdgpu_buffer_rsrc_t r, int j, const double (&v)[NF]) {
+  const int off = j * NF * 8;
+  int f = 0;
+#pragma unroll
+  for (; f + 1 < NF; f += 2) {
+    u32x4 a;
+    a.x = unsigned(__double2loint(v[f]));
+    a.y = unsigned(__double2hiint(v[f]));
+    a.z = unsigned(__double2loint(v[f + 1]));
+    a.w = unsigned(__double2hiint(v[f + 1]));
+    __builtin_amdgcn_raw_buffer_store_b128(a, r, off + 8 * f, 0, kSc1);
+  }
+  if (f < NF) {
+    u32x2 a;
+    a.x = unsigned(__double2loint(v[f]));
+    a.y = unsigned(__double2hiint(v[f]));
+    __builtin_amdgcn_raw_buffer_store_b64(a, r, off + 8 * f, 0, kSc1);
+  }
+}
+
+// wave 0 of the workgroup waits until every dependency of unit u has raised its flag
+__device__ __forceinline__ void ilu_flow_wait(const IluFlow &F, int u) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const int p0 = F.dep_ptr[u], p1 = F.dep_ptr[u + 1];
+  for (int kb = p0; kb < p1; kb += 64) {
+    const int k = kb + lane;
+    const int w = k < p1 ? F.dep_list[k] : -1;
+    bool ok = w < 0 || __hip_atomic_load(F.flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (__all(ok)) continue;
+    const unsigned long long t0 = wall_clock64();
+    while (true) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!ok)
+        ok = __hip_atomic_load(F.flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      if (__all(ok)) break;
+      const bool late = wall_clock64() - t0 > kIluFlowTimeout;
+      if (late && lane == 0)
+        __hip_atomic_store(F.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (late || __hip_atomic_load(F.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return;  // results are void; the host reports the timeout
+    }
+  }
+}
+
+// one unit = one 256-row block of one colour launch of k_ilu0_solve_lds, the same arithmetic
+template <int NF, int PAT, int KIND, int B, typename VT>
+__device__ __forceinline__ void ilu_flow_unit(const DevLayout &L, const IluFlow &F, int u, int st,
+                                              const VT *__restrict__ lv, const VT *__restrict__ uv,
+                                              const double *__restrict__ d, double *v,
+                                              double *sx) {
+  constexpr int NV = popc9(PAT), NS = slot_vals<NV, VT>();
+  constexpr bool FWD = KIND != kIluBwd;
+  const __amdgpu_buffer_rsrc_t rv = vec_rsrc(v);
+  const int bl = u - F.unit0[st], r0 = F.r0[st], r1 = F.r1[st], blk = F.blk0[st] + bl;
+  const bool live = r0 + bl * kBlock + int(threadIdx.x) < r1;
+  const int pos = live ? r0 + bl * kBlock + int(threadIdx.x) : r0;
+  const int *__restrict__ ptr = FWD ? L.lsx_ptr : L.usx_ptr;
+  const int *__restrict__ lst = FWD ? L.lsx_list : L.usx_list;
+  const int u0 = ptr[blk], u1 = ptr[blk + 1];
+  const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, pos, live);
+  const int row = R.row;
+  double own[NF], Dg[NV];
+  if (FWD) load_nf<NF>(d, size_t(row), own);
+  load_split_vals<NV, 0, VT, KIND == kIluFwd>(R.dg, R.dlane, Dg);
+  const int chunk = pos / kRows;
+  const uint16_t *__restrict__ lix =
+      (FWD ? L.lsx_idx + L.lchunk_off[chunk] : L.usx_idx + L.uchunk_off[chunk]) + R.lane;
+  const int s0 = FWD ? 0 : 1;
+  int li[B];
+  VT ar[B][NS];
+  auto fetch = [&](int sb) {
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int s = sb + b;
+      li[b] = s < R.len ? int(lix[s * kRows]) : 0xFFFF;
+      const VT *sbp = R.vc + size_t(s) * NS * kRows;
+      if (s >= R.len) {
+#pragma unroll
+        for (int qq = 0; qq < NS; qq++) ar[b][qq] = VT(0);
+      } else if constexpr (std::is_same<VT, double>::value) {
+        load_split_vals<NV, 0>(sbp, R.lane, ar[b]);
+      } else if constexpr (NV == 1) {
+        ar[b][0] = sbp[R.lane];
+      } else {
+        load_f32_slot<NV, 0, float>(sbp, R.lane, ar[b]);
+      }
+    }
+  };
+  fetch(s0);
+  const int cnt = u1 - u0;
+  constexpr int kSU = ILU_SU;
+  int jj[kSU];
+#pragma unroll
+  for (int q = 0; q < kSU; q++) {
+    const int k = int(threadIdx.x) + q * kBlock;
+    jj[q] = k < cnt ? lst[u0 + k] : -1;
+  }
+  // the rows this unit reads are final once their units' flags are up
+  ilu_flow_wait(F, u);
+  __syncthreads();
+  if (!FWD) load_nf_sc1<NF>(rv, row, own);
+  {
+    double t[kSU][NF];
+#pragma unroll
+    for (int q = 0; q < kSU; q++)
+      if (jj[q] >= 0) load_nf_sc1<NF>(rv, jj[q], t[q]);
+#pragma unroll
+    for (int q = 0; q < kSU; q++) {
+      const int k = int(threadIdx.x) + q * kBlock;
+      if (jj[q] >= 0)
+#pragma unroll
+        for (int f = 0; f < NF; f++) sx[k * NF + f] = t[q][f];
+    }
+  }
+  for (int k = int(threadIdx.x) + kSU * kBlock; k < cnt; k += kBlock) {
+    double t[NF];
+    load_nf_sc1<NF>(rv, lst[u0 + k], t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
+  }
+  __syncthreads();
+  double acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) acc[f] = 0.0;
+  for (int sb = s0; sb < R.len; sb += B) {
+    if (sb != s0) fetch(sb);
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const bool use = li[b] != 0xFFFF;
+      double vj[NF];
+#pragma unroll
+      for (int g = 0; g < NF; g++) vj[g] = use ? sx[li[b] * NF + g] : 0.0;
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int g = 0; g < NF; g++) {
+          const int qq = pat_index(PAT, f, g);
+          if (qq >= 0)
+            acc[f] = __builtin_fma(-(use ? double(ar[b][qq]) : 0.0), vj[g], acc[f]);
+        }
+    }
+  }
+  if (live) {
+#pragma unroll
+    for (int f = 0; f < NF; f++) acc[f] += own[f];
+    if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
+    if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
+    store_nf_sc1<NF>(rv, row, acc);
+  }
+  // publish: every storing wave drains its write-through stores, then one lane raises the flag
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(F.flags + u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NF, int PAT, int B, typename VT>
+__global__ __launch_bounds__(kBlock) void k_ilu0_flow(DevLayout L, IluFlow F,
+                                                      const VT *__restrict__ lv,
+                                                      const VT *__restrict__ uv,
+                                                      const double *__restrict__ d, double *v) {
+  extern __shared__ double smem[];  // [0, 2): the ticket; [2, ..): staged records
+  int *tk = reinterpret_cast<int *>(smem);
+  if (threadIdx.x == 0)
+    tk[0] = int(__hip_atomic_fetch_add(F.flags + F.nunits, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  const int u = tk[0];
+  if (u >= F.nunits) return;  // uniform (never: the grid is the unit count)
+  int st = 0;
+  while (st + 1 < F.nstages && u >= F.unit0[st + 1]) st++;
+  const int kind = F.kind[st];
+  if (kind == kIluFwd)
+    ilu_flow_unit<NF, PAT, kIluFwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+  else if (kind == kIluLast)
+    ilu_flow_unit<NF, PAT, kIluLast, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+  else
+    ilu_flow_unit<NF, PAT, kIluBwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+}
+
 // split storage position p takes the block (row, slot) = (src >> 6, src & 63) of the full SELL:
 // FROMK: expanded and masked from the k-form matrix, else copied from the NV-form ILU factors;
 // padding (src < 0) gets zeros
@@ -1916,6 +2143,31 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
       go(std::integral_constant<int, kIluLast>(), nc - 1);
       for (int c = nc - 2; c >= 0; c--) go(std::integral_constant<int, kIluBwd>(), c);
     }));
+    return hipGetLastError();
+  };
+  return f32 ? run(float()) : run(double());
+}
+
+hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pat, const void *lvp,
+                            const void *uvp, const double *d, double *v, hipStream_t s, int f32) {
+  if (F.nunits <= 0) return hipSuccess;
+  if (!L.lsx_ptr || F.nstages > kIluFlowMaxStages) return hipErrorInvalidValue;
+  // flags and the ticket, one block from the allocation's start, a multiple of 16 bytes
+  hipError_t e = hipMemsetAsync(F.flags, 0, (size_t(F.nunits + 1) * 4 + 15) & ~size_t(15), s);
+  if (e != hipSuccess) return e;
+  const size_t lds = 16 + size_t(L.sx_max) * nf * sizeof(double);
+  const int kBsel = ilu_lds_bsel() ? ilu_lds_bsel() : (L.n_owned > 1500000 ? 3 : 2);
+  auto run = [&](auto vt) -> hipError_t {
+    using VT = decltype(vt);
+    const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
+    PNP_PAT_DISPATCH(nf, pat, {
+      if (kBsel == 3)
+        hipLaunchKernelGGL((k_ilu0_flow<NFc, PATc, 3, VT>), dim3(F.nunits), dim3(kBlock), lds, s,
+                           L, F, lv, uv, d, v);
+      else
+        hipLaunchKernelGGL((k_ilu0_flow<NFc, PATc, 2, VT>), dim3(F.nunits), dim3(kBlock), lds, s,
+                           L, F, lv, uv, d, v);
+    });
     return hipGetLastError();
   };
   return f32 ? run(float()) : run(double());

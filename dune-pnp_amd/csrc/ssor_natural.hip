@@ -106,6 +106,9 @@ __global__ void __launch_bounds__(kB)
 // waiting and takes NaN operands, so the grid always drains.
 // The arithmetic is the level kernel's: same products, same shuffle-ordered subtraction, the
 // forward result 0.0 + 1.0 * (rhs / a_RR), the backward one v_R + 1.0 * (rhs / a_RR).
+#ifndef NAT_POLL_ONE
+#define NAT_POLL_ONE 1  // build-flag A/B knob: 0 = every lane re-reads its pending operands
+#endif
 constexpr unsigned long long kNatPending = ~0ull;
 constexpr unsigned long long kNatTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
 
@@ -157,18 +160,37 @@ __global__ void __launch_bounds__(kB)
         const unsigned long long t0 = wall_clock64();
         while (true) {
           __builtin_amdgcn_s_sleep(1);
-          pend = false;
+          // NAT_POLL_ONE: only the first lane with a pending operand re-reads its pending operands
+          // until they have all arrived, then every lane re-reads once: a waiting wave issues one
+          // lane's loads per pass instead of up to 64 x kS, so the pollers do not fill the memory
+          // queues the producers' stores and loads wait in (the hop latency sits in the consumer
+          // CU's queue, MI355X_MICROARCH.md price list, handoff-1to1)
+          const bool poll = NAT_POLL_ONE ? lane == __ffsll((unsigned long long)__ballot(pend)) - 1
+                                         : true;
+          if (poll) {
+            pend = false;
 #pragma unroll
-          for (int q = 0; q < kS; q++)
-            if (b[q] == kNatPending) {
-              b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
-              pend |= b[q] == kNatPending;
-            }
+            for (int q = 0; q < kS; q++)
+              if (b[q] == kNatPending) {
+                b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+                pend |= b[q] == kNatPending;
+              }
+          }
+          if (NAT_POLL_ONE && !__any(poll && pend)) {  // the polled lane is complete: sweep all
+            pend = false;
+#pragma unroll
+            for (int q = 0; q < kS; q++)
+              if (b[q] == kNatPending) {
+                b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+                pend |= b[q] == kNatPending;
+              }
+          }
           if (!__any(pend)) break;
           const bool late = wall_clock64() - t0 > kNatTimeout;
           if (late && lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-          if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          if (late || (NAT_POLL_ONE ? false : __hip_atomic_load(abort_word, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT))) {
 #pragma unroll
             for (int q = 0; q < kS; q++)
               if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;  // NaN: drain the grid

@@ -34,7 +34,7 @@ OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSO
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG, PREC_SSOR_NATURAL = range(6)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
 (OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD, OPT_BICG_TWORED, OPT_AMG_FALLBACK,
- OPT_GRAPH, OPT_SEQ_ORDER) = 1, 2, 3, 4, 5, 6, 7
+ OPT_GRAPH, OPT_SEQ_ORDER, OPT_ILU_FLOW) = 1, 2, 3, 4, 5, 6, 7, 8
 DEVICE_PTRS, JAC_FD = 1, 2
 CREATE_ABSORB_THIN_COLOR = 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,

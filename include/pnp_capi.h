@@ -369,7 +369,13 @@ enum {
    * the reference program's even where BiCGSTAB is chaotic in the last bits.  A parity mode, far
    * slower than the default.  Preconditioners NONE, JACOBI, SSOR_NATURAL; P1 contexts of one rank;
    * pnp_op_args.c_extra unsupported.  0 (default): the GPU's own summation orders. */
-  PNP_OPT_SEQ_ORDER = 7
+  PNP_OPT_SEQ_ORDER = 7,
+  /* 1: each ILU(0) application (PNP_PREC_ILU0) is ONE dataflow launch instead of one launch per
+   * colour and sweep direction: every 256-row block of every colour launch is a unit taken in the
+   * launches' order by an atomic ticket, and a unit waits only for the units whose rows it reads
+   * (linalg.hip k_ilu0_flow).  The same arithmetic per row, so the same results bit for bit.
+   * 0: the colour launches (the environment variable PNP_ILU_FLOW=0/1 sets the default). */
+  PNP_OPT_ILU_FLOW = 8
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 

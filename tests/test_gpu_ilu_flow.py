@@ -1,0 +1,108 @@
+"""One-launch ILU(0) application (PNP_OPT_ILU_FLOW, linalg.hip k_ilu0_flow), -m gpu: the dataflow
+launch runs the colour launches' arithmetic per row, so every result must be BITWISE the colour
+launches' -- single applications (both factor precisions, from colour 0 and, inside BiCGSTAB, from
+colour 1), BiCGSTAB solutions and counts (eager and graph-replayed), partitioned ranks, and on the
+full config-3 system (2.2 M DOF: ~5,000 units per launch, the size where the hand-offs run under
+load, each consumer's L1 warm with lines that other units rewrite during the launch)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import pnp_amd as P
+from conftest import DATA
+from test_gpu import golden
+from test_gpu_multirank import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def h(a):
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _both(ctx, fn):
+    out = []
+    for flow in (0, 1):
+        ctx.set_option(P.OPT_ILU_FLOW, flow)
+        out.append(fn())
+    ctx.set_option(P.OPT_ILU_FLOW, 0)
+    return out
+
+
+@pytest.mark.parametrize("name", ["pore_small_k0", "cylinder_k0", "pore_pnp_k0"])
+def test_flow_apply_and_solve_bitwise(name):
+    z, mesh, par, orc = golden(name)
+    x = z["newton_pnp_x0"] if "newton_pnp_x0" in z else z["pnp_x"]
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    ctx.jacobian(x, export=False)
+    rhs = ctx.residual(x)
+    for f32 in (1, 0):
+        ctx.set_option(P.OPT_ILU_F32, f32)
+        a, b = _both(ctx, lambda: h(ctx.prec_apply(rhs, P.PREC_ILU0)))
+        assert a == b, f"apply f32={f32}"
+        for graph in (0, 1):
+            ctx.set_option(P.OPT_GRAPH, graph)
+
+            def solve():
+                sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=1e-10, maxit=20000)
+                return h(sol), res["iterations"], res["it_half"]
+            a, b = _both(ctx, solve)
+            assert a == b, f"solve f32={f32} graph={graph}: {a} vs {b}"
+    ctx.close()
+
+
+def test_flow_pb_scalar_newton_bitwise():
+    z, mesh, par, orc = golden("pore_small_k0")
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PB)
+    a, b = _both(ctx, lambda: (lambda u, r: (h(u), r["linear_iterations"]))(
+        *ctx.newton(np.zeros(mesh.nv), prec=P.PREC_ILU0)))
+    assert a == b
+    ctx.close()
+
+
+def test_flow_partitioned_ranks_bitwise():
+    z, mesh, par, orc = golden("pore_small_k0")
+    x = z["newton_pnp_x0"]
+
+    def fn(c, r):
+        c.set_operator(P.OP_PNP)
+        c.jacobian(x, export=False)
+        b = c.sync_vector(c.residual(x))
+        out = []
+        for flow in (0, 1):
+            c.set_option(P.OPT_ILU_FLOW, flow)
+            sol, res = c.linear_solve(b, prec=P.PREC_ILU0, reduction=1e-10, maxit=20000)
+            out.append((h(c.sync_vector(sol)), res["iterations"]))
+        return out
+    outs = run_ranks(3, mesh, par, fn)
+    for o in outs:
+        assert o[0] == o[1]
+
+
+def test_flow_config3_bitwise():
+    """The bench's system: 2.2 M DOF at the Boltzmann state's neighbourhood (random state of the
+    full-size parity test), fixed BiCGSTAB iterations, flow on and off: identical iterates."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp/pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(4)
+    par = P.Params.from_config(cfg)
+    rng = np.random.default_rng(20261015)
+    nv = mesh.nv
+    x = np.concatenate([rng.uniform(-1, 1, nv), 0.06 * rng.uniform(0.5, 1.5, nv),
+                        0.06 * rng.uniform(0.5, 1.5, nv)])
+    ctx = P.Context(mesh, par)
+    ctx.set_operator(P.OP_PNP)
+    ctx.jacobian(x, export=False)
+    rhs = ctx.residual(x)
+
+    def run():
+        outs = [h(ctx.prec_apply(rhs, P.PREC_ILU0))]
+        sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=1e-12, maxit=60)
+        outs += [h(sol), res["it_half"]]
+        return outs
+    a, b = _both(ctx, run)
+    assert a == b
+    ctx.close()
