@@ -46,22 +46,54 @@ import pnp_amd as P  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured copy rate is in
 #                       the line (`measured_copy_gbs`)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "pmc_summary.json")
 SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
+
+
+def pmc_summary():
+    """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py), or None."""
+    for path in (PMC_SUMMARY, PMC_SUMMARY.replace("r04", "r03"), PMC_SUMMARY.replace("r04", "r02")):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            d["path"] = os.path.relpath(path, ROOT)
+            return d
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def pmc_traffic(kernel_prefix):
     """Per-launch HBM-side bytes of a kernel from the committed rocprofv3 PMC summary, or None."""
-    try:
-        with open(PMC_SUMMARY if os.path.exists(PMC_SUMMARY)
-                  else PMC_SUMMARY.replace("r03", "r02")) as f:
-            ks = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
+    d = pmc_summary()
+    if not d:
         return None
-    for name, v in ks.items():
+    for name, v in d["kernels"].items():
         if kernel_prefix in name:
             return v["traffic_bytes"]
     return None
+
+
+BLAS_KERNELS = ("k_update_fwd0", "k_update_xr", "k_update_p", "k_reduce")
+
+
+def pmc_blas_bytes():
+    """HBM-side bytes per BiCGSTAB iteration of the vector-update and reduction kernels (the
+    device timers' `blas` class), from the committed PMC summary: per kernel its mean bytes per
+    launch x its launches per iteration (the summary records the iterations its run made), FETCH_SIZE
+    x 2 as calibrated in profiles/r04/calib (every access width the hot path uses).  None when no
+    summary records its iteration count."""
+    d = pmc_summary()
+    if not d or not d.get("bicgstab_iterations"):
+        return None
+    it = d["bicgstab_iterations"]
+    tot, parts = 0.0, {}
+    for name, v in d["kernels"].items():
+        if any(k in name for k in BLAS_KERNELS):
+            b = v["traffic_bytes"] * v["launches_fetch"] / it
+            parts[name.split("(")[0].replace("void pnp::(anonymous namespace)::", "")] = b
+            tot += b
+    return {"bytes": tot, "per_kernel": parts, "source": d["path"]}
 
 
 def tile_mesh(mesh, n):
@@ -243,9 +275,14 @@ def byte_models(info, nf, N_local, T_local, prec):
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
     if info["ilu_f32"] and info["nvb"] == 7:
         ilu -= 16 * V  # the forward steps read only the 12-B lower tail of each diagonal block
-    blas = 192 * N_local  # ~24 vector passes per iteration (the contract's figure)
+    pb = pmc_blas_bytes()
+    # the update kernels' counted bytes (PMC); ~24 vector passes (the contract's 192 N) only when
+    # no committed summary has them
+    blas = pb["bytes"] if pb else 192 * N_local
     return {"asm": B_asm, "it_contract": B_it, "spmv_stored": spmv, "ilu_stored": ilu,
-            "blas": blas, "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}
+            "blas": blas, "blas_source": (f"PMC: {pb['source']}" if pb else "model: 192 N"),
+            "blas_per_kernel": pb["per_kernel"] if pb else None,
+            "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}
 
 
 def make_context(mesh, cfg, rank, world, local, dist):
@@ -360,7 +397,8 @@ def measure(ctx, mesh, args, prec, dist, world):
         "it_contract": rl(B["it_contract"], it_ev), "it_stored": rl(B["it_stored"], it_ev),
         "spmv_stored": rl(B["spmv_stored"], spmv_s),
         "ilu_stored": rl(B["ilu_stored"], prec_s) if prec != P.PREC_NONE else None,
-        "blas": rl(B["blas"], blas_s),
+        "blas": dict(rl(B["blas"], blas_s), source=B["blas_source"],
+                     per_kernel_bytes=B["blas_per_kernel"]),
     }
 
 
@@ -644,8 +682,9 @@ def main():
                                         "bytes, not counted HBM bytes",
                          "hbm_gbs_from_traffic": (traffic / aw["seconds"] / 1e9) if traffic
                                                  else None,
-                         "traffic_source": "profiles/r03/pmc_summary.json (rocprofv3 FETCH_SIZE x2 "
-                                           "+ WRITE_SIZE per launch, separate passes)",
+                         "traffic_source": ((pmc_summary() or {}).get("path", "none") +
+                                            " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                                            "separate passes; x2 calibrated in profiles/r04/calib)"),
                          "kernel": "k_assemble_ga<OP_PNP,1> (gather-all fan walk)",
                          "bytes_per_launch": aw["bytes"], "avg_launch_us": aw["seconds"] * 1e6,
                          "timing": "one HIP event pair on the library stream around K back-to-"

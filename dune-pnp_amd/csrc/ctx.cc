@@ -212,7 +212,7 @@ struct pnp_ctx {
   // the one-launch dataflow sweep (launch_ssor_natural_flow): units, forward units first
   std::vector<int4> nat_units;
   DBuf<int4> d_nat_units;
-  int nat_units_f = 0;
+  int nat_units_f = 0, nat_tail_f = 0, nat_tail_b = 0;
   bool nat_units_ok = false;
   DBuf<unsigned> nat_abort;  // [0]: set by a sweep whose operand wait timed out (sticky)
   DBuf<int> csr_diag;        // index of each CSR-view row's diagonal entry
@@ -822,22 +822,35 @@ struct pnp_ctx {
           }
         }
       }
-      // dataflow units for the one-launch sweep: up to kNatUnit consecutive rows of one level,
+      // dataflow units for the one-launch sweep: up to ssor_natural_unit_rows() consecutive rows of one level,
       // {first sweep position, rows | width << 8, the level's row count, ELL index of the unit's
-      // first row}; forward units in level order, then backward units in level order
+      // first row}; forward units in level order, then backward units in level order.  The
+      // sweep's tail -- the levels from the last one wider than PNP_NAT_TAIL rows to its end --
+      // can run in one workgroup (ssor_natural.hip); default 0 (no tail): one CU is slower
+      // (PNP config 3: 2.36 ms per application without, 3.29 / 4.83 ms with 512 / 1024-row tails,
+      // profiles/r04/ssor_natural_tail_r4e.log)
+      static const int tail_rows = [] {
+        const char *ev = std::getenv("PNP_NAT_TAIL");
+        return ev ? std::max(0, std::atoi(ev)) : 0;
+      }();
+      int ltail = nlev;
+      while (tail_rows > 0 && ltail > 0 && lptr[ltail] - lptr[ltail - 1] <= tail_rows) ltail--;
       for (int l = 0; l < nlev && nat_units_ok; l++) {
+        if (l == ltail) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
         const int nl = lptr[l + 1] - lptr[l];
         const long long w = nl > 0 ? (W.eoff[l + 1] - W.eoff[l]) / nl : 0;
-        for (int t0 = lptr[l]; t0 < lptr[l + 1]; t0 += pnp::kNatUnit) {
+        const int urows = pnp::ssor_natural_unit_rows();
+        for (int t0 = lptr[l]; t0 < lptr[l + 1]; t0 += urows) {
           const long long e0 = W.eoff[l] + (t0 - lptr[l]);
           if (w > 255 || W.eoff[l + 1] > INT32_MAX) {
             nat_units_ok = false;
             break;
           }
-          const int rows = std::min(pnp::kNatUnit, lptr[l + 1] - t0);
+          const int rows = std::min(urows, lptr[l + 1] - t0);
           nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), nl, int(e0)));
         }
       }
+      if (ltail >= nlev) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
       if (fwd) nat_units_f = int(nat_units.size());
       int rc2;
       if ((rc2 = upv(W.info, info, "natural SSOR rows")) ||
@@ -895,6 +908,8 @@ struct pnp_ctx {
     F.units = d_nat_units.p;
     F.nunits = int(nat_units.size());
     F.nunits_f = nat_units_f;
+    F.tail_f = nat_tail_f;
+    F.tail_b = nat_tail_b;
     F.fwd = nat_f.view();
     F.bwd = nat_b.view();
     F.abort_word = nat_abort.p;
@@ -1042,10 +1057,17 @@ struct pnp_ctx {
   // v = ILU(0)^-1 d over the owned rows, colours from c_first (launch_ilu0_apply's contract): one
   // dataflow launch when PNP_OPT_ILU_FLOW is on and d and v are distinct, else the colour launches
   int ilu_apply(const double *d, double *vout, int c_first, const char *what) {
-    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1)) {
+    // the resident-grid form needs the device to itself: not with in-process ranks sharing it
+    // (and one context per GPU at N > 1); PNP_ILU_FLOW_TICKET=1: the ticketed form (any residency)
+    static const int ticket = [] {
+      const char *ev = std::getenv("PNP_ILU_FLOW_TICKET");
+      return ev && std::atoi(ev) != 0 ? 1 : 0;
+    }();
+    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (ticket || !dist)) {
       IluFlowDev &D = ilu_flow[c_first];
       int rc;
       if (!D.built && (rc = ilu_flow_build(c_first, D))) return rc;
+      D.F.persistent = ticket ? 0 : 1;
       if (D.ok) {
         hipError_t e = pnp::launch_ilu0_flow(dl, D.F, nf, pat, lvals.p, uvals.p, d, vout, stream,
                                              f32_now());

@@ -356,6 +356,7 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int 
 constexpr int kIluFlowMaxStages = 32;
 struct IluFlow {
   int nstages = 0, nunits = 0;
+  int persistent = 1;  // 1: a resident grid takes units b, b + G, ...; 0: one ticketed WG per unit
   int unit0[kIluFlowMaxStages + 1] = {};  // first unit of each stage
   int kind[kIluFlowMaxStages] = {};       // kIluFwd 0 / kIluBwd 1 / kIluLast 2
   int r0[kIluFlowMaxStages] = {}, r1[kIluFlowMaxStages] = {};  // the stage colour's positions
@@ -451,16 +452,20 @@ struct NatSweep {
 };
 hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
                                const double *d, double *v, hipStream_t s);
-// The same two sweeps as ONE launch (dataflow): units of up to kNatUnit rows of one level, int4
+// The same two sweeps as ONE launch (dataflow): units of up to ssor_natural_unit_rows() rows of one level, int4
 // {first sweep position, rows | width << 8 | backward << 16, the level's row count, ELL index of
 // the unit's first row}, forward units (nunits_f) then backward ones, each in level order.  An
 // operand code in ecol (both forms): c >= 0 the forward value of row c, c == -1 zero, c <= -2 the
 // backward value of row -(c + 2).  vf / vb (n each): forward / backward results; abort_word[0]
 // is set when an operand wait times out.
-constexpr int kNatUnit = 8;
+// rows per unit = rows per wavefront of the flow kernel (64 / its lanes per row)
+int ssor_natural_unit_rows();
 struct NatFlow {
   const int4 *units = nullptr;
   int nunits = 0, nunits_f = 0;
+  // first unit of each sweep's narrow tail (levels of at most PNP_NAT_TAIL rows to the sweep's
+  // end), run by one workgroup: forward [tail_f, nunits_f), backward [tail_b, nunits)
+  int tail_f = 0, tail_b = 0;
   NatSweep fwd, bwd;
   unsigned *abort_word = nullptr;
 };

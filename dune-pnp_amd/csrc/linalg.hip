@@ -1311,7 +1311,27 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_flow(DevLayout L, IluFlow F,
                                                       const VT *__restrict__ lv,
                                                       const VT *__restrict__ uv,
                                                       const double *__restrict__ d, double *v) {
-  extern __shared__ double smem[];  // [0, 2): the ticket; [2, ..): staged records
+  extern __shared__ double smem[];  // [0, 2): reserved (16-B aligned staging); [2, ..): records
+  if (F.persistent) {
+    // resident grid (sized from the occupancy query): workgroup b takes units b, b + G, ... in
+    // order.  The smallest unfinished unit's workgroup has finished its own earlier units, so it
+    // runs that unit, whose dependencies are all finished: progress needs every workgroup of the
+    // grid resident, which a single-stream context gives it
+    int st = 0;
+    for (int u = blockIdx.x; u < F.nunits; u += gridDim.x) {
+      while (st + 1 < F.nstages && u >= F.unit0[st + 1]) st++;
+      const int kind = F.kind[st];
+      if (kind == kIluFwd)
+        ilu_flow_unit<NF, PAT, kIluFwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+      else if (kind == kIluLast)
+        ilu_flow_unit<NF, PAT, kIluLast, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+      else
+        ilu_flow_unit<NF, PAT, kIluBwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
+    }
+    return;
+  }
+  // one workgroup per unit, the unit taken by an atomic ticket (no residency assumption: lower
+  // tickets belong to running workgroups); one ticket word serialises ~5,000 dequeues per launch
   int *tk = reinterpret_cast<int *>(smem);
   if (threadIdx.x == 0)
     tk[0] = int(__hip_atomic_fetch_add(F.flags + F.nunits, 1u, __ATOMIC_RELAXED,
@@ -2148,6 +2168,16 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
   return f32 ? run(float()) : run(double());
 }
 
+// every workgroup of a grid resident at once: CUs x the occupancy at this LDS size (capped by n)
+template <typename K>
+static int resident_grid(K kern, size_t lds, int n) {
+  int dev = 0, cus = 0, per = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBlock, lds);
+  return std::min(n, std::max(1, cus * std::max(1, per)));
+}
+
 hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pat, const void *lvp,
                             const void *uvp, const double *d, double *v, hipStream_t s, int f32) {
   if (F.nunits <= 0) return hipSuccess;
@@ -2160,13 +2190,15 @@ hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pa
   auto run = [&](auto vt) -> hipError_t {
     using VT = decltype(vt);
     const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
+    auto go = [&](auto kern) {
+      const int grid = F.persistent ? resident_grid(kern, lds, F.nunits) : F.nunits;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, L, F, lv, uv, d, v);
+    };
     PNP_PAT_DISPATCH(nf, pat, {
       if (kBsel == 3)
-        hipLaunchKernelGGL((k_ilu0_flow<NFc, PATc, 3, VT>), dim3(F.nunits), dim3(kBlock), lds, s,
-                           L, F, lv, uv, d, v);
+        go(k_ilu0_flow<NFc, PATc, 3, VT>);
       else
-        hipLaunchKernelGGL((k_ilu0_flow<NFc, PATc, 2, VT>), dim3(F.nunits), dim3(kBlock), lds, s,
-                           L, F, lv, uv, d, v);
+        go(k_ilu0_flow<NFc, PATc, 2, VT>);
     });
     return hipGetLastError();
   };

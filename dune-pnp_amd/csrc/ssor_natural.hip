@@ -106,26 +106,35 @@ __global__ void __launch_bounds__(kB)
 // waiting and takes NaN operands, so the grid always drains.
 // The arithmetic is the level kernel's: same products, same shuffle-ordered subtraction, the
 // forward result 0.0 + 1.0 * (rhs / a_RR), the backward one v_R + 1.0 * (rhs / a_RR).
-#ifndef NAT_POLL_ONE
-#define NAT_POLL_ONE 1  // build-flag A/B knob: 0 = every lane re-reads its pending operands
-#endif
 constexpr unsigned long long kNatPending = ~0ull;
 constexpr unsigned long long kNatTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
 
+// The sweeps' tails (PNP_NAT_TAIL, off by default): the natural order's dependency graph is wide
+// for its first levels and then narrow for as many again (pore_pnp k=4, PNP: 171 levels holding
+// 2.14 M rows, then 177 levels of 78 K rows; PB: 63 levels of 676 K rows, then 206 of 62 K).
+// Across CUs each hop costs a write-through store and a poll served from the memory side (~2.5 us
+// per level, measured); the tail units can instead run in ONE workgroup of 16 waves on one CU,
+// polling each other through that CU's caches (workgroup-scope atomics).  Measured slower: one CU
+// works through a tail level's ~55 units 16 at a time, each with its own load latency (PNP
+// config 3: 2.36 ms per application without a tail, 3.29 / 4.83 ms with 512 / 1024-row tails;
+// profiles/r04/ssor_natural_tail_r4e.log).  Launch order: forward head (the resident grid),
+// forward tail (one workgroup), backward head, backward tail.
+template <int SCOPE>
 __device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, SCOPE);
 }
 
-__global__ void __launch_bounds__(kB)
-    k_ssor_nat_flow(const int4 *__restrict__ units, int nunits, int nunits_f,
+template <int BLK, int SCOPE>
+__global__ void __launch_bounds__(BLK)
+    k_ssor_nat_flow(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
                     const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
                     const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
                     const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
                     const double *__restrict__ val, const double *__restrict__ d,
                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
   const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
-  const int G = gridDim.x * (kB / 64);
-  for (int u = blockIdx.x * (kB / 64) + threadIdx.x / 64; u < nunits; u += G) {
+  const int G = gridDim.x * (BLK / 64);
+  for (int u = u0 + blockIdx.x * (BLK / 64) + threadIdx.x / 64; u < u1; u += G) {
     const int4 U = units[u];
     const bool bwd = u >= nunits_f;  // uniform
     const int rows = U.y & 255, width = (U.y >> 8) & 255;
@@ -151,7 +160,7 @@ __global__ void __launch_bounds__(kB)
 #pragma unroll
       for (int q = 0; q < kS; q++) {
         a[q] = ix[q] >= 0 ? val[ix[q]] : 0.0;
-        b[q] = c[q] == -1 ? 0ull : nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+        b[q] = c[q] == -1 ? 0ull : nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
       }
       bool pend = false;
 #pragma unroll
@@ -160,37 +169,18 @@ __global__ void __launch_bounds__(kB)
         const unsigned long long t0 = wall_clock64();
         while (true) {
           __builtin_amdgcn_s_sleep(1);
-          // NAT_POLL_ONE: only the first lane with a pending operand re-reads its pending operands
-          // until they have all arrived, then every lane re-reads once: a waiting wave issues one
-          // lane's loads per pass instead of up to 64 x kS, so the pollers do not fill the memory
-          // queues the producers' stores and loads wait in (the hop latency sits in the consumer
-          // CU's queue, MI355X_MICROARCH.md price list, handoff-1to1)
-          const bool poll = NAT_POLL_ONE ? lane == __ffsll((unsigned long long)__ballot(pend)) - 1
-                                         : true;
-          if (poll) {
-            pend = false;
+          pend = false;
 #pragma unroll
-            for (int q = 0; q < kS; q++)
-              if (b[q] == kNatPending) {
-                b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
-                pend |= b[q] == kNatPending;
-              }
-          }
-          if (NAT_POLL_ONE && !__any(poll && pend)) {  // the polled lane is complete: sweep all
-            pend = false;
-#pragma unroll
-            for (int q = 0; q < kS; q++)
-              if (b[q] == kNatPending) {
-                b[q] = nat_ld(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
-                pend |= b[q] == kNatPending;
-              }
-          }
+          for (int q = 0; q < kS; q++)
+            if (b[q] == kNatPending) {
+              b[q] = nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+              pend |= b[q] == kNatPending;
+            }
           if (!__any(pend)) break;
           const bool late = wall_clock64() - t0 > kNatTimeout;
           if (late && lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-          if (late || (NAT_POLL_ONE ? false : __hip_atomic_load(abort_word, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+          if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
             for (int q = 0; q < kS; q++)
               if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;  // NaN: drain the grid
@@ -212,19 +202,21 @@ __global__ void __launch_bounds__(kB)
       double own = 0.0;
       if (bwd) {
         unsigned long long w;
-        while ((w = nat_ld(vf + I.x)) == kNatPending &&
+        while ((w = nat_ld<SCOPE>(vf + I.x)) == kNatPending &&
                !__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         }
         own = __longlong_as_double(w);
       }
       const double out = own + 1.0 * (rhs / val[I.z]);
       __hip_atomic_store(bwd ? vb + I.x : vf + I.x,
-                         (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+                         (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED, SCOPE);
     }
   }
 }
+constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
 }  // namespace
+
+int ssor_natural_unit_rows() { return 64 / kL; }
 
 hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
                                     double *vf, double *vb, hipStream_t s) {
@@ -232,7 +224,8 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     int dev = 0, cus = 0, per = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_flow, kB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>,
+                                                 kB, 0);
     const char *ev = std::getenv("PNP_NAT_FLOW_WG_PER_CU");  // A/B knob, capped at the occupancy
     if (ev && std::atoi(ev) > 0) per = std::min(per, std::atoi(ev));
     return std::max(1, cus * std::max(1, per));
@@ -240,12 +233,24 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
   hipError_t e = hipMemsetAsync(vf, 0xFF, sizeof(double) * size_t(n), s);
   if (e == hipSuccess) e = hipMemsetAsync(vb, 0xFF, sizeof(double) * size_t(n), s);
   if (e != hipSuccess) return e;
-  const int blocks = std::min(grid, (F.nunits + kB / 64 - 1) / (kB / 64));
-  if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ssor_nat_flow, dim3(blocks), dim3(kB), 0, s, F.units, F.nunits, F.nunits_f,
-                     F.fwd.info, F.fwd.ecol, F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val,
-                     d, reinterpret_cast<unsigned long long *>(vf),
-                     reinterpret_cast<unsigned long long *>(vb), F.abort_word);
+  auto vfu = reinterpret_cast<unsigned long long *>(vf);
+  auto vbu = reinterpret_cast<unsigned long long *>(vb);
+  // [u0, u1) of one sweep: head units on the resident grid, tail units in one workgroup
+  auto sweep = [&](int u0, int ut, int u1) {
+    if (ut > u0) {
+      const int blocks = std::min(grid, (ut - u0 + kB / 64 - 1) / (kB / 64));
+      hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB), 0,
+                         s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
+                         F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+    }
+    if (u1 > ut)
+      hipLaunchKernelGGL((k_ssor_nat_flow<kTailBlk, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3(1),
+                         dim3(kTailBlk), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,
+                         F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
+                         F.abort_word);
+  };
+  sweep(0, F.tail_f, F.nunits_f);
+  sweep(F.nunits_f, F.tail_b, F.nunits);
   return hipGetLastError();
 }
 

@@ -2,7 +2,8 @@
 into per-kernel per-launch HBM-side bytes, with the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per 128-B request,
 so it is doubled; WRITE_SIZE is taken as is.  FETCH_SIZE is in KB (rocprofv3 derived metric).
-usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv> <out.json>"""
+usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv> <out.json>
+       [bicgstab iterations of the profiled run (bench.py's per-iteration BLAS bytes)]"""
 import collections
 import csv
 import json
@@ -23,7 +24,8 @@ w, nw = per_kernel(sys.argv[2], "WRITE_SIZE")
 out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes with "
                  "--kernel-trace (tools/gpu_run.sh pmcf/pmcw on tools/prof_target.py, config 3, "
                  "ILU0); FETCH_SIZE x2 (gfx950 correction), both KB -> bytes x1024",
-       "kernels": {}}
+       "kernels": {},
+       "bicgstab_iterations": int(sys.argv[4]) if len(sys.argv) > 4 else None}
 for k in sorted(set(f) | set(w)):
     fb = 2 * 1024 * f.get(k, 0.0)
     wb = 1024 * w.get(k, 0.0)
