@@ -106,6 +106,9 @@ __global__ void __launch_bounds__(kB)
 // waiting and takes NaN operands, so the grid always drains.
 // The arithmetic is the level kernel's: same products, same shuffle-ordered subtraction, the
 // forward result 0.0 + 1.0 * (rhs / a_RR), the backward one v_R + 1.0 * (rhs / a_RR).
+#ifndef NAT_POLL_DEPTH
+#define NAT_POLL_DEPTH 1  // build-flag A/B knob: polls in flight per pending operand
+#endif
 constexpr unsigned long long kNatPending = ~0ull;
 constexpr unsigned long long kNatTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
 
@@ -167,15 +170,50 @@ __global__ void __launch_bounds__(BLK)
       for (int q = 0; q < kS; q++) pend |= b[q] == kNatPending;
       if (__any(pend)) {
         const unsigned long long t0 = wall_clock64();
+        // NAT_POLL_DEPTH polls in flight per pending operand: a new poll is issued every pass and
+        // the oldest one consumed, so an arriving value is seen about one round trip after it
+        // lands instead of up to two (depth 1: issue, wait, check)
+        constexpr int PD = NAT_POLL_DEPTH;
+        unsigned long long fl[PD > 1 ? PD - 1 : 1][kS];
+#pragma unroll
+        for (int p = 0; p + 1 < PD; p++) {
+#pragma unroll
+          for (int q = 0; q < kS; q++)
+            fl[p][q] = b[q] == kNatPending
+                           ? nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)))
+                           : 0ull;
+          __builtin_amdgcn_s_sleep(1);
+        }
         while (true) {
           __builtin_amdgcn_s_sleep(1);
           pend = false;
+          if constexpr (PD > 1) {
+            unsigned long long nw[kS];
 #pragma unroll
-          for (int q = 0; q < kS; q++)
-            if (b[q] == kNatPending) {
-              b[q] = nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
-              pend |= b[q] == kNatPending;
-            }
+            for (int q = 0; q < kS; q++)
+              nw[q] = b[q] == kNatPending
+                          ? nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)))
+                          : 0ull;
+#pragma unroll
+            for (int q = 0; q < kS; q++)
+              if (b[q] == kNatPending) {
+                b[q] = fl[0][q];
+                pend |= b[q] == kNatPending;
+              }
+#pragma unroll
+            for (int p = 0; p + 2 < PD; p++)
+#pragma unroll
+              for (int q = 0; q < kS; q++) fl[p][q] = fl[p + 1][q];
+#pragma unroll
+            for (int q = 0; q < kS; q++) fl[PD - 2][q] = nw[q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < kS; q++)
+              if (b[q] == kNatPending) {
+                b[q] = nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+                pend |= b[q] == kNatPending;
+              }
+          }
           if (!__any(pend)) break;
           const bool late = wall_clock64() - t0 > kNatTimeout;
           if (late && lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED,

@@ -15,6 +15,9 @@
 //                  PNP_PREC_SSOR_NATURAL; bcgs_ssork_mc: the multicolour sweep, same method, other order)
 //                 [--degree k]   (md / pb modes: PDEGREE, src/instationary_pnp_from_pb_md.hh:26-28;
 //                                 the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111)
+//                 [--reference-order]  (--reference-solvers with PNP_OPT_SEQ_ORDER: the reference's
+//                                 sequential arithmetic, so every Newton step's BiCGSTAB count is its
+//                                 single-rank program's; Newton prints its per-step lines)
 //                 [--reference-solvers]  (stationary / pb / instationary: the reference's own
 //                                 choices, src/stationary_pnp_from_pb.hh:168-169,329-331 -- PB with
 //                                 ISTLBackend_NOVLP_BCGS_SSORk = --pb-prec ssor_natural, PNP with
@@ -56,7 +59,9 @@ static void usage() {
       "                [--out prefix] [--md-reduction r]\n"
       "                [--linear-solver bcgs_ssork|bcgs_ssork_mc|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
       "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n"
-      "                [--reference-solvers]  (PB: ISTL SeqSSOR in DOF order, PNP: no preconditioner)\n");
+      "                [--reference-solvers]  (PB: ISTL SeqSSOR in DOF order, PNP: no preconditioner)\n"
+      "                [--reference-order]    (the same solvers in the reference's summation orders,\n"
+      "                                        PNP_OPT_SEQ_ORDER: per-step iteration counts as the reference's)\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -181,6 +186,7 @@ int main(int argc, char **argv) {
   std::string cfgfile = argv[1], mode = "stationary", prec = "ssor", pb_prec = "ssor", out;
   std::string amg_smoother;  // empty: SSOR for the PB phase, ILU(0) for the PNP phases
   int refine = 0, steps = -1, device = -1, degree = 1;
+  bool ref_order = false;
   double mesh_scale = 1.0;  // size scale when the mesh comes from a .geo (gmsh -clscale)
   double md_reduction = -1;  // md mode: override the linear reductions (1e-5 diffusion, 1e-10 Poisson)
   // Newton absolute limit (PDELab NewtonTerminate abs_limit, default 1e-12 as in PDELab); the
@@ -211,6 +217,10 @@ int main(int argc, char **argv) {
     else if (a == "--reference-solvers") {
       pb_prec = "ssor_natural";
       prec = "none";
+    } else if (a == "--reference-order") {  // the reference's solvers in its summation orders
+      pb_prec = "ssor_natural";
+      prec = "none";
+      ref_order = true;
     }
     else if (a == "--dump-steps") {
       std::string l = next();
@@ -255,6 +265,10 @@ int main(int argc, char **argv) {
       throw pnp_gpu::Error(PNP_E_ARG, "--degree applies to the md and pb modes (the stationary "
                                       "and instationary drivers are P1: src/stationary_pnp_from_pb.hh:206-208)");
     pnp_gpu::Context ctx(mesh, params, device, world > 1 ? &comm : nullptr, degree);
+    // PNP_OPT_SEQ_ORDER: element-order assembly, ISTL's sequential mv / dot / updates, so every
+    // Newton step takes the reference program's BiCGSTAB iteration count (one rank, P1)
+    if (ref_order) pnp_gpu::check(pnp_set_option(ctx.get(), PNP_OPT_SEQ_ORDER, 1), ctx.get());
+    const int newton_verbosity = rank == 0 ? (ref_order ? 2 : 1) : 0;
     int nv = ctx.nv();  // DOF nodes of the P_degree space
     if (rank == 0)
       std::printf("mesh %s refined %d: %d vertices, P%d: %d nodes, config %s (%s)\n",
@@ -276,17 +290,15 @@ int main(int argc, char **argv) {
     pbnewton.setMinLinearReduction(s.cfg.newton_min_linear_reduction);
     pbnewton.setMaxIterations(s.cfg.newton_max_iterations);
     pbnewton.setLineSearchMaxIterations(s.cfg.newton_line_search_max_iteration);
-    pbnewton.setVerbosityLevel(rank == 0 ? 1 : 0);
+    pbnewton.setVerbosityLevel(newton_verbosity);
     try {
       pbnewton.apply();
     } catch (pnp_gpu::Error &e) {
       std::printf("Something has happened (%s)\n", e.what());  // :181-185
     }
     ctx.sync(pbu, 1);  // owned entries of every rank -> global PB potential
-    if (mode == "pb") {
-      if (!out.empty() && rank == 0) write_vector(out + "_pb.dat", pbu, nv);
-      return 0;
-    }
+    if (!out.empty() && rank == 0) write_vector(out + "_pb.dat", pbu, nv);
+    if (mode == "pb") return 0;
     // ---- PNP initial state (interpolate(BCExtension), :282) --------------------------------
     V u(3 * size_t(nv));
     pnp_gpu::check(pnp_initial_state(ctx.get(), pbu.data(), u.data()), ctx.get());
@@ -299,7 +311,7 @@ int main(int argc, char **argv) {
       nw.setMaxIterations(s.cfg.newton_max_iterations);
       nw.setLineSearchMaxIterations(s.cfg.newton_line_search_max_iteration);
       nw.setAbsoluteLimit(abs_limit);
-      nw.setVerbosityLevel(rank == 0 ? 1 : 0);
+      nw.setVerbosityLevel(newton_verbosity);
     };
     int status = 0;
     if (mode == "stationary") {  // :293-369

@@ -171,3 +171,53 @@ def test_seq_mode_rejects_other_preconditioners():
     ctx.jacobian(x)
     with pytest.raises(P.PnpError):
         ctx.linear_solve(ctx.residual(x), prec=P.PREC_ILU0)
+
+
+def test_driver_reference_order_per_step_counts(tmp_path):
+    """pnp_main --reference-order (the stationary driver, src/stationary_pnp_from_pb.hh: PB Newton
+    with BCGS_SSORk :168-169, then PNP Newton with BCGS_NOPREC :329-331, the config's Newton
+    settings) in the reference's summation orders: every Newton step's BiCGSTAB count equals the
+    oracle's, PB and PNP, and the PNP solution is the oracle's bit for bit (the oracle's PNP Newton
+    starts from the driver's own PB potential: sinh / cosh may differ in the last bit, above)."""
+    import os
+    import re
+    import subprocess
+    import meshio
+    from conftest import DATA
+    exe = os.path.join(os.path.dirname(P.LIB_PATH), "pnp_main")
+    cfgp = os.path.join(DATA, "cylinder_config.cfg")
+    prefix = str(tmp_path / "cyl")
+    out = subprocess.run([exe, cfgp, "--reference-order", "--out", prefix], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    steps, cur = [], None
+    for ln in out.stdout.splitlines():
+        m = re.search(r"Newton iteration\s+(\d+)\..*\(linear iterations (\d+)\)", ln)
+        if m:
+            if int(m.group(1)) == 1:
+                cur = []
+                steps.append(cur)
+            cur.append(int(m.group(2)))
+    assert len(steps) == 2, out.stdout
+    cfg = P.read_config(cfgp)
+    mesh = P.Mesh.read_gmsh(cfg.meshfile)
+    s = cfg.system
+    orc = O.Problem(meshio.Mesh(mesh.xy, mesh.tri, mesh.bseg, mesh.bgroup), cfg.surfaces,
+                    l_b=s["l_b"], c0=s["c0"], tau=s["tau"], cylindrical=s["cylindrical"])
+    kw = dict(reduction=s["newtonReduction"], min_linear_reduction=s["newtonMinLinearReduction"],
+              maxit=int(s["newtonMaxIterations"]),
+              line_search_maxit=int(s["newtonLineSearchMaxIteration"]),
+              linear_maxit=int(s["linearSolverIterations"]))
+    _, rpb = orc.newton(orc.operator(O.OP_PB, flux=orc.flux(), mask=orc.mask(1)),
+                        np.zeros(mesh.nv), prec=O.PREC_SSOR, **kw)
+    pb_o = list(rpb.step_linear_iterations[:rpb.iterations])
+    pb_gpu = np.loadtxt(prefix + "_pb.dat")
+    x0 = orc.initial_state(pb_gpu)
+    uo, ro = orc.newton(orc.operator(O.OP_PNP, flux=orc.flux(), mask=orc.mask(3)), x0,
+                        prec=O.PREC_NONE, **kw)
+    pnp_o = list(ro.step_linear_iterations[:ro.iterations])
+    print(f"driver PB {steps[0]} PNP {steps[1]}; oracle PB {pb_o} PNP {pnp_o}")
+    assert steps[0] == pb_o
+    assert steps[1] == pnp_o
+    u_drv = np.loadtxt(prefix + "_pnp.dat").T.ravel()
+    np.testing.assert_array_equal(u_drv, uo)

@@ -4,11 +4,12 @@
 // arguments, a memset node every 16 launches as the BiCGSTAB blocks have), instantiates, replays
 // three times, checks the result.  Run plain and under rocprofv3 --kernel-trace; if only the
 // profiled run fails, the fault is the profiler's handling of large captures, not the library's.
-// usage: graph_capture_prof N [N ...]   (tools/micro, not part of the product)
+// usage: graph_capture_prof N[:R] ...   (R replays, default 3; tools/micro, not part of the product)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -34,6 +35,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&b, n * sizeof(double)));
   for (int ai = 1; ai < argc; ai++) {
     const int N = std::atoi(argv[ai]);
+    const char *colon = std::strchr(argv[ai], ':');
+    const int R = colon ? std::atoi(colon + 1) : 3;
     CK(hipMemsetAsync(a, 0, n * sizeof(double), s));
     hipGraph_t g;
     hipGraphExec_t x;
@@ -46,12 +49,12 @@ int main(int argc, char **argv) {
     size_t nodes = 0;
     CK(hipGraphGetNodes(g, nullptr, &nodes));
     CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
-    for (int r = 0; r < 3; r++) CK(hipGraphLaunch(x, s));
+    for (int r = 0; r < R; r++) CK(hipGraphLaunch(x, s));
     CK(hipStreamSynchronize(s));
     double h = 0;
     CK(hipMemcpy(&h, a + n - 1, sizeof(double), hipMemcpyDeviceToHost));
-    std::printf("{\"launches\": %d, \"nodes\": %zu, \"result\": %.1f, \"expect\": %.1f, \"ok\": %s}\n",
-                N, nodes, h, 3.0 * N, h == 3.0 * N ? "true" : "false");
+    std::printf("{\"launches\": %d, \"replays\": %d, \"nodes\": %zu, \"result\": %.1f, \"expect\": %.1f, \"ok\": %s}\n",
+                N, R, nodes, h, double(R) * N, h == double(R) * N ? "true" : "false");
     std::fflush(stdout);
     CK(hipGraphExecDestroy(x));
     CK(hipGraphDestroy(g));

@@ -7,4 +7,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_ssor_natural.py -x -q --tim
 for lib in kl16 kl32; do
   PNP_AMD_LIB=dune-pnp_amd/ab/lib_$lib.so timeout -k 10 300 python -u -m pytest tests/test_gpu_ssor_natural.py -x -q --timeout 200 --timeout-method thread > $O/nat_tests_$lib.log 2>&1; echo "nat tests $lib rc=$?"
 done
-bash tools/ab_nat_libs.sh r4f/ab - kl16 kl32
+timeout -k 10 300 python -u -m pytest tests/test_gpu_seq_order.py -x -q -k driver --timeout 250 --timeout-method thread -s > $O/driver_ref_order.log 2>&1; echo "driver test rc=$?"
+bash tools/ab_nat_libs.sh r4f/ab - kl16 kl32 pd2 pd4
