@@ -5,6 +5,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <queue>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -196,6 +197,22 @@ struct pnp_ctx {
     std::vector<long long> eoff;
     DBuf<int4> info;
     DBuf<int> ecol, eidx;
+    // the tail as chains (PNP_NAT_CHAIN): lane-group row lists, rows, padded entries
+    bool chain_ok = false;
+    int chain_groups = 0, chain_wpad = 0;
+    DBuf<int> cgptr, cecode, ceidx;
+    DBuf<int4> crec;
+    pnp::NatFlow::Chains chains() const {
+      pnp::NatFlow::Chains c;
+      if (!chain_ok) return c;
+      c.ngroups = chain_groups;
+      c.wpad = chain_wpad;
+      c.gptr = cgptr.p;
+      c.rec = crec.p;
+      c.ecode = cecode.p;
+      c.eidx = ceidx.p;
+      return c;
+    }
     pnp::NatSweep view() const {
       pnp::NatSweep w;
       w.nlev = int(lptr.size()) - 1;
@@ -228,7 +245,7 @@ struct pnp_ctx {
   struct IluFlowDev {
     bool built = false, ok = false;
     pnp::IluFlow F;
-    DBuf<int> dep_ptr, dep_list;
+    DBuf<int> dep_ptr, dep_list, qlist;
     DBuf<unsigned> flags;
   };
   IluFlowDev ilu_flow[2];
@@ -833,8 +850,105 @@ struct pnp_ctx {
         const char *ev = std::getenv("PNP_NAT_TAIL");
         return ev ? std::max(0, std::atoi(ev)) : 0;
       }();
+      // PNP_NAT_CHAIN (rows): the tail as chains instead (k_ssor_nat_chain; takes precedence)
+      static const int chain_rows = [] {
+        const char *ev = std::getenv("PNP_NAT_CHAIN");
+        return ev ? std::max(0, std::atoi(ev)) : 0;
+      }();
+      const int trows = chain_rows > 0 ? chain_rows : tail_rows;
       int ltail = nlev;
-      while (tail_rows > 0 && ltail > 0 && lptr[ltail] - lptr[ltail - 1] <= tail_rows) ltail--;
+      while (trows > 0 && ltail > 0 && lptr[ltail] - lptr[ltail - 1] <= trows) ltail--;
+      W.chain_ok = false;
+      if (chain_rows > 0 && ltail < nlev) {
+        // heavy-path chains of the tail: parent = the first dependency on the level just before
+        // (inside the tail); each row continues the chain of its child with the longest path
+        // below it; chains packed into lane groups by level interval (greedy, by start level)
+        const int t0 = lptr[ltail], t1 = lptr[nlev];
+        auto isdep = [&](int R, int C) {
+          return C != R && !empty(C) && (fwd ? C < R : C > R);
+        };
+        std::vector<int> parent(n, -1), heavy(n, -1), hbest(n, 0);
+        int wmax = 0;
+        for (int t = t0; t < t1; t++) {
+          const int R = rl[t];
+          wmax = std::max(wmax, cnt[R + 1] - cnt[R]);
+          for (int k = cnt[R]; k < cnt[R + 1]; k++) {
+            const int C = col[k];
+            if (isdep(R, C) && lev[C] == lev[R] - 1 && lev[C] >= ltail) {
+              parent[R] = C;
+              break;
+            }
+          }
+        }
+        for (int t = t1 - 1; t >= t0; t--) {  // decreasing level
+          const int R = rl[t], P = parent[R], h = 1 + hbest[R];
+          if (P >= 0 && h > hbest[P]) {
+            hbest[P] = h;
+            heavy[P] = R;
+          }
+        }
+        // at most the grid's resident lane groups (the kernel's progress needs them all
+        // resident): past that, a chain shares the group that frees first, its rows interleaved
+        // by level (a row whose parent is not the group's previous row reads it from memory)
+        const int gcap = std::max(1, pnp::ssor_natural_chain_capacity());
+        std::vector<std::vector<int>> grows;
+        std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>,
+                            std::greater<std::pair<int, int>>> freeq;  // (end level, group)
+        bool shared = false;
+        for (int t = t0; t < t1; t++) {
+          const int R = rl[t];
+          if (parent[R] >= 0 && heavy[parent[R]] == R) continue;  // inside a chain
+          int g;
+          if (!freeq.empty() && (freeq.top().first < lev[R] || int(grows.size()) >= gcap)) {
+            shared |= freeq.top().first >= lev[R];
+            g = freeq.top().second;
+            freeq.pop();
+          } else {
+            g = int(grows.size());
+            grows.emplace_back();
+          }
+          int X = R, last = lev[R];
+          for (; X >= 0; X = heavy[X]) {
+            grows[g].push_back(X);
+            last = lev[X];
+          }
+          freeq.push({std::max(last, 0), g});
+        }
+        if (shared)  // every group's rows in level order (stable: a chain's rows stay in order)
+          for (auto &G : grows)
+            std::stable_sort(G.begin(), G.end(), [&](int a, int b) { return lev[a] < lev[b]; });
+        const int wpad = wmax;
+        if (wpad <= pnp::ssor_natural_chain_width()) {
+          std::vector<int> gptr(1, 0), ecode, eidx;
+          std::vector<int4> rec;
+          for (const auto &G : grows) {
+            for (int R : G) {
+              const int len = cnt[R + 1] - cnt[R];
+              rec.push_back(make_int4(R, len, diag[R], 0));
+              for (int k = 0; k < wpad; k++) {
+                if (k < len) {
+                  const int C = col[cnt[R] + k];
+                  ecode.push_back(empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2)));
+                  eidx.push_back(cnt[R] + k);
+                } else {
+                  ecode.push_back(-1);
+                  eidx.push_back(-1);
+                }
+              }
+            }
+            gptr.push_back(int(rec.size()));
+          }
+          int rc2;
+          if ((rc2 = upv(W.cgptr, gptr, "natural SSOR chains")) ||
+              (rc2 = upv(W.crec, rec, "natural SSOR chains")) ||
+              (rc2 = upv(W.cecode, ecode, "natural SSOR chains")) ||
+              (rc2 = upv(W.ceidx, eidx, "natural SSOR chains")))
+            return rc2;
+          W.chain_groups = int(grows.size());
+          W.chain_wpad = wpad;
+          W.chain_ok = true;
+        }
+      }
       for (int l = 0; l < nlev && nat_units_ok; l++) {
         if (l == ltail) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
         const int nl = lptr[l + 1] - lptr[l];
@@ -910,6 +1024,8 @@ struct pnp_ctx {
     F.nunits_f = nat_units_f;
     F.tail_f = nat_tail_f;
     F.tail_b = nat_tail_b;
+    F.chain_f = nat_f.chains();
+    F.chain_b = nat_b.chains();
     F.fwd = nat_f.view();
     F.bwd = nat_b.view();
     F.abort_word = nat_abort.p;
@@ -1040,7 +1156,21 @@ struct pnp_ctx {
     if ((rc = upv(D.dep_ptr, dptr, "ILU(0) dataflow deps")) ||
         (rc = upv(D.dep_list, dlist, "ILU(0) dataflow deps")))
       return rc;
-    hipError_t e = D.flags.alloc(size_t(nu + 1 + 3) & ~size_t(3));
+    // 8 queues (IluFlow::persistent 2): the q-th eighth of every stage, in unit order
+    std::vector<int> ql;
+    ql.reserve(nu);
+    F.qptr[0] = 0;
+    for (int q = 0; q < 8; q++) {
+      for (int s2 = 0; s2 < F.nstages; s2++) {
+        const int a = F.unit0[s2], n = F.unit0[s2 + 1] - a;
+        for (int k = a + int((long long)n * q / 8); k < a + int((long long)n * (q + 1) / 8); k++)
+          ql.push_back(k);
+      }
+      F.qptr[q + 1] = int(ql.size());
+    }
+    if (ql.empty()) ql.push_back(0);
+    if ((rc = upv(D.qlist, ql, "ILU(0) dataflow queues"))) return rc;
+    hipError_t e = D.flags.alloc(size_t(nu + 1 + 8 * 16 + 3) & ~size_t(3));
     if (e == hipSuccess && !ilu_flow_abort.p) {
       e = ilu_flow_abort.alloc(4);
       if (e == hipSuccess) e = hipMemset(ilu_flow_abort.p, 0, 16);
@@ -1049,6 +1179,7 @@ struct pnp_ctx {
     F.dep_ptr = D.dep_ptr.p;
     F.dep_list = D.dep_list.p;
     F.flags = D.flags.p;
+    F.qlist = D.qlist.p;
     F.abort_word = ilu_flow_abort.p;
     D.F = F;
     D.ok = true;
@@ -1059,15 +1190,17 @@ struct pnp_ctx {
   int ilu_apply(const double *d, double *vout, int c_first, const char *what) {
     // the resident-grid form needs the device to itself: not with in-process ranks sharing it
     // (and one context per GPU at N > 1); PNP_ILU_FLOW_TICKET=1: the ticketed form (any residency)
-    static const int ticket = [] {
-      const char *ev = std::getenv("PNP_ILU_FLOW_TICKET");
-      return ev && std::atoi(ev) != 0 ? 1 : 0;
+    // PNP_ILU_FLOW_MODE: IluFlow::persistent (0 ticket, 1 static resident grid, 2 queues)
+    static const int mode = [] {
+      const char *ev = std::getenv("PNP_ILU_FLOW_MODE");
+      const int m = ev ? std::atoi(ev) : 2;
+      return (m >= 0 && m <= 2) ? m : 2;
     }();
-    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (ticket || !dist)) {
+    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (mode == 0 || !dist)) {
       IluFlowDev &D = ilu_flow[c_first];
       int rc;
       if (!D.built && (rc = ilu_flow_build(c_first, D))) return rc;
-      D.F.persistent = ticket ? 0 : 1;
+      D.F.persistent = mode;
       if (D.ok) {
         hipError_t e = pnp::launch_ilu0_flow(dl, D.F, nf, pat, lvals.p, uvals.p, d, vout, stream,
                                              f32_now());

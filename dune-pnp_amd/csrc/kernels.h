@@ -356,13 +356,19 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int 
 constexpr int kIluFlowMaxStages = 32;
 struct IluFlow {
   int nstages = 0, nunits = 0;
-  int persistent = 1;  // 1: a resident grid takes units b, b + G, ...; 0: one ticketed WG per unit
+  // 0: one workgroup per unit, taken by one atomic ticket; 1: a resident grid, workgroup b takes
+  // units b, b + G, ...; 2: a resident grid over 8 queues (blockIdx % 8: the XCD label of the
+  // round-robin dispatch), each an increasing unit list (qlist[qptr[q] ..), the q-th eighth of
+  // every stage) with its own ticket at flags[nunits + 16 q], emptied queues helped in turn
+  int persistent = 1;
+  const int *qlist = nullptr;
+  int qptr[9] = {};
   int unit0[kIluFlowMaxStages + 1] = {};  // first unit of each stage
   int kind[kIluFlowMaxStages] = {};       // kIluFwd 0 / kIluBwd 1 / kIluLast 2
   int r0[kIluFlowMaxStages] = {}, r1[kIluFlowMaxStages] = {};  // the stage colour's positions
   int blk0[kIluFlowMaxStages] = {};       // the colour's first block in the staging-list numbering
   const int *dep_ptr = nullptr, *dep_list = nullptr;
-  unsigned *flags = nullptr;              // [nunits + 1], padded to 16 B
+  unsigned *flags = nullptr;              // [nunits + 1 + 8 x 16], padded to 16 B
   unsigned *abort_word = nullptr;
 };
 hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pat, const void *lv,
@@ -460,12 +466,24 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
 // is set when an operand wait times out.
 // rows per unit = rows per wavefront of the flow kernel (64 / its lanes per row)
 int ssor_natural_unit_rows();
+// the longest row the chain kernel takes (entries per lane group pass)
+int ssor_natural_chain_width();
+// lane groups of the chain kernel resident at once on this device
+int ssor_natural_chain_capacity();
 struct NatFlow {
   const int4 *units = nullptr;
   int nunits = 0, nunits_f = 0;
-  // first unit of each sweep's narrow tail (levels of at most PNP_NAT_TAIL rows to the sweep's
-  // end), run by one workgroup: forward [tail_f, nunits_f), backward [tail_b, nunits)
+  // first unit of each sweep's narrow tail (levels of at most PNP_NAT_TAIL / PNP_NAT_CHAIN rows to
+  // the sweep's end): forward [tail_f, nunits_f), backward [tail_b, nunits)
   int tail_f = 0, tail_b = 0;
+  // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: lane group g walks
+  // rows gptr[g] .. gptr[g+1] of rec ({ext row, entry count, diagonal value index, 0}); row q's
+  // entries at q * wpad .. + count of ecode (operand codes, as NatFlow's) and eidx (value indices)
+  struct Chains {
+    int ngroups = 0, wpad = 0;
+    const int *gptr = nullptr, *ecode = nullptr, *eidx = nullptr;
+    const int4 *rec = nullptr;
+  } chain_f, chain_b;
   NatSweep fwd, bwd;
   unsigned *abort_word = nullptr;
 };

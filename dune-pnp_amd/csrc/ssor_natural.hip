@@ -27,6 +27,7 @@
 // across ranks, as the reference's NOVLP SSOR acts on the local matrix only).
 #include "kernels.h"
 
+#include <climits>
 #include <cstdlib>
 #include <algorithm>
 
@@ -252,9 +253,140 @@ __global__ void __launch_bounds__(BLK)
   }
 }
 constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
+
+// ---- the narrow tail as chains (NatChains, PNP_NAT_CHAIN) ---------------------------------------
+// In the narrow tail almost every row has exactly one dependency on the level just before its own
+// (pore_pnp k=4, PB forward: 60,851 of 61,851 tail rows; tools/nat_dag.py): the tail is a forest of
+// chains.  The host cuts it into heavy paths (each row continues the chain of the child with the
+// longest remaining path) and packs the chains into lane groups by level interval; a group of kL
+// lanes walks its rows in order, and a row's dependency on the row the group computed just before
+// it is taken from that row's result in the group's registers -- no memory hop.  Other operands
+// are polled as in the flow kernel.  Each group advances on its own: every pass, the groups whose
+// current row has all its operands compute it and move on, the others poll again, so a group never
+// waits for a group of its own wave.  The next rows' records and entries are loaded two rows ahead,
+// their values and operands one row ahead.  The arithmetic is the level kernel's (products in
+// column order subtracted by the row's first lane), so the result is the oracle's bit for bit.
+// Progress: a row depends only on rows of lower levels; a group's rows are in increasing level
+// order; the lowest pending row over all groups has all its operands, and its group computes it in
+// the next pass (every group of the small grid resident, one context per stream).
+struct ChainStage {
+  int4 rec;                  // {row, entry count, diagonal value index, 0}; row < 0: none
+  int c[kS], ix[kS];         // operand codes and value indices of this lane's entries
+  double a[kS];              // values
+  unsigned long long b[kS];  // operands (kNatPending: not final yet)
+  double d0, own, adiag;     // the row's first lane: d, its forward value (backward), a_RR
+};
+
+__global__ void __launch_bounds__(kB)
+    k_ssor_nat_chain(const int *__restrict__ gptr, int ngroups, const int4 *__restrict__ rec,
+                     const int *__restrict__ ecode, const int *__restrict__ eidx, int wpad,
+                     const double *__restrict__ val, const double *__restrict__ d,
+                     unsigned long long *vf, unsigned long long *vb, int bwd,
+                     unsigned *abort_word) {
+  const int lane = threadIdx.x % 64, j = lane % kL, base = lane - j;
+  const int g = (blockIdx.x * kB + int(threadIdx.x)) / kL;
+  const bool gl = g < ngroups;
+  int p = gl ? gptr[g] : 0;
+  const int pend = gl ? gptr[g + 1] : 0;
+  unsigned long long *out = bwd ? vb : vf;
+  auto op_addr = [&](int c) { return c >= 0 ? vf + c : vb + (-(c + 2)); };
+  auto ld = [&](const unsigned long long *q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // the operand code under which a row's own result is read by later rows of its sweep
+  auto code_of = [&](int row) { return row < 0 ? INT_MIN : (bwd ? -(row + 2) : row); };
+  auto load_rec = [&](int q, ChainStage &S) {
+    const bool in = q < pend;
+    S.rec = in ? rec[q] : make_int4(-1, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kS; u++) {
+      const int k = j + u * kL;
+      const bool e = in && k < wpad;
+      S.c[u] = e ? ecode[size_t(q) * wpad + k] : -1;
+      S.ix[u] = e ? eidx[size_t(q) * wpad + k] : -1;
+    }
+  };
+  // values, d, a_RR and the operands of a staged row; the one computed by this group just before
+  // it (prevcode) is not loaded: it comes from the group's registers
+  auto load_vals = [&](ChainStage &S, int prevcode) {
+#pragma unroll
+    for (int u = 0; u < kS; u++) {
+      S.a[u] = S.ix[u] >= 0 ? val[S.ix[u]] : 0.0;
+      S.b[u] = (S.c[u] == -1 || S.c[u] == prevcode) ? 0ull : ld(op_addr(S.c[u]));
+    }
+    const bool h = S.rec.x >= 0 && j == 0;
+    S.d0 = h ? d[S.rec.x] : 0.0;
+    S.own = (h && bwd) ? __longlong_as_double(ld(vf + S.rec.x)) : 0.0;
+    S.adiag = h ? val[S.rec.z] : 1.0;
+  };
+  ChainStage s0, s1, s2;  // s0: the current row; s1, s2: the next two
+  load_rec(p, s0);
+  load_rec(p + 1, s1);
+  load_rec(p + 2, s2);
+  int prevcode = INT_MIN;  // no row computed yet
+  double prev = 0.0;
+  load_vals(s0, prevcode);
+  load_vals(s1, code_of(s0.rec.x));
+  unsigned long long t0 = wall_clock64();
+  while (__any(p < pend)) {
+    const bool act = p < pend;
+    const double pv = __shfl(prev, base, 64);
+    bool wait = false;
+#pragma unroll
+    for (int u = 0; u < kS; u++)
+      if (act && s0.c[u] != -1 && s0.c[u] != prevcode && s0.b[u] == kNatPending) {
+        s0.b[u] = ld(op_addr(s0.c[u]));
+        wait |= s0.b[u] == kNatPending;
+      }
+    const unsigned long long wm = __ballot(wait);
+    const bool ready = act && ((wm >> base) & ((1ull << kL) - 1)) == 0;
+    double pr[kS];
+#pragma unroll
+    for (int u = 0; u < kS; u++) {
+      const double o = s0.c[u] == -1         ? 0.0
+                       : s0.c[u] == prevcode ? pv
+                                             : __longlong_as_double(s0.b[u]);
+      pr[u] = s0.ix[u] >= 0 ? s0.a[u] * o : 0.0;
+    }
+    double rhs = s0.d0;
+    const int width = s0.rec.y;
+#pragma unroll
+    for (int k = 0; k < kC; k++) {
+      const double q = __shfl(pr[k / kL], base + k % kL, 64);
+      if (j == 0 && k < width) rhs -= q;
+    }
+    if (ready) {
+      if (j == 0) {
+        const double res = s0.own + 1.0 * (rhs / s0.adiag);
+        __hip_atomic_store(out + s0.rec.x, (unsigned long long)__double_as_longlong(res),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = res;
+      }
+      prevcode = code_of(s0.rec.x);
+      t0 = wall_clock64();
+      p++;
+      s0 = s1;
+      s1 = s2;
+      load_rec(p + 2, s2);
+      load_vals(s1, code_of(s0.rec.x));
+    } else if (act && wall_clock64() - t0 > kNatTimeout) {
+      if (lane == 0)
+        __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;  // results void; the host reports the timeout
+    }
+  }
+}
 }  // namespace
 
 int ssor_natural_unit_rows() { return 64 / kL; }
+int ssor_natural_chain_width() { return kC; }
+int ssor_natural_chain_capacity() {
+  int dev = 0, cus = 0, per = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_chain, kB, 0);
+  return cus * std::max(1, per) * (kB / kL);
+}
 
 hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
                                     double *vf, double *vb, hipStream_t s) {
@@ -274,21 +406,25 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
   auto vfu = reinterpret_cast<unsigned long long *>(vf);
   auto vbu = reinterpret_cast<unsigned long long *>(vb);
   // [u0, u1) of one sweep: head units on the resident grid, tail units in one workgroup
-  auto sweep = [&](int u0, int ut, int u1) {
+  auto sweep = [&](int u0, int ut, int u1, const NatFlow::Chains &C, int bwd) {
     if (ut > u0) {
       const int blocks = std::min(grid, (ut - u0 + kB / 64 - 1) / (kB / 64));
       hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB), 0,
                          s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
                          F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
     }
-    if (u1 > ut)
+    if (u1 > ut && C.ngroups > 0)
+      hipLaunchKernelGGL(k_ssor_nat_chain, dim3((C.ngroups * kL + kB - 1) / kB), dim3(kB), 0, s,
+                         C.gptr, C.ngroups, C.rec, C.ecode, C.eidx, C.wpad, val, d, vfu, vbu, bwd,
+                         F.abort_word);
+    else if (u1 > ut)
       hipLaunchKernelGGL((k_ssor_nat_flow<kTailBlk, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3(1),
                          dim3(kTailBlk), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,
                          F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
                          F.abort_word);
   };
-  sweep(0, F.tail_f, F.nunits_f);
-  sweep(F.nunits_f, F.tail_b, F.nunits);
+  sweep(0, F.tail_f, F.nunits_f, F.chain_f, 0);
+  sweep(F.nunits_f, F.tail_b, F.nunits, F.chain_b, 1);
   return hipGetLastError();
 }
 
