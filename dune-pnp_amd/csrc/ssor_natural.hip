@@ -259,12 +259,12 @@ constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
 // (pore_pnp k=4, PB forward: 60,851 of 61,851 tail rows; tools/nat_dag.py): the tail is a forest of
 // chains.  The host cuts it into heavy paths (each row continues the chain of the child with the
 // longest remaining path) and packs the chains into lane groups by level interval; a group of kL
-// lanes walks its rows in order, and a row's dependency on the row the group computed just before
-// it is taken from that row's result in the group's registers -- no memory hop.  Other operands
+// lanes walks its rows in order, and a row's dependency on the two rows the group computed just
+// before it is taken from their results in the group's registers -- no memory hop.  Other operands
 // are polled as in the flow kernel.  Each group advances on its own: every pass, the groups whose
 // current row has all its operands compute it and move on, the others poll again, so a group never
-// waits for a group of its own wave.  The next rows' records and entries are loaded two rows ahead,
-// their values and operands one row ahead.  The arithmetic is the level kernel's (products in
+// waits for a group of its own wave.  The next two rows' records, entries, values and operands are
+// in flight while the current one waits or computes.  The arithmetic is the level kernel's (products in
 // column order subtracted by the row's first lane), so the result is the oracle's bit for bit.
 // Progress: a row depends only on rows of lower levels; a group's rows are in increasing level
 // order; the lowest pending row over all groups has all its operands, and its group computes it in
@@ -306,35 +306,39 @@ __global__ void __launch_bounds__(kB)
       S.ix[u] = e ? eidx[size_t(q) * wpad + k] : -1;
     }
   };
-  // values, d, a_RR and the operands of a staged row; the one computed by this group just before
-  // it (prevcode) is not loaded: it comes from the group's registers
-  auto load_vals = [&](ChainStage &S, int prevcode) {
+  // values, d, a_RR and the operands of a staged row; operands that are the results of the two
+  // rows this group computes just before it (codes k1, k2) are not loaded: they are taken from the
+  // group's registers when the row is computed
+  auto load_vals = [&](ChainStage &S, int k1, int k2) {
 #pragma unroll
     for (int u = 0; u < kS; u++) {
       S.a[u] = S.ix[u] >= 0 ? val[S.ix[u]] : 0.0;
-      S.b[u] = (S.c[u] == -1 || S.c[u] == prevcode) ? 0ull : ld(op_addr(S.c[u]));
+      S.b[u] = (S.c[u] == -1 || S.c[u] == k1 || S.c[u] == k2) ? 0ull : ld(op_addr(S.c[u]));
     }
     const bool h = S.rec.x >= 0 && j == 0;
     S.d0 = h ? d[S.rec.x] : 0.0;
     S.own = (h && bwd) ? __longlong_as_double(ld(vf + S.rec.x)) : 0.0;
     S.adiag = h ? val[S.rec.z] : 1.0;
   };
-  ChainStage s0, s1, s2;  // s0: the current row; s1, s2: the next two
+  ChainStage s0, s1, s2;  // s0: the current row; s1, s2: the next two, values and operands issued
   load_rec(p, s0);
   load_rec(p + 1, s1);
   load_rec(p + 2, s2);
-  int prevcode = INT_MIN;  // no row computed yet
-  double prev = 0.0;
-  load_vals(s0, prevcode);
-  load_vals(s1, code_of(s0.rec.x));
+  // the group's last two results (head lane) and their operand codes
+  int code1 = INT_MIN, code2 = INT_MIN;
+  double val1 = 0.0, val2 = 0.0;
+  load_vals(s0, INT_MIN, INT_MIN);
+  load_vals(s1, code_of(s0.rec.x), INT_MIN);
+  load_vals(s2, code_of(s1.rec.x), code_of(s0.rec.x));
   unsigned long long t0 = wall_clock64();
   while (__any(p < pend)) {
     const bool act = p < pend;
-    const double pv = __shfl(prev, base, 64);
+    const double pv1 = __shfl(val1, base, 64), pv2 = __shfl(val2, base, 64);
     bool wait = false;
 #pragma unroll
     for (int u = 0; u < kS; u++)
-      if (act && s0.c[u] != -1 && s0.c[u] != prevcode && s0.b[u] == kNatPending) {
+      if (act && s0.c[u] != -1 && s0.c[u] != code1 && s0.c[u] != code2 &&
+          s0.b[u] == kNatPending) {
         s0.b[u] = ld(op_addr(s0.c[u]));
         wait |= s0.b[u] == kNatPending;
       }
@@ -343,9 +347,10 @@ __global__ void __launch_bounds__(kB)
     double pr[kS];
 #pragma unroll
     for (int u = 0; u < kS; u++) {
-      const double o = s0.c[u] == -1         ? 0.0
-                       : s0.c[u] == prevcode ? pv
-                                             : __longlong_as_double(s0.b[u]);
+      const double o = s0.c[u] == -1      ? 0.0
+                       : s0.c[u] == code1 ? pv1
+                       : s0.c[u] == code2 ? pv2
+                                          : __longlong_as_double(s0.b[u]);
       pr[u] = s0.ix[u] >= 0 ? s0.a[u] * o : 0.0;
     }
     double rhs = s0.d0;
@@ -356,19 +361,21 @@ __global__ void __launch_bounds__(kB)
       if (j == 0 && k < width) rhs -= q;
     }
     if (ready) {
+      code2 = code1;
+      val2 = val1;
+      code1 = code_of(s0.rec.x);
       if (j == 0) {
         const double res = s0.own + 1.0 * (rhs / s0.adiag);
         __hip_atomic_store(out + s0.rec.x, (unsigned long long)__double_as_longlong(res),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        prev = res;
+        val1 = res;
       }
-      prevcode = code_of(s0.rec.x);
       t0 = wall_clock64();
       p++;
       s0 = s1;
       s1 = s2;
       load_rec(p + 2, s2);
-      load_vals(s1, code_of(s0.rec.x));
+      load_vals(s2, code_of(s1.rec.x), code_of(s0.rec.x));
     } else if (act && wall_clock64() - t0 > kNatTimeout) {
       if (lane == 0)
         __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
