@@ -895,24 +895,31 @@ struct pnp_ctx {
         std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>,
                             std::greater<std::pair<int, int>>> freeq;  // (end level, group)
         bool shared = false;
+        long long rr = 0;  // over the cap: chains dealt round-robin (a balanced share per group)
+        std::vector<int> gend;  // each group's last level; heap entries that disagree are stale
         for (int t = t0; t < t1; t++) {
           const int R = rl[t];
           if (parent[R] >= 0 && heavy[parent[R]] == R) continue;  // inside a chain
+          while (!freeq.empty() && freeq.top().first != gend[freeq.top().second]) freeq.pop();
           int g;
-          if (!freeq.empty() && (freeq.top().first < lev[R] || int(grows.size()) >= gcap)) {
-            shared |= freeq.top().first >= lev[R];
+          if (!freeq.empty() && freeq.top().first < lev[R]) {
             g = freeq.top().second;
             freeq.pop();
+          } else if (int(grows.size()) >= gcap) {
+            g = int(rr++ % gcap);
+            shared = true;
           } else {
             g = int(grows.size());
             grows.emplace_back();
+            gend.push_back(-1);
           }
           int X = R, last = lev[R];
           for (; X >= 0; X = heavy[X]) {
             grows[g].push_back(X);
             last = lev[X];
           }
-          freeq.push({std::max(last, 0), g});
+          gend[g] = std::max(gend[g], last);
+          freeq.push({gend[g], g});
         }
         if (shared)  // every group's rows in level order (stable: a chain's rows stay in order)
           for (auto &G : grows)
