@@ -245,7 +245,7 @@ struct pnp_ctx {
   struct IluFlowDev {
     bool built = false, ok = false;
     pnp::IluFlow F;
-    DBuf<int> dep_ptr, dep_list, qlist;
+    DBuf<int> dep_ptr, dep_list;
     DBuf<unsigned> flags;
   };
   IluFlowDev ilu_flow[2];
@@ -1163,21 +1163,7 @@ struct pnp_ctx {
     if ((rc = upv(D.dep_ptr, dptr, "ILU(0) dataflow deps")) ||
         (rc = upv(D.dep_list, dlist, "ILU(0) dataflow deps")))
       return rc;
-    // 8 queues (IluFlow::persistent 2): the q-th eighth of every stage, in unit order
-    std::vector<int> ql;
-    ql.reserve(nu);
-    F.qptr[0] = 0;
-    for (int q = 0; q < 8; q++) {
-      for (int s2 = 0; s2 < F.nstages; s2++) {
-        const int a = F.unit0[s2], n = F.unit0[s2 + 1] - a;
-        for (int k = a + int((long long)n * q / 8); k < a + int((long long)n * (q + 1) / 8); k++)
-          ql.push_back(k);
-      }
-      F.qptr[q + 1] = int(ql.size());
-    }
-    if (ql.empty()) ql.push_back(0);
-    if ((rc = upv(D.qlist, ql, "ILU(0) dataflow queues"))) return rc;
-    hipError_t e = D.flags.alloc(size_t(nu + 1 + 8 * 16 + 3) & ~size_t(3));
+    hipError_t e = D.flags.alloc(size_t(nu + 1 + 3) & ~size_t(3));
     if (e == hipSuccess && !ilu_flow_abort.p) {
       e = ilu_flow_abort.alloc(4);
       if (e == hipSuccess) e = hipMemset(ilu_flow_abort.p, 0, 16);
@@ -1186,7 +1172,6 @@ struct pnp_ctx {
     F.dep_ptr = D.dep_ptr.p;
     F.dep_list = D.dep_list.p;
     F.flags = D.flags.p;
-    F.qlist = D.qlist.p;
     F.abort_word = ilu_flow_abort.p;
     D.F = F;
     D.ok = true;
@@ -1197,11 +1182,13 @@ struct pnp_ctx {
   int ilu_apply(const double *d, double *vout, int c_first, const char *what) {
     // the resident-grid form needs the device to itself: not with in-process ranks sharing it
     // (and one context per GPU at N > 1); PNP_ILU_FLOW_TICKET=1: the ticketed form (any residency)
-    // PNP_ILU_FLOW_MODE: IluFlow::persistent (0 ticket, 1 static resident grid, 2 queues)
+    // PNP_ILU_FLOW_MODE: IluFlow::persistent (0 ticket, 1 static resident grid, the default).
+    // A third form, a resident grid over 8 ticketed queues, hung in the bitwise tests (killed
+    // after 180 s of silence, gpurun_out r4i) and was removed
     static const int mode = [] {
       const char *ev = std::getenv("PNP_ILU_FLOW_MODE");
-      const int m = ev ? std::atoi(ev) : 2;
-      return (m >= 0 && m <= 2) ? m : 2;
+      const int m = ev ? std::atoi(ev) : 1;
+      return (m >= 0 && m <= 1) ? m : 1;
     }();
     if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (mode == 0 || !dist)) {
       IluFlowDev &D = ilu_flow[c_first];

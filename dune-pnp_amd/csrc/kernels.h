@@ -357,18 +357,14 @@ constexpr int kIluFlowMaxStages = 32;
 struct IluFlow {
   int nstages = 0, nunits = 0;
   // 0: one workgroup per unit, taken by one atomic ticket; 1: a resident grid, workgroup b takes
-  // units b, b + G, ...; 2: a resident grid over 8 queues (blockIdx % 8: the XCD label of the
-  // round-robin dispatch), each an increasing unit list (qlist[qptr[q] ..), the q-th eighth of
-  // every stage) with its own ticket at flags[nunits + 16 q], emptied queues helped in turn
+  // units b, b + G, ...
   int persistent = 1;
-  const int *qlist = nullptr;
-  int qptr[9] = {};
   int unit0[kIluFlowMaxStages + 1] = {};  // first unit of each stage
   int kind[kIluFlowMaxStages] = {};       // kIluFwd 0 / kIluBwd 1 / kIluLast 2
   int r0[kIluFlowMaxStages] = {}, r1[kIluFlowMaxStages] = {};  // the stage colour's positions
   int blk0[kIluFlowMaxStages] = {};       // the colour's first block in the staging-list numbering
   const int *dep_ptr = nullptr, *dep_list = nullptr;
-  unsigned *flags = nullptr;              // [nunits + 1 + 8 x 16], padded to 16 B
+  unsigned *flags = nullptr;              // [nunits + 1], padded to 16 B
   unsigned *abort_word = nullptr;
 };
 hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pat, const void *lv,

@@ -1312,42 +1312,6 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_flow(DevLayout L, IluFlow F,
                                                       const VT *__restrict__ uv,
                                                       const double *__restrict__ d, double *v) {
   extern __shared__ double smem[];  // [0, 2): reserved (16-B aligned staging); [2, ..): records
-  if (F.persistent == 2) {
-    // queue q = blockIdx % 8 first, then the others in turn once it is empty.  A queue's units are
-    // claimed in increasing order; the smallest unfinished unit's queue is not empty, so its own
-    // workgroups (every queue has G / 8 resident ones, none of which helps elsewhere before its
-    // queue is empty) claim it once their earlier units of that queue are done
-    int *tk = reinterpret_cast<int *>(smem);
-    const int q0 = blockIdx.x % 8;
-    while (true) {
-      if (threadIdx.x == 0) {
-        int u = -1;
-        for (int k = 0; k < 8 && u < 0; k++) {
-          const int q = (q0 + k) & 7;
-          if (__hip_atomic_load(F.flags + F.nunits + 16 * q, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT) >= unsigned(F.qptr[q + 1] - F.qptr[q]))
-            continue;  // empty: no ticket taken
-          const unsigned t = __hip_atomic_fetch_add(F.flags + F.nunits + 16 * q, 1u,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (t < unsigned(F.qptr[q + 1] - F.qptr[q])) u = F.qlist[F.qptr[q] + t];
-        }
-        tk[0] = u;
-      }
-      __syncthreads();
-      const int u = tk[0];
-      __syncthreads();  // the word is rewritten by the next claim
-      if (u < 0) return;
-      int st = 0;
-      while (st + 1 < F.nstages && u >= F.unit0[st + 1]) st++;
-      const int kind = F.kind[st];
-      if (kind == kIluFwd)
-        ilu_flow_unit<NF, PAT, kIluFwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
-      else if (kind == kIluLast)
-        ilu_flow_unit<NF, PAT, kIluLast, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
-      else
-        ilu_flow_unit<NF, PAT, kIluBwd, B, VT>(L, F, u, st, lv, uv, d, v, smem + 2);
-    }
-  }
   if (F.persistent) {
     // resident grid (sized from the occupancy query): workgroup b takes units b, b + G, ... in
     // order.  The smallest unfinished unit's workgroup has finished its own earlier units, so it
@@ -2219,8 +2183,7 @@ hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pa
   if (F.nunits <= 0) return hipSuccess;
   if (!L.lsx_ptr || F.nstages > kIluFlowMaxStages) return hipErrorInvalidValue;
   // flags and the ticket, one block from the allocation's start, a multiple of 16 bytes
-  hipError_t e = hipMemsetAsync(F.flags, 0, (size_t(F.nunits + 1 + 8 * 16) * 4 + 15) & ~size_t(15),
-                                s);
+  hipError_t e = hipMemsetAsync(F.flags, 0, (size_t(F.nunits + 1) * 4 + 15) & ~size_t(15), s);
   if (e != hipSuccess) return e;
   const size_t lds = 16 + size_t(L.sx_max) * nf * sizeof(double);
   const int kBsel = ilu_lds_bsel() ? ilu_lds_bsel() : (L.n_owned > 1500000 ? 3 : 2);
@@ -2228,8 +2191,7 @@ hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pa
     using VT = decltype(vt);
     const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
     auto go = [&](auto kern) {
-      int grid = F.persistent ? resident_grid(kern, lds, F.nunits) : F.nunits;
-      if (F.persistent == 2) grid = std::max(8, grid - grid % 8);  // G / 8 per queue
+      const int grid = F.persistent ? resident_grid(kern, lds, F.nunits) : F.nunits;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, L, F, lv, uv, d, v);
     };
     PNP_PAT_DISPATCH(nf, pat, {
