@@ -8,7 +8,8 @@ the bench line reports, by the kernel dispatched right before each one on the sa
   cold     -- after the 1 GiB k_scrub read (`roofline_cold`)
 and print per-regime launch counts and average / min / max durations, so each `frac` of the line
 follows from the committed profile (bytes per launch / average duration / 8 TB/s).
-usage: python tools/asm_regimes.py <run_kernel_trace.csv> <B_asm bytes> [out.json] [kernel substr]"""
+usage: python tools/asm_regimes.py <run_kernel_trace.csv> <B_asm bytes> [out.json] [kernel substr]
+       [grid size in threads: only launches of this grid, e.g. 738048 = config 3]"""
 import collections
 import csv
 import json
@@ -16,7 +17,8 @@ import sys
 
 path, b_asm = sys.argv[1], float(sys.argv[2])
 out_path = sys.argv[3] if len(sys.argv) > 3 else None
-key = sys.argv[4] if len(sys.argv) > 4 else "k_assemble_ga<0, 1, 3, 9, 6"
+key = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] else "k_assemble_ga<0, 1, 3, 9, 6"
+grid = sys.argv[5] if len(sys.argv) > 5 else None
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 last = {}
 run = {}
@@ -24,8 +26,12 @@ acc = collections.defaultdict(list)
 for r in rows:
     q = (r["Agent_Id"], r["Queue_Id"])
     name = r["Kernel_Name"]
-    if key in name:
+    if key in name and grid and r["Grid_Size_X"] != grid:
+        name = "(other grid) " + name  # another system's assembly: a predecessor like any kernel
+    if key in name and not name.startswith("(other grid)"):
         prev = last.get(q, "")
+        if prev.startswith("(other grid)"):
+            prev = "another system's assembly"
         run[q] = run.get(q, 0) + 1 if key in prev else 0
         if key in prev:
             reg = "warm" if run[q] >= 2 else "rewarm"
@@ -38,7 +44,8 @@ for r in rows:
         acc[reg].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
     if "__amd_rocclr" not in name:  # runtime copies / fills (scalar read-backs) do not count
         last[q] = name
-res = {"kernel": key, "bytes_per_launch": b_asm, "peak_gbs": 8000.0, "regimes": {}}
+res = {"kernel": key, "grid_threads": grid, "bytes_per_launch": b_asm, "peak_gbs": 8000.0,
+       "source": path, "regimes": {}}
 for reg, v in acc.items():
     avg = sum(v) / len(v)
     res["regimes"][reg] = {"launches": len(v), "avg_us": avg, "min_us": min(v), "max_us": max(v),
