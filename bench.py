@@ -74,6 +74,22 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
+ASM_REGIMES = os.path.join(ROOT, "profiles", "r04", "asm_regimes_config3_r4k.json")
+
+
+def profile_regime(name):
+    """The committed rocprofv3 trace's average for one assembly regime (tools/asm_regimes.py:
+    warm / in_situ / cold launches of the config-3 assembly), or None."""
+    try:
+        with open(ASM_REGIMES) as f:
+            d = json.load(f)
+        r = d["regimes"][name]
+        return {"avg_launch_us": r["avg_us"], "frac": r["frac"], "launches": r["launches"],
+                "source": os.path.relpath(ASM_REGIMES, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 BLAS_KERNELS = ("k_update_fwd0", "k_update_xr", "k_update_p", "k_reduce")
 
 
@@ -691,6 +707,7 @@ def main():
                                    "back launches",
                          "avg_launch_us_per_launch_events":
                              M["asm_warm_per_launch_events_s"] * 1e6,
+                         "profile": profile_regime("warm") if args.scaling == "weak" else None,
                          "note": "warm: back-to-back launches, the matrix write stream stays in "
                                  "the Infinity Cache at config 3 (partly on-die bandwidth); "
                                  "roofline_in_situ is the launch as Newton runs it, right after "
@@ -700,12 +717,15 @@ def main():
                                  "bytes_per_launch": asit["bytes"],
                                  "avg_launch_us": asit["seconds"] * 1e6,
                                  "frac_of_measured_copy": asit["achieved"] / copy_gbs,
+                                 "profile": (profile_regime("in_situ") if args.scaling == "weak"
+                                             else None),
                                  "timing": f"HIP event pair per launch, each launch right after "
                                            f"{args.bicg_iters} BiCGSTAB iterations"},
             "roofline_cold": {"bound": "hbm", "achieved": ac["achieved"], "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": ac["frac"], "bytes_per_launch": ac["bytes"],
                               "avg_launch_us": ac["seconds"] * 1e6,
                               "frac_of_measured_copy": ac["achieved"] / copy_gbs,
+                              "profile": profile_regime("cold") if args.scaling == "weak" else None,
                               "scrub": f"{SCRUB_BYTES >> 20} MiB read between launches"},
             "measured_copy_gbs": copy_gbs,
             "roofline_bicgstab": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
