@@ -403,8 +403,12 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>,
                                                  kB, 0);
-    const char *ev = std::getenv("PNP_NAT_FLOW_WG_PER_CU");  // A/B knob, capped at the occupancy
-    if (ev && std::atoi(ev) > 0) per = std::min(per, std::atoi(ev));
+    // 4 workgroups per CU (16 waves): fewer pollers than the occupancy allows and enough for
+    // the wide levels (PNP config 3: 2.25 ms per application against 2.36 at the occupancy, 2.94
+    // at 1; profiles/r04/nat_wg*_r4d.log).  PNP_NAT_FLOW_WG_PER_CU overrides (capped at the
+    // occupancy)
+    const char *ev = std::getenv("PNP_NAT_FLOW_WG_PER_CU");
+    per = std::min(per, (ev && std::atoi(ev) > 0) ? std::atoi(ev) : 4);
     return std::max(1, cus * std::max(1, per));
   }();
   hipError_t e = hipMemsetAsync(vf, 0xFF, sizeof(double) * size_t(n), s);
