@@ -340,7 +340,20 @@ struct pnp_ctx {
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
   bool use_graphs() const {
-    return graph_opt == 1 || (graph_opt < 0 && L.n_owned <= (1 << 17));
+    return graph_opt == 1 || (graph_opt < 0 && L.n_owned <= (1 << 17) && !profiled());
+  }
+  // rocprofv3 (ROCm 7.2) --kernel-trace dies with SIGSEGV once it has traced some 12,000-15,000
+  // graph-launched kernels, whatever the graph (tools/micro/graph_capture_prof.hip):
+  // under the profiler (its launcher exports ROCPROF_* variables) graph replay stays off unless
+  // PNP_OPT_GRAPH forces it; the eager launches give the same results bit for bit
+  static bool profiled() {
+    static const bool p = [] {
+      extern char **environ;
+      for (char **e = environ; e && *e; e++)
+        if (std::strncmp(*e, "ROCPROF_", 8) == 0) return true;
+      return false;
+    }();
+    return p;
   }
   struct GraphKey {
     int count, prec, fuse, nf, pat, f32;
@@ -1238,7 +1251,8 @@ struct pnp_ctx {
     // not with more than one rank: in-process ranks share the device, and another rank's thread
     // touching the legacy stream during a capture would invalidate it
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (!env_on || dist || nat_graph_failed || hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+    if (!env_on || dist || nat_graph_failed || profiled() ||
+        hipStreamIsCapturing(stream, &cs) != hipSuccess ||
         cs != hipStreamCaptureStatusNone)
       return issue();
     if (!nat_exec) {

@@ -8,3 +8,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-me
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u bench.py > $O/bench.log 2>&1; echo "bench rc=$?"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/gprof -o run -- python3 tools/graph_prof_check.py > $O/graph_prof_check.log 2>&1; echo "graph prof check rc=$?"
