@@ -230,14 +230,6 @@ struct pnp_ctx {
   std::vector<int4> nat_units;
   DBuf<int4> d_nat_units;
   int nat_units_f = 0, nat_tail_f = 0, nat_tail_b = 0;
-  // two levels per hop (k_ssor_nat_rflow): units {first position, rows, first parent, parents},
-  // parents' rows, per-CSR-entry parent slots of each sweep
-  std::vector<int4> nat_runits;
-  std::vector<int> nat_plist;
-  std::vector<signed char> nat_eslot_f, nat_eslot_b;
-  DBuf<int4> d_nat_runits;
-  DBuf<int> d_nat_plist;
-  DBuf<signed char> d_nat_eslot_f, d_nat_eslot_b;
   bool nat_units_ok = false;
   DBuf<unsigned> nat_abort;  // [0]: set by a sweep whose operand wait timed out (sticky)
   DBuf<int> csr_diag;        // index of each CSR-view row's diagonal entry
@@ -990,32 +982,6 @@ struct pnp_ctx {
           }
           const int rows = std::min(urows, lptr[l + 1] - t0);
           nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), nl, int(e0)));
-          // two levels per hop (k_ssor_nat_rflow): the distinct level-(l-1) dependencies of the
-          // unit's rows, recomputed by the unit; their entries' slots in eslot.  Past
-          // kRecMaxParents the unit reads them from memory like the flow kernel (eslot -1)
-          std::vector<int> par;
-          for (int t = t0; t < t0 + rows; t++) {
-            const int R = rl[t];
-            for (int k = cnt[R]; k < cnt[R + 1]; k++) {
-              const int C = col[k];
-              if (C != R && !empty(C) && (fwd ? C < R : C > R) && lev[C] == l - 1) par.push_back(C);
-            }
-          }
-          std::sort(par.begin(), par.end());
-          par.erase(std::unique(par.begin(), par.end()), par.end());
-          if (int(par.size()) > pnp::kRecMaxParents) par.clear();
-          std::vector<signed char> &es = fwd ? nat_eslot_f : nat_eslot_b;
-          if (es.empty()) es.assign(std::max<long long>(1, cnt[n]), (signed char)-1);
-          for (int t = t0; t < t0 + rows && !par.empty(); t++) {
-            const int R = rl[t];
-            for (int k = cnt[R]; k < cnt[R + 1]; k++) {
-              const int C = col[k];
-              if (C != R && !empty(C) && (fwd ? C < R : C > R) && lev[C] == l - 1)
-                es[k] = (signed char)(std::lower_bound(par.begin(), par.end(), C) - par.begin());
-            }
-          }
-          nat_runits.push_back(make_int4(t0, rows, int(nat_plist.size()), int(par.size())));
-          nat_plist.insert(nat_plist.end(), par.begin(), par.end());
         }
       }
       if (ltail >= nlev) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
@@ -1027,21 +993,9 @@ struct pnp_ctx {
       return upv(W.eidx, eidx, "natural SSOR entries");
     };
     nat_units.clear();
-    nat_runits.clear();
-    nat_plist.clear();
-    nat_eslot_f.clear();
-    nat_eslot_b.clear();
     nat_units_ok = true;
     if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
     if (nat_units_ok && (rc = upv(d_nat_units, nat_units, "natural SSOR units"))) return rc;
-    if (nat_units_ok) {  // two levels per hop (PNP_NAT_RECOMP)
-      if (nat_plist.empty()) nat_plist.push_back(0);
-      if ((rc = upv(d_nat_runits, nat_runits, "natural SSOR units")) ||
-          (rc = upv(d_nat_plist, nat_plist, "natural SSOR parents")) ||
-          (rc = upv(d_nat_eslot_f, nat_eslot_f, "natural SSOR parents")) ||
-          (rc = upv(d_nat_eslot_b, nat_eslot_b, "natural SSOR parents")))
-        return rc;
-    }
     if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess ||
         (e = nat_vf.alloc(std::max(1, n))) != hipSuccess || (e = nat_abort.alloc(4)) != hipSuccess ||
         (e = hipMemset(nat_abort.p, 0, 16)) != hipSuccess)
@@ -1092,19 +1046,6 @@ struct pnp_ctx {
     F.tail_b = nat_tail_b;
     F.chain_f = nat_f.chains();
     F.chain_b = nat_b.chains();
-    static const bool recomp = [] {
-      const char *ev = std::getenv("PNP_NAT_RECOMP");
-      return ev && std::atoi(ev) != 0;
-    }();
-    if (recomp) {
-      F.rec.runits = d_nat_runits.p;
-      F.rec.plist = d_nat_plist.p;
-      F.rec.eslot_f = d_nat_eslot_f.p;
-      F.rec.eslot_b = d_nat_eslot_b.p;
-      F.rec.rowptr = csr_rowptr.p;
-      F.rec.col = csr_col.p;
-      F.rec.diag = csr_diag.p;
-    }
     F.fwd = nat_f.view();
     F.bwd = nat_b.view();
     F.abort_word = nat_abort.p;

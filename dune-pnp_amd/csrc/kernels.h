@@ -460,8 +460,6 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
 // operand code in ecol (both forms): c >= 0 the forward value of row c, c == -1 zero, c <= -2 the
 // backward value of row -(c + 2).  vf / vb (n each): forward / backward results; abort_word[0]
 // is set when an operand wait times out.
-// the most level-(L-1) dependencies a unit recomputes (k_ssor_nat_rflow)
-constexpr int kRecMaxParents = 32;
 // rows per unit = rows per wavefront of the flow kernel (64 / its lanes per row)
 int ssor_natural_unit_rows();
 // the longest row the chain kernel takes (entries per lane group pass)
@@ -482,14 +480,6 @@ struct NatFlow {
     const int *gptr = nullptr, *ecode = nullptr, *eidx = nullptr;
     const int4 *rec = nullptr;
   } chain_f, chain_b;
-  // two levels per hop (k_ssor_nat_rflow, PNP_NAT_RECOMP), when runits != null: units {first
-  // sweep position, rows, first parent in plist, parents}, the CSR view (rowptr, col, diag) and
-  // per CSR entry its parent slot in its row's unit (eslot, one array per sweep)
-  struct Rec {
-    const int4 *runits = nullptr;
-    const int *plist = nullptr, *rowptr = nullptr, *col = nullptr, *diag = nullptr;
-    const signed char *eslot_f = nullptr, *eslot_b = nullptr;
-  } rec;
   NatSweep fwd, bwd;
   unsigned *abort_word = nullptr;
 };

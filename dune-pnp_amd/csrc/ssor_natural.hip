@@ -254,148 +254,6 @@ __global__ void __launch_bounds__(BLK)
 }
 constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
 
-// ---- two levels per hop: the parents recomputed (NatFlow::rec, PNP_NAT_RECOMP) -----------------
-// A row of level L waits for its dependencies on level L - 1 (1 or 2 of them for PB, up to 4 for
-// PNP; tools/nat_dag.py) and, through them, for level L - 2.  Here each unit first computes the
-// distinct level-(L-1) dependencies of its rows itself -- the same statements on the same final
-// operands, so the same bits -- into a per-wave LDS table, and its own rows take those operands
-// from the table: a unit then waits only for values of levels <= L - 2, so a hop spans two levels
-// and the critical path has half as many hops (PNP config 3: 696 -> 348).  The rows are read
-// straight from the CSR view (row-contiguous, ascending columns, the oracle's order), which the
-// parent recomputation reads as well.  eslot (per CSR entry, per sweep) names an entry's parent slot
-// in its row's unit, -1 when the operand is read from vf / vb as in k_ssor_nat_flow.
-// one row's SeqSSOR value (forward: 0 + 1.0 * ((d - sum) / a_RR); backward: v_f + 1.0 * (...)),
-// kL lanes, the head lane returns it; operands of the given eslot entries come from tab
-template <bool BWD>
-__device__ __forceinline__ double rec_row(int R, bool live, int j, int base, int lane,
-                                          const int *__restrict__ rowptr,
-                                          const int *__restrict__ col,
-                                          const double *__restrict__ val,
-                                          const int *__restrict__ diag,
-                                          const signed char *__restrict__ eslot,
-                                          const double *tab, const double *__restrict__ d,
-                                          unsigned long long *vf, unsigned long long *vb,
-                                          unsigned *abort_word) {
-  const int r0 = live ? rowptr[R] : 0, len = live ? rowptr[R + 1] - r0 : 0;
-  int c[kS], sl[kS];
-  double a[kS];
-  unsigned long long b[kS];
-#pragma unroll
-  for (int q = 0; q < kS; q++) {
-    const int k = j + q * kL;
-    const bool in = k < len;
-    c[q] = in ? col[r0 + k] : -1;
-    sl[q] = (in && eslot) ? int(eslot[r0 + k]) : -1;
-    a[q] = in ? val[r0 + k] : 0.0;
-  }
-  // operand codes as NatSweep's: forward -- the new value of an earlier row, else 0; backward --
-  // the forward value of rows <= R, the new backward value of later rows
-  auto addr = [&](int C) -> unsigned long long * {
-    if (C < 0) return nullptr;
-    if (!BWD) return C < R ? vf + C : nullptr;
-    return C <= R ? vf + C : vb + C;
-  };
-#pragma unroll
-  for (int q = 0; q < kS; q++) {
-    unsigned long long *p = sl[q] >= 0 ? nullptr : addr(c[q]);
-    b[q] = p ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-             : (sl[q] >= 0 ? (unsigned long long)__double_as_longlong(tab[sl[q]]) : 0ull);
-  }
-  bool pend = false;
-#pragma unroll
-  for (int q = 0; q < kS; q++) pend |= b[q] == kNatPending && sl[q] < 0 && addr(c[q]);
-  if (__any(pend)) {
-    const unsigned long long t0 = wall_clock64();
-    while (true) {
-      __builtin_amdgcn_s_sleep(1);
-      pend = false;
-#pragma unroll
-      for (int q = 0; q < kS; q++) {
-        unsigned long long *p = sl[q] >= 0 ? nullptr : addr(c[q]);
-        if (p && b[q] == kNatPending) {
-          b[q] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          pend |= b[q] == kNatPending;
-        }
-      }
-      if (!__any(pend)) break;
-      const bool late = wall_clock64() - t0 > kNatTimeout;
-      if (late && lane == 0)
-        __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-#pragma unroll
-        for (int q = 0; q < kS; q++)
-          if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;
-        break;
-      }
-    }
-  }
-  double pr[kS];
-#pragma unroll
-  for (int q = 0; q < kS; q++) {
-    const bool zero = sl[q] < 0 && !addr(c[q]);  // not an operand: the level kernel's 0.0
-    const double o = zero ? 0.0 : __longlong_as_double(b[q]);
-    pr[q] = (j + q * kL < len) ? a[q] * o : 0.0;
-  }
-  double rhs = (live && j == 0) ? d[R] : 0.0;
-#pragma unroll
-  for (int k = 0; k < kC; k++) {
-    const double p = __shfl(pr[k / kL], base + k % kL, 64);
-    if (j == 0 && k < len) rhs -= p;
-  }
-  double out = 0.0;
-  if (live && j == 0) {
-    const double own = BWD ? __longlong_as_double(__hip_atomic_load(vf + R, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT))
-                           : 0.0;
-    out = own + 1.0 * (rhs / val[diag[R]]);
-  }
-  return out;
-}
-
-// units {first sweep position, rows, first parent, parent count}; parents plist (row ids)
-__global__ void __launch_bounds__(kB)
-    k_ssor_nat_rflow(const int4 *__restrict__ units, int nunits, int nunits_f,
-                     const int4 *__restrict__ info_f, const int4 *__restrict__ info_b,
-                     const int *__restrict__ plist, const signed char *__restrict__ eslot_f,
-                     const signed char *__restrict__ eslot_b, const int *__restrict__ rowptr,
-                     const int *__restrict__ col, const double *__restrict__ val,
-                     const int *__restrict__ diag, const double *__restrict__ d,
-                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
-  __shared__ double tab[kB / 64][kRecMaxParents];
-  const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
-  const int w = threadIdx.x / 64;
-  const int G = gridDim.x * (kB / 64);
-  for (int u = blockIdx.x * (kB / 64) + w; u < nunits; u += G) {
-    const int4 U = units[u];
-    const bool bwd = u >= nunits_f;  // uniform
-    // phase A: the unit's parents, kL lanes each, 64 / kL per pass, into this wave's table
-    for (int pb = 0; pb < U.w; pb += 64 / kL) {
-      const int i = pb + t;
-      const bool live = i < U.w;
-      const int R = live ? plist[U.z + i] : 0;
-      const double v = bwd ? rec_row<true>(R, live, j, base, lane, rowptr, col, val, diag, nullptr,
-                                           nullptr, d, vf, vb, abort_word)
-                           : rec_row<false>(R, live, j, base, lane, rowptr, col, val, diag, nullptr,
-                                            nullptr, d, vf, vb, abort_word);
-      if (live && j == 0) tab[w][i] = v;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // phase B: the unit's own rows, parents' values from the table
-    const bool live = t < (U.y & 255);
-    const int4 I = live ? (bwd ? info_b : info_f)[U.x + t] : make_int4(0, 0, 0, 0);
-    const double v = bwd ? rec_row<true>(I.x, live, j, base, lane, rowptr, col, val, diag,
-                                         eslot_b, tab[w], d, vf, vb, abort_word)
-                         : rec_row<false>(I.x, live, j, base, lane, rowptr, col, val, diag,
-                                          eslot_f, tab[w], d, vf, vb, abort_word);
-    if (live && j == 0)
-      __hip_atomic_store(bwd ? vb + I.x : vf + I.x, (unsigned long long)__double_as_longlong(v),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_wave_barrier();  // the table is rewritten by the wave's next unit
-  }
-}
-
 // ---- the narrow tail as chains (NatChains, PNP_NAT_CHAIN) ---------------------------------------
 // In the narrow tail almost every row has exactly one dependency on the level just before its own
 // (pore_pnp k=4, PB forward: 60,851 of 61,851 tail rows; tools/nat_dag.py): the tail is a forest of
@@ -559,14 +417,6 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
   auto vfu = reinterpret_cast<unsigned long long *>(vf);
   auto vbu = reinterpret_cast<unsigned long long *>(vb);
   // [u0, u1) of one sweep: head units on the resident grid, tail units in one workgroup
-  if (F.rec.runits) {  // both sweeps, two levels per hop, one launch
-    const int blocks = std::min(grid, (F.nunits + kB / 64 - 1) / (kB / 64));
-    hipLaunchKernelGGL(k_ssor_nat_rflow, dim3(blocks), dim3(kB), 0, s, F.rec.runits, F.nunits,
-                       F.nunits_f, F.fwd.info, F.bwd.info, F.rec.plist, F.rec.eslot_f,
-                       F.rec.eslot_b, F.rec.rowptr, F.rec.col, val, F.rec.diag, d, vfu, vbu,
-                       F.abort_word);
-    return hipGetLastError();
-  }
   auto sweep = [&](int u0, int ut, int u1, const NatFlow::Chains &C, int bwd) {
     if (ut > u0) {
       const int blocks = std::min(grid, (ut - u0 + kB / 64 - 1) / (kB / 64));

@@ -1,5 +1,4 @@
-"""Natural-order SSOR schedule variants, -m gpu: tails as chains (PNP_NAT_CHAIN, k_ssor_nat_chain)
-and two levels per hop (PNP_NAT_RECOMP, k_ssor_nat_rflow), against the default dataflow;
+"""Natural-order SSOR tails as chains (PNP_NAT_CHAIN, ssor_natural.hip k_ssor_nat_chain), -m gpu:
 the chain kernel runs the level kernel's arithmetic per row, so applications, BiCGSTAB solves and
 PB / PNP Newton must be BITWISE the default schedule's -- with a threshold that makes every level
 a tail level (the whole sweep as chains), with a mid threshold (head as dataflow units, tail as
@@ -74,11 +73,6 @@ def run(**knobs):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")][-1]
     return json.loads(line[len("RESULT "):])
-
-
-def test_two_levels_per_hop_is_bitwise_the_dataflow_schedule():
-    """PNP_NAT_RECOMP: each unit recomputes its rows' level-(L-1) dependencies (k_ssor_nat_rflow)."""
-    assert run(FULL=1, PNP_NAT_RECOMP=1) == run(FULL=1)
 
 
 def test_chain_tails_are_bitwise_the_dataflow_schedule():
