@@ -942,16 +942,27 @@ struct pnp_ctx {
           std::vector<int> gptr(1, 0), ecode, eidx;
           std::vector<int4> rec;
           for (const auto &G : grows) {
-            for (int R : G) {
+            const int H = pnp::ssor_natural_chain_history();
+            for (size_t t = 0; t < G.size(); t++) {
+              const int R = G[t];
               const int len = cnt[R + 1] - cnt[R];
               rec.push_back(make_int4(R, len, diag[R], 0));
               for (int k = 0; k < wpad; k++) {
                 if (k < len) {
                   const int C = col[cnt[R] + k];
-                  ecode.push_back(empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2)));
+                  const int fc = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
+                  // kind: 0 zero, 1 forward value, 2 backward value, 3 in the wave's registers
+                  int code = fc == -1 ? 0 : fc >= 0 ? (fc << 2 | 1) : ((-(fc + 2)) << 2 | 2);
+                  const bool fresh = fwd ? (code & 3) == 1 : (code & 3) == 2;  // this sweep's value
+                  for (int h = 1; fresh && h <= H && size_t(h) <= t; h++)
+                    if (G[t - h] == C) {
+                      code = h << 2 | 3;
+                      break;
+                    }
+                  ecode.push_back(code);
                   eidx.push_back(cnt[R] + k);
                 } else {
-                  ecode.push_back(-1);
+                  ecode.push_back(0);
                   eidx.push_back(-1);
                 }
               }

@@ -462,9 +462,11 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
 // is set when an operand wait times out.
 // rows per unit = rows per wavefront of the flow kernel (64 / its lanes per row)
 int ssor_natural_unit_rows();
-// the longest row the chain kernel takes (entries per lane group pass)
+// the longest row the chain kernel takes (one entry per lane of its wave)
 int ssor_natural_chain_width();
-// lane groups of the chain kernel resident at once on this device
+// results the chain kernel keeps in registers (operand kind 3 reaches back this many rows)
+int ssor_natural_chain_history();
+// groups (one wave each) of the chain kernel resident at once on this device
 int ssor_natural_chain_capacity();
 struct NatFlow {
   const int4 *units = nullptr;
@@ -472,9 +474,10 @@ struct NatFlow {
   // first unit of each sweep's narrow tail (levels of at most PNP_NAT_TAIL / PNP_NAT_CHAIN rows to
   // the sweep's end): forward [tail_f, nunits_f), backward [tail_b, nunits)
   int tail_f = 0, tail_b = 0;
-  // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: lane group g walks
-  // rows gptr[g] .. gptr[g+1] of rec ({ext row, entry count, diagonal value index, 0}); row q's
-  // entries at q * wpad .. + count of ecode (operand codes, as NatFlow's) and eidx (value indices)
+  // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: the wave of group g
+  // walks rows gptr[g] .. gptr[g+1] of rec ({ext row, entry count, diagonal value index, 0}); row
+  // q's entries at q * wpad .. + count of ecode (idx << 2 | kind: 0 zero, 1 vf[idx], 2 vb[idx],
+  // 3 the group's result idx rows back) and eidx (value indices, -1 padding)
   struct Chains {
     int ngroups = 0, wpad = 0;
     const int *gptr = nullptr, *ecode = nullptr, *eidx = nullptr;

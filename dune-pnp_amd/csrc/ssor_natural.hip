@@ -128,7 +128,9 @@ __device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p
   return __hip_atomic_load(p, __ATOMIC_RELAXED, SCOPE);
 }
 
-template <int BLK, int SCOPE>
+// PAD > 0: the workgroup reserves PAD bytes of LDS it never uses, so that at most one workgroup
+// runs per CU (the sparse tail grid, below)
+template <int BLK, int SCOPE, int PAD = 0>
 __global__ void __launch_bounds__(BLK)
     k_ssor_nat_flow(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
                     const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
@@ -136,6 +138,10 @@ __global__ void __launch_bounds__(BLK)
                     const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
                     const double *__restrict__ val, const double *__restrict__ d,
                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
+  if constexpr (PAD > 0) {
+    __shared__ char pad[PAD];
+    if (u0 < 0) reinterpret_cast<volatile char *>(pad)[threadIdx.x] = 1;  // never: u0 >= 0
+  }
   const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
   const int G = gridDim.x * (BLK / 64);
   for (int u = u0 + blockIdx.x * (BLK / 64) + threadIdx.x / 64; u < u1; u += G) {
@@ -253,146 +259,147 @@ __global__ void __launch_bounds__(BLK)
   }
 }
 constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
+// The sparse tail grid (PNP_NAT_TAIL_WPC = 1, 2 or 4 waves per CU): the tail levels on a grid of
+// at most one workgroup per CU (96 KB of LDS reserved each), so that a consumer CU's memory queue
+// holds only its own few waves' polls -- the hand-off price sits in the consumer CU's queue
+// (MI355X_MICROARCH.md handoff-1to1: 0.8-1.1 us between unloaded CUs, 2.3-3.5 us with 8-15 busy
+// waves on them), and the head grid's 16 polling waves per CU pay the latter on every tail level.
+constexpr int kTailPad = 96 * 1024;
 
 // ---- the narrow tail as chains (NatChains, PNP_NAT_CHAIN) ---------------------------------------
-// In the narrow tail almost every row has exactly one dependency on the level just before its own
-// (pore_pnp k=4, PB forward: 60,851 of 61,851 tail rows; tools/nat_dag.py): the tail is a forest of
-// chains.  The host cuts it into heavy paths (each row continues the chain of the child with the
-// longest remaining path) and packs the chains into lane groups by level interval; a group of kL
-// lanes walks its rows in order, and a row's dependency on the two rows the group computed just
-// before it is taken from their results in the group's registers -- no memory hop.  Other operands
-// are polled as in the flow kernel.  Each group advances on its own: every pass, the groups whose
-// current row has all its operands compute it and move on, the others poll again, so a group never
-// waits for a group of its own wave.  The next two rows' records, entries, values and operands are
-// in flight while the current one waits or computes.  The arithmetic is the level kernel's (products in
-// column order subtracted by the row's first lane), so the result is the oracle's bit for bit.
-// Progress: a row depends only on rows of lower levels; a group's rows are in increasing level
-// order; the lowest pending row over all groups has all its operands, and its group computes it in
-// the next pass (every group of the small grid resident, one context per stream).
-struct ChainStage {
-  int4 rec;                  // {row, entry count, diagonal value index, 0}; row < 0: none
-  int c[kS], ix[kS];         // operand codes and value indices of this lane's entries
-  double a[kS];              // values
-  unsigned long long b[kS];  // operands (kNatPending: not final yet)
-  double d0, own, adiag;     // the row's first lane: d, its forward value (backward), a_RR
-};
+// In the narrow tail almost every row depends on exactly one row of the level just before its own
+// (pore_pnp k=4, PB forward: 60,851 of 61,851 tail rows; tools/nat_dag.py): the tail is a forest.
+// The host cuts it into heavy paths (each row continues the chain of its child with the longest
+// remaining path) and packs the chains into groups by level interval; ONE WAVE walks a group's rows
+// in order, lane k holding the row's entry k.  A row's operands that are the results of the group's
+// last kChainH rows are taken from the wave's registers (the host marks them), so a step along a
+// chain costs the row's arithmetic, not a memory hop.  Other operands are polled as in the flow
+// kernel (write-through stores of final values into all-ones vectors).
+// Software pipeline, so that a step waits for no memory: the row's record and entry codes are
+// loaded 2D steps ahead (stage A), its values, d, a_RR and operands D steps ahead (stage B, from
+// stage A's indices); the loop is unrolled by 2D so that every stage lives in fixed registers,
+// and every load is unconditional (positions clamped to the group's last row), so the compiler
+// can count the loads in flight instead of draining them (round 4's first chain kernel kept its
+// stages in rotating structs with predicated loads and waited for every load every step:
+// profiles/r04/ssor_natural_chain_r4j.log).
+// The arithmetic is the level kernel's: products a_RC * v_C in column order, subtracted from d_R
+// one by one, forward 0.0 + 1.0 * (rhs / a_RR), backward v_R + 1.0 * (rhs / a_RR): the oracle's
+// SeqSSOR bit for bit.
+// Progress: a row depends only on rows of lower levels and a group's rows are in increasing level
+// order, so the lowest uncomputed row's group is at that row and its operands are final; every
+// group's wave is resident (the host packs at most ssor_natural_chain_capacity() groups).
+// Operand codes (host): idx << 2 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
+// result idx (1..kChainH) rows back.
+#ifndef NAT_CHAIN_D
+#define NAT_CHAIN_D 4  // build-flag A/B knob: stage-B lead in steps (stage A leads by twice that)
+#endif
+constexpr int kChainD = NAT_CHAIN_D, kChainA = 2 * kChainD, kChainH = 4;
 
-__global__ void __launch_bounds__(kB)
-    k_ssor_nat_chain(const int *__restrict__ gptr, int ngroups, const int4 *__restrict__ rec,
+__global__ void __launch_bounds__(64)
+    k_ssor_nat_chain(const int *__restrict__ gptr, const int4 *__restrict__ rec,
                      const int *__restrict__ ecode, const int *__restrict__ eidx, int wpad,
                      const double *__restrict__ val, const double *__restrict__ d,
                      unsigned long long *vf, unsigned long long *vb, int bwd,
                      unsigned *abort_word) {
-  const int lane = threadIdx.x % 64, j = lane % kL, base = lane - j;
-  const int g = (blockIdx.x * kB + int(threadIdx.x)) / kL;
-  const bool gl = g < ngroups;
-  int p = gl ? gptr[g] : 0;
-  const int pend = gl ? gptr[g + 1] : 0;
-  unsigned long long *out = bwd ? vb : vf;
-  auto op_addr = [&](int c) { return c >= 0 ? vf + c : vb + (-(c + 2)); };
+  constexpr int D = kChainD, A = kChainA;
+  const int lane = threadIdx.x;
+  const int p0 = gptr[blockIdx.x], len = gptr[blockIdx.x + 1] - p0;
+  if (len <= 0) return;
+  const int kl = lane < wpad ? lane : wpad - 1;
   auto ld = [&](const unsigned long long *q) {
     return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  // the operand code under which a row's own result is read by later rows of its sweep
-  auto code_of = [&](int row) { return row < 0 ? INT_MIN : (bwd ? -(row + 2) : row); };
-  auto load_rec = [&](int q, ChainStage &S) {
-    const bool in = q < pend;
-    S.rec = in ? rec[q] : make_int4(-1, 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < kS; u++) {
-      const int k = j + u * kL;
-      const bool e = in && k < wpad;
-      S.c[u] = e ? ecode[size_t(q) * wpad + k] : -1;
-      S.ix[u] = e ? eidx[size_t(q) * wpad + k] : -1;
-    }
+  auto opnd = [&](int c) {  // the operand's address (kind 0 and 3: a harmless dummy)
+    const int k = c & 3, i = c >> 2;
+    return k == 1 ? vf + i : k == 2 ? vb + i : vf;
   };
-  // values, d, a_RR and the operands of a staged row; operands that are the results of the two
-  // rows this group computes just before it (codes k1, k2) are not loaded: they are taken from the
-  // group's registers when the row is computed
-  auto load_vals = [&](ChainStage &S, int k1, int k2) {
-#pragma unroll
-    for (int u = 0; u < kS; u++) {
-      S.a[u] = S.ix[u] >= 0 ? val[S.ix[u]] : 0.0;
-      S.b[u] = (S.c[u] == -1 || S.c[u] == k1 || S.c[u] == k2) ? 0ull : ld(op_addr(S.c[u]));
-    }
-    const bool h = S.rec.x >= 0 && j == 0;
-    S.d0 = h ? d[S.rec.x] : 0.0;
-    S.own = (h && bwd) ? __longlong_as_double(ld(vf + S.rec.x)) : 0.0;
-    S.adiag = h ? val[S.rec.z] : 1.0;
+  int4 ra[A];
+  int ca[A], xa[A];
+  double av[D], dv[D], ov[D], gv[D];
+  unsigned long long bv[D];
+  auto stage_a = [&](int s, int slot) {
+    const int p = p0 + (s < len ? s : len - 1);
+    ra[slot] = rec[p];
+    ca[slot] = ecode[size_t(p) * wpad + kl];
+    xa[slot] = eidx[size_t(p) * wpad + kl];
   };
-  ChainStage s0, s1, s2;  // s0: the current row; s1, s2: the next two, values and operands issued
-  load_rec(p, s0);
-  load_rec(p + 1, s1);
-  load_rec(p + 2, s2);
-  // the group's last two results (head lane) and their operand codes
-  int code1 = INT_MIN, code2 = INT_MIN;
-  double val1 = 0.0, val2 = 0.0;
-  load_vals(s0, INT_MIN, INT_MIN);
-  load_vals(s1, code_of(s0.rec.x), INT_MIN);
-  load_vals(s2, code_of(s1.rec.x), code_of(s0.rec.x));
-  unsigned long long t0 = wall_clock64();
-  while (__any(p < pend)) {
-    const bool act = p < pend;
-    const double pv1 = __shfl(val1, base, 64), pv2 = __shfl(val2, base, 64);
-    bool wait = false;
+  auto stage_b = [&](int sa, int sb) {
+    av[sb] = val[xa[sa] >= 0 ? xa[sa] : 0];
+    bv[sb] = ld(opnd(ca[sa]));
+    dv[sb] = d[ra[sa].x];
+    ov[sb] = __longlong_as_double(ld(vf + ra[sa].x));  // the forward value (backward sweep)
+    gv[sb] = val[ra[sa].z];
+  };
 #pragma unroll
-    for (int u = 0; u < kS; u++)
-      if (act && s0.c[u] != -1 && s0.c[u] != code1 && s0.c[u] != code2 &&
-          s0.b[u] == kNatPending) {
-        s0.b[u] = ld(op_addr(s0.c[u]));
-        wait |= s0.b[u] == kNatPending;
+  for (int i = 0; i < A; i++) stage_a(i, i);
+#pragma unroll
+  for (int i = 0; i < D; i++) stage_b(i, i);
+  double h1 = 0.0, h2 = 0.0, h3 = 0.0, h4 = 0.0;  // the group's last results
+  for (int s = 0; s < len; s += A) {
+#pragma unroll
+    for (int i = 0; i < A; i++) {
+      const int st = s + i;
+      if (st < len) {  // uniform
+        const int c = ca[i], kind = c & 3, width = ra[i].y;
+        const bool live = lane < width;
+        unsigned long long b = bv[i % D];
+        bool pend = live && (kind == 1 || kind == 2) && b == kNatPending;
+        if (__any(pend)) {
+          const unsigned long long t0 = wall_clock64();
+          while (true) {
+            __builtin_amdgcn_s_sleep(1);
+            if (pend) {
+              b = ld(opnd(c));
+              pend = b == kNatPending;
+            }
+            if (!__any(pend)) break;
+            const bool late = wall_clock64() - t0 > kNatTimeout;
+            if (late && lane == 0)
+              __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              if (pend) b = 0x7FF8000000000000ull;  // NaN: drain the grid
+              break;
+            }
+          }
+        }
+        const int hi = c >> 2;
+        const double hv = hi == 1 ? h1 : hi == 2 ? h2 : hi == 3 ? h3 : h4;
+        const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);
+        const double pr = (live && xa[i] >= 0) ? av[i % D] * o : 0.0;
+        const unsigned long long pb = __double_as_longlong(pr);
+        const int plo = int(unsigned(pb)), phi = int(unsigned(pb >> 32));
+        double rhs = dv[i % D];
+        for (int k = 0; k < width; k++) {
+          const unsigned lo = unsigned(__builtin_amdgcn_readlane(plo, k));
+          const unsigned hh = unsigned(__builtin_amdgcn_readlane(phi, k));
+          rhs -= __longlong_as_double((long long)((unsigned long long)hh << 32 | lo));
+        }
+        const double own = bwd ? ov[i % D] : 0.0;
+        const double out = own + 1.0 * (rhs / gv[i % D]);
+        if (lane == 0)
+          __hip_atomic_store((bwd ? vb : vf) + ra[i].x, (unsigned long long)__double_as_longlong(out),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h4 = h3;
+        h3 = h2;
+        h2 = h1;
+        h1 = out;
       }
-    const unsigned long long wm = __ballot(wait);
-    const bool ready = act && ((wm >> base) & ((1ull << kL) - 1)) == 0;
-    double pr[kS];
-#pragma unroll
-    for (int u = 0; u < kS; u++) {
-      const double o = s0.c[u] == -1      ? 0.0
-                       : s0.c[u] == code1 ? pv1
-                       : s0.c[u] == code2 ? pv2
-                                          : __longlong_as_double(s0.b[u]);
-      pr[u] = s0.ix[u] >= 0 ? s0.a[u] * o : 0.0;
-    }
-    double rhs = s0.d0;
-    const int width = s0.rec.y;
-#pragma unroll
-    for (int k = 0; k < kC; k++) {
-      const double q = __shfl(pr[k / kL], base + k % kL, 64);
-      if (j == 0 && k < width) rhs -= q;
-    }
-    if (ready) {
-      code2 = code1;
-      val2 = val1;
-      code1 = code_of(s0.rec.x);
-      if (j == 0) {
-        const double res = s0.own + 1.0 * (rhs / s0.adiag);
-        __hip_atomic_store(out + s0.rec.x, (unsigned long long)__double_as_longlong(res),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        val1 = res;
-      }
-      t0 = wall_clock64();
-      p++;
-      s0 = s1;
-      s1 = s2;
-      load_rec(p + 2, s2);
-      load_vals(s2, code_of(s1.rec.x), code_of(s0.rec.x));
-    } else if (act && wall_clock64() - t0 > kNatTimeout) {
-      if (lane == 0)
-        __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;  // results void; the host reports the timeout
+      stage_b((i + D) % A, i % D);  // step st + D
+      stage_a(st + A, i);           // step st + A
     }
   }
 }
 }  // namespace
 
 int ssor_natural_unit_rows() { return 64 / kL; }
-int ssor_natural_chain_width() { return kC; }
+int ssor_natural_chain_width() { return 64; }
+int ssor_natural_chain_history() { return kChainH; }
 int ssor_natural_chain_capacity() {
   int dev = 0, cus = 0, per = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_chain, kB, 0);
-  return cus * std::max(1, per) * (kB / kL);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_chain, 64, 0);
+  return cus * std::max(1, per);
 }
 
 hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
@@ -411,6 +418,16 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     per = std::min(per, (ev && std::atoi(ev) > 0) ? std::atoi(ev) : 4);
     return std::max(1, cus * std::max(1, per));
   }();
+  static const int cus = [] {
+    int dev = 0, c = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, c);
+  }();
+  static const int tail_wpc = [] {
+    const char *ev = std::getenv("PNP_NAT_TAIL_WPC");
+    return ev ? std::max(0, std::atoi(ev)) : 0;
+  }();
   hipError_t e = hipMemsetAsync(vf, 0xFF, sizeof(double) * size_t(n), s);
   if (e == hipSuccess) e = hipMemsetAsync(vb, 0xFF, sizeof(double) * size_t(n), s);
   if (e != hipSuccess) return e;
@@ -425,10 +442,20 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
                          F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
     }
     if (u1 > ut && C.ngroups > 0)
-      hipLaunchKernelGGL(k_ssor_nat_chain, dim3((C.ngroups * kL + kB - 1) / kB), dim3(kB), 0, s,
-                         C.gptr, C.ngroups, C.rec, C.ecode, C.eidx, C.wpad, val, d, vfu, vbu, bwd,
-                         F.abort_word);
-    else if (u1 > ut)
+      hipLaunchKernelGGL(k_ssor_nat_chain, dim3(C.ngroups), dim3(64), 0, s, C.gptr, C.rec, C.ecode,
+                         C.eidx, C.wpad, val, d, vfu, vbu, bwd, F.abort_word);
+    else if (u1 > ut && tail_wpc > 0) {
+      const int per = tail_wpc >= 4 ? 4 : tail_wpc >= 2 ? 2 : 1;
+      const int blocks = std::min(cus, (u1 - ut + per - 1) / per);
+#define NAT_TAIL_GRID(W)                                                                          \
+  hipLaunchKernelGGL((k_ssor_nat_flow<64 * W, __HIP_MEMORY_SCOPE_AGENT, kTailPad>), dim3(blocks), \
+                     dim3(64 * W), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,     \
+                     F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word)
+      if (per == 1) NAT_TAIL_GRID(1);
+      else if (per == 2) NAT_TAIL_GRID(2);
+      else NAT_TAIL_GRID(4);
+#undef NAT_TAIL_GRID
+    } else if (u1 > ut)
       hipLaunchKernelGGL((k_ssor_nat_flow<kTailBlk, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3(1),
                          dim3(kTailBlk), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,
                          F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
