@@ -480,6 +480,36 @@ def rccl_parity(sctx, smesh, scfg, x0, rank, world, local, dist):
     return out
 
 
+def ssork_natural_leg(ctx, mesh, x0, nit):
+    """The reference's default linear solver, BCGS_SSORk (BiCGSTAB + ISTL SeqSSOR in the
+    reference's DOF order, PNP_PREC_SSOR_NATURAL: bitwise the oracle's SeqSSOR), on the config-3
+    PNP system at x0 and on the PB system at its potential: one preconditioner application (device
+    timers: forward + backward sweep, scatter and gather) and one BiCGSTAB iteration (two
+    applications, two SpMVs, the reductions), after two untimed iterations (N=1 only: the one-launch
+    dataflow schedule needs the whole device)."""
+    out = {}
+    nv = mesh.nv
+    for name, op, x in (("pnp", P.OP_PNP, x0), ("pb", P.OP_PB, x0[:nv])):
+        ctx.set_operator(op)
+        ctx.state_set(x)
+        ctx.assemble_state(1)
+        ctx.bicgstab_iterations(2, P.PREC_SSOR_NATURAL)
+        t0 = time.perf_counter()
+        ctx.bicgstab_iterations(nit, P.PREC_SSOR_NATURAL)
+        wall = (time.perf_counter() - t0) / nit
+        ctx.timers(enable=True, reset=True)
+        ctx.bicgstab_iterations(nit, P.PREC_SSOR_NATURAL)
+        tm = ctx.timers(enable=False)
+        ctx.timers(reset=True)
+        out[name] = {"dofs": int(len(x)), "ms_per_apply": tm["prec_ms"] / max(1, tm["prec_launches"]),
+                     "ms_per_iter": 1e3 * wall, "iters_per_s": 1.0 / wall}
+    ctx.set_operator(P.OP_PNP)
+    out["schedule"] = ("forward and backward sweep each: the wide levels as dataflow units, the "
+                       "narrow ones (at most the resident chain groups' count of rows) as chains, "
+                       "one wave per chain group (ssor_natural.hip)")
+    return out
+
+
 def strong_mesh(refine):
     cfg = P.read_config(os.path.join(ROOT, "data", "pore_without_dna", "pore.cfg"))
     return cfg, P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(refine)
@@ -513,6 +543,8 @@ def main():
                     help="skip the AMG-preconditioned time-to-solution leg")
     ap.add_argument("--amg-multi", action="store_true",
                     help="run the AMG time-to-solution leg at N>1 too (default: N=1 only)")
+    ap.add_argument("--no-ssork", action="store_true",
+                    help="skip the BCGS_SSORk (natural-order SSOR) leg")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the multi-GPU self-check (rccl_parity) on the config-5 system")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -601,6 +633,9 @@ def main():
                       "preconditioner": "amg (ILU0 smoother, 2 block-Jacobi sweeps omega=0.8 "
                                         "on the coarse levels)",
                       "amg_rows": ctx.amg_info()["rows"]}
+    ssork = None
+    if world == 1 and not args.no_ssork:
+        ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters)
     ctx.close()
 
     # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
@@ -758,6 +793,7 @@ def main():
             "pnp_newton_time_to_solution": newton,
             "pnp_newton_time_to_solution_f64_factors": newton_f64,
             "pnp_newton_time_to_solution_amg": newton_amg,
+            "bicgstab_ssork_natural": ssork,
             "strong_scaling": strong,
             "rccl_parity": parity,
         }

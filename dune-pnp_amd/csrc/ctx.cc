@@ -863,10 +863,14 @@ struct pnp_ctx {
         const char *ev = std::getenv("PNP_NAT_TAIL");
         return ev ? std::max(0, std::atoi(ev)) : 0;
       }();
-      // PNP_NAT_CHAIN (rows): the tail as chains instead (k_ssor_nat_chain; takes precedence)
+      // PNP_NAT_CHAIN (rows): the tail as chains (k_ssor_nat_chain; takes precedence over
+      // PNP_NAT_TAIL).  Default: the levels of at most as many rows as the chain kernel keeps
+      // groups resident (8,192 on MI355X), so that no two chains share a group at one level
+      // (pore_pnp k=4 per application, PB 1.31 -> 0.57 ms, PNP config 3 2.22 -> 1.57 ms;
+      // threshold sweep profiles/r04/chain2/).  PNP_NAT_CHAIN=0: dataflow units only
       static const int chain_rows = [] {
         const char *ev = std::getenv("PNP_NAT_CHAIN");
-        return ev ? std::max(0, std::atoi(ev)) : 0;
+        return ev ? std::max(0, std::atoi(ev)) : std::max(0, pnp::ssor_natural_chain_capacity());
       }();
       const int trows = chain_rows > 0 ? chain_rows : tail_rows;
       int ltail = nlev;

@@ -291,9 +291,12 @@ constexpr int kTailPad = 96 * 1024;
 // Operand codes (host): idx << 2 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
 // result idx (1..kChainH) rows back.
 #ifndef NAT_CHAIN_D
-#define NAT_CHAIN_D 4  // build-flag A/B knob: stage-B lead in steps (stage A leads by twice that)
+#define NAT_CHAIN_D 2  // build-flag A/B knob: stage-B lead in steps (stage A leads by twice that)
 #endif
-constexpr int kChainD = NAT_CHAIN_D, kChainA = 2 * kChainD, kChainH = 4;
+#ifndef NAT_CHAIN_H
+#define NAT_CHAIN_H 4  // build-flag A/B knob: results kept in registers
+#endif
+constexpr int kChainD = NAT_CHAIN_D, kChainA = 2 * kChainD, kChainH = NAT_CHAIN_H;
 
 __global__ void __launch_bounds__(64)
     k_ssor_nat_chain(const int *__restrict__ gptr, const int4 *__restrict__ rec,
@@ -334,7 +337,9 @@ __global__ void __launch_bounds__(64)
   for (int i = 0; i < A; i++) stage_a(i, i);
 #pragma unroll
   for (int i = 0; i < D; i++) stage_b(i, i);
-  double h1 = 0.0, h2 = 0.0, h3 = 0.0, h4 = 0.0;  // the group's last results
+  double h[kChainH];  // the group's last results, h[0] the latest
+#pragma unroll
+  for (int q = 0; q < kChainH; q++) h[q] = 0.0;
   for (int s = 0; s < len; s += A) {
 #pragma unroll
     for (int i = 0; i < A; i++) {
@@ -363,7 +368,10 @@ __global__ void __launch_bounds__(64)
           }
         }
         const int hi = c >> 2;
-        const double hv = hi == 1 ? h1 : hi == 2 ? h2 : hi == 3 ? h3 : h4;
+        double hv = h[0];
+#pragma unroll
+        for (int q = 1; q < kChainH; q++)
+          if (hi == q + 1) hv = h[q];
         const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);
         const double pr = (live && xa[i] >= 0) ? av[i % D] * o : 0.0;
         const unsigned long long pb = __double_as_longlong(pr);
@@ -379,10 +387,9 @@ __global__ void __launch_bounds__(64)
         if (lane == 0)
           __hip_atomic_store((bwd ? vb : vf) + ra[i].x, (unsigned long long)__double_as_longlong(out),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h4 = h3;
-        h3 = h2;
-        h2 = h1;
-        h1 = out;
+#pragma unroll
+        for (int q = kChainH - 1; q > 0; q--) h[q] = h[q - 1];
+        h[0] = out;
       }
       stage_b((i + D) % A, i % D);  // step st + D
       stage_a(st + A, i);           // step st + A

@@ -1,9 +1,10 @@
 """Natural-order SSOR tails as chains (PNP_NAT_CHAIN, ssor_natural.hip k_ssor_nat_chain), -m gpu:
 the chain kernel runs the level kernel's arithmetic per row, so applications, BiCGSTAB solves and
-PB / PNP Newton must be BITWISE the default schedule's -- with a threshold that makes every level
-a tail level (the whole sweep as chains), with a mid threshold (head as dataflow units, tail as
-chains), and on the config-3 system.  The knob is read once per process: each setting runs in a
-child process."""
+PB / PNP Newton must be BITWISE the dataflow-units-only schedule's (PNP_NAT_CHAIN=0) -- with the
+default threshold (the resident-group capacity), with one that makes every level a tail level (the
+whole sweep as chains, groups shared past the capacity), with a small one (head as dataflow units,
+tail as chains), and on the config-3 system.  The knob is read once per process: each setting runs
+in a child process."""
 import json
 import os
 import subprocess
@@ -76,6 +77,7 @@ def run(**knobs):
 
 
 def test_chain_tails_are_bitwise_the_dataflow_schedule():
-    ref = run(FULL=1)
+    ref = run(FULL=1, PNP_NAT_CHAIN=0)
+    assert run(FULL=1) == ref  # the default threshold
     assert run(FULL=1, PNP_NAT_CHAIN=1 << 30) == ref  # every level a tail level: all chains
     assert run(FULL=1, PNP_NAT_CHAIN=2048) == ref
