@@ -229,7 +229,7 @@ struct pnp_ctx {
   // the one-launch dataflow sweep (launch_ssor_natural_flow): units, forward units first
   std::vector<int4> nat_units;
   DBuf<int4> d_nat_units;
-  int nat_units_f = 0, nat_tail_f = 0, nat_tail_b = 0;
+  int nat_units_f = 0, nat_tail_f = 0, nat_tail_b = 0, nat_max_width = 0;
   bool nat_units_ok = false;
   DBuf<unsigned> nat_abort;  // [0]: set by a sweep whose operand wait timed out (sticky)
   DBuf<int> csr_diag;        // index of each CSR-view row's diagonal entry
@@ -997,6 +997,7 @@ struct pnp_ctx {
           }
           const int rows = std::min(urows, lptr[l + 1] - t0);
           nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), nl, int(e0)));
+          nat_max_width = std::max(nat_max_width, int(w));
         }
       }
       if (ltail >= nlev) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
@@ -1009,6 +1010,7 @@ struct pnp_ctx {
     };
     nat_units.clear();
     nat_units_ok = true;
+    nat_max_width = 0;
     if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
     if (nat_units_ok && (rc = upv(d_nat_units, nat_units, "natural SSOR units"))) return rc;
     if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess ||
@@ -1059,6 +1061,7 @@ struct pnp_ctx {
     F.nunits_f = nat_units_f;
     F.tail_f = nat_tail_f;
     F.tail_b = nat_tail_b;
+    F.max_width = nat_max_width;
     F.chain_f = nat_f.chains();
     F.chain_b = nat_b.chains();
     F.fwd = nat_f.view();

@@ -474,6 +474,7 @@ struct NatFlow {
   // first unit of each sweep's narrow tail (levels of at most PNP_NAT_TAIL / PNP_NAT_CHAIN rows to
   // the sweep's end): forward [tail_f, nunits_f), backward [tail_b, nunits)
   int tail_f = 0, tail_b = 0;
+  int max_width = 0;  // the longest row of any unit (the pipelined head takes up to 24 entries)
   // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: the wave of group g
   // walks rows gptr[g] .. gptr[g+1] of rec ({ext row, entry count, diagonal value index, 0}); row
   // q's entries at q * wpad .. + count of ecode (idx << 2 | kind: 0 zero, 1 vf[idx], 2 vb[idx],

@@ -111,6 +111,14 @@ __global__ void __launch_bounds__(kB)
 #define NAT_POLL_DEPTH 1  // build-flag A/B knob: polls in flight per pending operand
 #endif
 constexpr unsigned long long kNatPending = ~0ull;
+#ifndef NAT_BACKOFF_MAX
+#define NAT_BACKOFF_MAX 1  // build-flag A/B knob: longest pause between polls, in s_sleep 1 units
+#endif
+// the pause before the next poll of a wait: 1, 2, 4, ... NAT_BACKOFF_MAX s_sleep 1 periods
+__device__ __forceinline__ void nat_backoff(int &k) {
+  for (int i = 0; i < k; i++) __builtin_amdgcn_s_sleep(1);
+  k = k * 2 < NAT_BACKOFF_MAX ? k * 2 : NAT_BACKOFF_MAX;
+}
 constexpr unsigned long long kNatTimeout = 100000000ull;  // wall_clock64 ticks (100 MHz): 1 s
 
 // The sweeps' tails (PNP_NAT_TAIL, off by default): the natural order's dependency graph is wide
@@ -258,6 +266,165 @@ __global__ void __launch_bounds__(BLK)
     }
   }
 }
+// The same dataflow, software-pipelined across a wave's units (the default head; units of at most
+// kC entries per row, one pass).  The flow kernel above starts loading a unit's entries only when
+// it has finished its previous one: two dependent round trips (ELL slots, then values and
+// operands) land on the critical path of every level a wave joins late, ~4.3 us per wide level
+// against ~2.4 for a hop (PNP config 3, profiles/r04/chain2/nat_split_d4_8192.txt).  Here the
+// wave holds three units at once: it computes unit k while unit k+1's values, d, a_RR and first
+// operand loads (stage B, from unit k+1's ELL slots) and unit k+2's record and ELL slots (stage
+// A) are in flight.  Each stage has one register set, read before it is reloaded, and every load
+// is unconditional (positions clamped into the unit, padding selected afterwards), so the waits
+// count loads instead of draining them.  Operands still pending at compute time are polled as in
+// the flow kernel; the arithmetic is the flow kernel's, bit for bit.
+template <int BLK>
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
+    k_ssor_nat_pipe(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
+                    const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
+                    const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
+                    const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
+                    const double *__restrict__ val, const double *__restrict__ d,
+                    unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
+  const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
+  const int G = gridDim.x * (BLK / 64);
+  // wave-uniform (readfirstlane): the unit records become scalar loads, off the vector counter
+  const int ufirst =
+      __builtin_amdgcn_readfirstlane(u0 + blockIdx.x * (BLK / 64) + int(threadIdx.x) / 64);
+  if (ufirst >= u1) return;
+  auto opnd = [&](int c) { return c >= 0 ? vf + c : vb + (-(c + 2)); };
+  auto ld = [&](const unsigned long long *q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // two register sets per stage, used alternately (the loop below is unrolled by two), so that no
+  // stage register is copied while its load is in flight
+  int4 aU[2], aI[2];
+  int ac[2][kS], ax[2][kS];
+  int bc[2][kS], bx[2][kS], brow[2], bw8[2], bwid[2];
+  double ba[2][kS], bd[2], bg[2];
+  unsigned long long bb[2][kS], bo[2];
+  // stage A: the unit, its rows' records and ELL slots (raw; padding resolved in stage B)
+  auto stage_a = [&](int u, int S) {
+    const int uu = u < u1 ? u : u1 - 1;
+    aU[S] = units[uu];
+    const bool bw = uu >= nunits_f;
+    const int rows = aU[S].y & 255, width = (aU[S].y >> 8) & 255;
+    const int tt = t < rows ? t : rows - 1;
+    aI[S] = (bw ? info_b : info_f)[aU[S].x + tt];
+    const int *ec = bw ? ecol_b : ecol_f, *ei = bw ? eidx_b : eidx_f;
+#pragma unroll
+    for (int q = 0; q < kS; q++) {
+      const int k = j + q * kL, kk = k < width ? k : width - 1;
+      const size_t at = size_t(aU[S].w) + size_t(kk) * aU[S].z + tt;
+      ac[S][q] = ec[at];
+      ax[S][q] = ei[at];
+    }
+  };
+  // stage B: what the compute needs, from stage A's registers of the same set
+  auto stage_b = [&](int S) {
+    const int rows = aU[S].y & 255, width = (aU[S].y >> 8) & 255;
+    const bool live = t < rows;
+    brow[S] = aI[S].x;
+    bw8[S] = t < rows ? 1 : 0;
+    bwid[S] = width;  // wave-uniform (the unit record is a scalar load)
+#pragma unroll
+    for (int q = 0; q < kS; q++) {
+      const bool in = live && j + q * kL < width;
+      bc[S][q] = in ? ac[S][q] : -1;
+      bx[S][q] = in ? ax[S][q] : -1;
+      // materialised here: the compiler would otherwise sink the selects below the next stage A
+      // load into ac / ax, keep both generations live and copy them at the loop latch, waiting
+      // for those loads
+      asm volatile("" : "+v"(bc[S][q]), "+v"(bx[S][q]));
+      ba[S][q] = val[ax[S][q] >= 0 ? ax[S][q] : 0];
+      bb[S][q] = ld(ac[S][q] == -1 ? vf : opnd(ac[S][q]));
+    }
+    asm volatile("" : "+v"(brow[S]), "+v"(bw8[S]));
+    bd[S] = d[aI[S].x];
+    bg[S] = val[aI[S].z];
+    bo[S] = ld(vf + aI[S].x);  // the row's forward value (backward units)
+  };
+  // Each row of the unit is stored as soon as ITS operands are final (ballot over its kL lanes),
+  // not when the whole unit's are: a wide level's unit depends on ~24 producers, and waiting for
+  // the last of them put the slowest hand-off of every unit on the critical path.  The products
+  // and the ordered subtraction are recomputed for the whole wave whenever a row becomes ready
+  // (rows already stored, or not ready, discard theirs).
+  auto compute = [&](int u, int S) {
+    const bool bwd = u >= nunits_f;  // uniform
+    const bool live = bw8[S] & 1, head = live && j == 0;
+    const int width = bwid[S];
+    unsigned long long b[kS];
+#pragma unroll
+    for (int q = 0; q < kS; q++) b[q] = bc[S][q] == -1 ? 0ull : bb[S][q];
+    unsigned long long own = bo[S];
+    bool pend = bwd && head && own == kNatPending;
+#pragma unroll
+    for (int q = 0; q < kS; q++) pend |= b[q] == kNatPending;
+    bool stored = !live;  // per row (all its lanes agree)
+    const unsigned long long t0 = wall_clock64();
+    int bk = 1;
+    while (true) {
+      const unsigned long long pm = __ballot(pend);
+      const bool ready = !stored && ((pm >> base) & ((1ull << kL) - 1)) == 0;
+      if (__any(ready)) {
+        double pr[kS];
+#pragma unroll
+        for (int q = 0; q < kS; q++)
+          pr[q] = bx[S][q] >= 0 ? ba[S][q] * __longlong_as_double(b[q]) : 0.0;
+        double rhs = bd[S];
+        // only the unit's width: a c row of PNP has 14 entries, a PB row at most ~9 of kC = 24
+#pragma unroll
+        for (int k = 0; k < kC; k++) {
+          if (k < width) {  // uniform
+            const double p = __shfl(pr[k / kL], base + k % kL, 64);
+            if (head) rhs -= p;
+          }
+        }
+        if (head && ready) {
+          const double out = (bwd ? __longlong_as_double(own) : 0.0) + 1.0 * (rhs / bg[S]);
+          __hip_atomic_store(bwd ? vb + brow[S] : vf + brow[S],
+                             (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+        stored |= ready;
+      }
+      if (__all(stored)) break;
+      nat_backoff(bk);
+      pend = false;
+#pragma unroll
+      for (int q = 0; q < kS; q++)
+        if (b[q] == kNatPending) {
+          b[q] = ld(opnd(bc[S][q]));
+          pend |= b[q] == kNatPending;
+        }
+      if (bwd && head && own == kNatPending) {
+        own = ld(vf + brow[S]);
+        pend |= own == kNatPending;
+      }
+      const bool late = wall_clock64() - t0 > kNatTimeout;
+      if (late && lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+        for (int q = 0; q < kS; q++)
+          if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;  // NaN: drain the grid
+        if (own == kNatPending) own = 0x7FF8000000000000ull;
+        pend = false;
+      }
+    }
+  };
+  stage_a(ufirst, 0);
+  stage_b(0);
+  stage_a(ufirst + G, 1);
+  for (int u = ufirst; u < u1; u += 2 * G) {
+    stage_b(1);                // unit u + G
+    stage_a(u + 2 * G, 0);
+    compute(u, 0);
+    stage_b(0);                // unit u + 2G
+    stage_a(u + 3 * G, 1);
+    if (u + G < u1) compute(u + G, 1);  // uniform
+  }
+}
+
 constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
 // The sparse tail grid (PNP_NAT_TAIL_WPC = 1, 2 or 4 waves per CU): the tail levels on a grid of
 // at most one workgroup per CU (96 KB of LDS reserved each), so that a consumer CU's memory queue
@@ -351,8 +518,9 @@ __global__ void __launch_bounds__(64)
         bool pend = live && (kind == 1 || kind == 2) && b == kNatPending;
         if (__any(pend)) {
           const unsigned long long t0 = wall_clock64();
+          int bk = 1;
           while (true) {
-            __builtin_amdgcn_s_sleep(1);
+            nat_backoff(bk);
             if (pend) {
               b = ld(opnd(c));
               pend = b == kNatPending;
@@ -415,8 +583,11 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     int dev = 0, cus = 0, per = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>,
-                                                 kB, 0);
+    int per_flow = 0, per_pipe = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_flow,
+                                                 k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>, kB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pipe, k_ssor_nat_pipe<kB>, kB, 0);
+    per = std::min(per_flow, per_pipe);  // one grid size for both head kernels: all resident
     // 4 workgroups per CU (16 waves): fewer pollers than the occupancy allows and enough for
     // the wide levels (PNP config 3: 2.25 ms per application against 2.36 at the occupancy, 2.94
     // at 1; profiles/r04/nat_wg*_r4d.log).  PNP_NAT_FLOW_WG_PER_CU overrides (capped at the
@@ -431,6 +602,11 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
     return std::max(1, c);
   }();
+  // PNP_NAT_PIPE=0: the head as the unpipelined flow kernel (A/B)
+  static const bool pipe = [] {
+    const char *ev = std::getenv("PNP_NAT_PIPE");
+    return !(ev && std::atoi(ev) == 0);
+  }();
   static const int tail_wpc = [] {
     const char *ev = std::getenv("PNP_NAT_TAIL_WPC");
     return ev ? std::max(0, std::atoi(ev)) : 0;
@@ -444,9 +620,14 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
   auto sweep = [&](int u0, int ut, int u1, const NatFlow::Chains &C, int bwd) {
     if (ut > u0) {
       const int blocks = std::min(grid, (ut - u0 + kB / 64 - 1) / (kB / 64));
-      hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB), 0,
-                         s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
-                         F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+      if (F.max_width <= kC && pipe)
+        hipLaunchKernelGGL(k_ssor_nat_pipe<kB>, dim3(blocks), dim3(kB), 0, s, F.units, u0, ut,
+                           F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx, F.bwd.info, F.bwd.ecol,
+                           F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+      else
+        hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB),
+                           0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
+                           F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
     }
     if (u1 > ut && C.ngroups > 0)
       hipLaunchKernelGGL(k_ssor_nat_chain, dim3(C.ngroups), dim3(64), 0, s, C.gptr, C.rec, C.ecode,
