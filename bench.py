@@ -74,7 +74,7 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-ASM_REGIMES = os.path.join(ROOT, "profiles", "r04", "asm_regimes_config3_r4k.json")
+ASM_REGIMES = os.path.join(ROOT, "profiles", "r04", "final", "asm_regimes_config3_final.json")
 
 
 def profile_regime(name):
