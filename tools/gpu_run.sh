@@ -34,7 +34,7 @@ for step in "$@"; do
             fatal $rc || [ $rc -ne 0 ] || { timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace --output-format csv -d "$OUT/calib_req" -o run -- tools/micro/fetch_calib 2 >> "$OUT/calib.log" 2>&1; rc=$?; } ;;
     ab)     : > "$OUT/ab.log"; rc=0
             for i in 1 2 3; do
-              timeout -k 10 120 python tools/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
+              timeout -k 10 120 python tools/runs/ab/ab_asm.py >> "$OUT/ab.log" 2>&1; rc=$?
               fatal $rc && break
             done ;;
     *) echo "unknown step $step"; rc=0 ;;
