@@ -44,8 +44,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
 import pnp_amd as P  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured copy rate is in
-#                       the line (`measured_copy_gbs`)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured stream ceilings
+#                       are in the line (`measured_stream_gbs`, tools/micro/stream.hip)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "pmc_summary.json")
 SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
 
@@ -253,24 +253,42 @@ def host_cpu_info():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def measured_copy_gbs(device):
-    """Device copy rate (read + write bytes / s) of a 1 GiB buffer, past the Infinity Cache."""
-    import torch
-    n = (1 << 30) // 8
-    a = torch.empty(n, dtype=torch.float64, device=f"cuda:{device}").fill_(1.0)
-    b = torch.empty_like(a)
-    for _ in range(2):
-        b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2 * n * 8 * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+def measured_stream_gbs(device, reps=10):
+    """HBM ceilings measured on this box with hand-written dwordx4 streaming kernels
+    (tools/micro/stream.hip, 2 GiB buffers, 8x the Infinity Cache): read-only, write-only, copy
+    and the assembly's 26:74 read:write mix, each bytes moved / average launch time (GB/s).  The
+    guide's float4 copy reads 6.29 TB/s (MI355X_MICROARCH.md); torch's copy_ is not a ceiling."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "micro", "libstream.so"))
+    out = (ctypes.c_double * 4)()
+    shapes = (ctypes.c_double * 20)()
+    rc = lib.stream_measure(ctypes.c_int(device), ctypes.c_int(reps), out, shapes)
+    if rc != 0:
+        raise RuntimeError(f"stream_measure: HIP error {rc}")
+    names = ("read", "write", "copy", "asm_mix")
+    return {"read": out[0], "write": out[1], "copy": out[2], "asm_mix": out[3],
+            "shapes": {sh: {names[k]: shapes[4 * i + k] for k in range(4)}
+                       for i, sh in enumerate(("u1", "u2", "u4", "u8", "resident_u4"))},
+            "source": "tools/micro/stream.hip: dwordx4 kernels on 2 GiB buffers, the fastest of "
+                      f"5 shapes, mean of {reps} event-timed launches; asm_mix = 26:74 read:write "
+                      "(the assembly's PMC split)"}
+
+
+# which measured ceiling bounds each BiCGSTAB kernel class: the SpMV and the ILU(0) sweeps are
+# read streams (PMC: 266 MB read / 18 MB written per SpMV), the vector updates read and write
+STREAM_CEILING = {"spmv": "read", "ilu0_apply": "read", "blas_per_iter": "copy"}
+
+
+def with_stream_fracs(kernels, stream_gbs):
+    """Each kernel's achieved rate also as a fraction of its measured stream ceiling."""
+    out = {}
+    for k, v in kernels.items():
+        if v is None:
+            out[k] = None
+            continue
+        c = STREAM_CEILING[k]
+        out[k] = dict(v, measured_ceiling=c, frac_of_measured=v["achieved"] / stream_gbs[c])
+    return out
 
 
 def byte_models(info, nf, N_local, T_local, prec):
@@ -510,6 +528,127 @@ def ssork_natural_leg(ctx, mesh, x0, nit):
     return out
 
 
+def asm_bicg_rates(ctx, n, prec, nasm=10, nit=20):
+    """Warm assembly (one event pair around nasm back-to-back launches after two untimed ones) and
+    BiCGSTAB (nit fixed iterations after two untimed ones, wall clock) on the context's state."""
+    ctx.assemble_state(2)
+    t_asm = ctx.assemble_state_timed(nasm) / nasm
+    ctx.bicgstab_iterations(2, prec)
+    t0 = time.perf_counter()
+    ctx.bicgstab_iterations(nit, prec)
+    t_it = (time.perf_counter() - t0) / nit
+    return {"assemble_us": t_asm * 1e6, "assembled_dofs_per_s": n / t_asm,
+            "bicgstab_ms_per_iter": t_it * 1e3, "bicgstab_iters_per_s": 1.0 / t_it}
+
+
+def newton_summary(res, seconds):
+    return {"seconds": seconds, "converged": res["converged"], "iterations": res["iterations"],
+            "linear_iterations": res["linear_iterations"],
+            "assemble_s": res["assemble_seconds"], "solve_s": res["solve_seconds"]}
+
+
+def per_config_legs(prec, ie_steps=10):
+    """SURVEY.md §8(d)'s other configurations, bounded (N = 1 only, ~20 s):
+      config 1: PB on test/sphere_pb refined k=6 (733 K DOF; BASELINE configs[0]): PB Newton from
+                0, assembled DOFs/s, BiCGSTAB ms/it with the bench's preconditioner and with the
+                reference's default BCGS_SSORk (natural-order SSOR);
+      config 2: 2-ion PNP on test/cylinder.msh refined k=6 (3.3 M DOF): PB -> BCExtension -> PNP
+                Newton (time to solution), assembled DOFs/s, BiCGSTAB it/s;
+      config 4: instationary PNP (PnpOperator + PnpTOperator, implicit Euler, dt = tau,
+                src/instationary_pnp_from_pb.hh:409-431): the 100 steps on test/pore.msh that
+                BASELINE names, and ie_steps steps on pore_pnp k=3 (556 K DOF) with per-step
+                assembly and BiCGSTAB rates and the Newton / BiCGSTAB counts."""
+    out = {}
+    # ---- config 1 -------------------------------------------------------------------------------
+    t0 = time.perf_counter()
+    cfg = P.read_config(os.path.join(ROOT, "data", "sphere_pb", "sphere.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(6)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    ctx.set_operator(P.OP_PB)
+    t1 = time.perf_counter()
+    phi, res = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=prec)
+    pbn = newton_summary(res, time.perf_counter() - t1)
+    ctx.state_set(phi)
+    r = asm_bicg_rates(ctx, mesh.nv, prec)
+    r_nat = asm_bicg_rates(ctx, mesh.nv, P.PREC_SSOR_NATURAL, nasm=1)
+    ctx.close()
+    out["1"] = {"workload": "PB, test/sphere_pb/sphere.msh refined k=6", "dofs": mesh.nv,
+                "pb_newton": pbn, **r,
+                "bicgstab_ssork_natural_ms_per_iter": r_nat["bicgstab_ms_per_iter"],
+                "leg_seconds": time.perf_counter() - t0}
+    # ---- config 2 -------------------------------------------------------------------------------
+    t0 = time.perf_counter()
+    cfg = P.read_config(os.path.join(ROOT, "data", "cylinder_config.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(6)
+    ctx = P.Context(mesh, P.Params.from_config(cfg))
+    ctx.set_operator(P.OP_PB)
+    t1 = time.perf_counter()
+    phi, pres = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=prec)
+    x0 = ctx.initial_state(phi)
+    ctx.set_operator(P.OP_PNP)
+    s = cfg.system
+    t2 = time.perf_counter()
+    u, res = ctx.newton(x0, reduction=s["newtonReduction"],
+                        min_linear_reduction=s["newtonMinLinearReduction"], prec=prec,
+                        linear_maxit=int(s["linearSolverIterations"]))
+    t3 = time.perf_counter()
+    ctx.state_set(x0)
+    r = asm_bicg_rates(ctx, 3 * mesh.nv, prec)
+    ctx.close()
+    out["2"] = {"workload": "2-ion PNP, test/cylinder.msh refined k=6", "dofs": 3 * mesh.nv,
+                "pb_newton_s": t2 - t1, "pnp_newton": newton_summary(res, t3 - t2),
+                "time_to_solution_s": t3 - t1, **r, "leg_seconds": time.perf_counter() - t0}
+    # ---- config 4 -------------------------------------------------------------------------------
+    cfg = P.read_config(os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
+    s = cfg.system
+    for key, meshfile, refine, nsteps, kw in (
+            ("4", os.path.join(ROOT, "data", "pore.msh"), 0, 100,
+             dict(reduction=s["newtonReduction"], min_linear_reduction=s["newtonMinLinearReduction"],
+                  abs_limit=1e-12, maxit=int(s["newtonMaxIterations"]),
+                  line_search_maxit=int(s["newtonLineSearchMaxIteration"]))),
+            ("4_pore_pnp_k3", cfg.meshfile, 3, ie_steps,
+             # the refined stand-in's tolerances (tools/bench_configs.py config4r): the residual's
+             # rounding floor (~2e-10) sits above the reference's relative 1e-9 there
+             dict(reduction=1e-8, abs_limit=1e-9))):
+        t0 = time.perf_counter()
+        mesh = P.Mesh.read_gmsh(meshfile).refine(refine)
+        ctx = P.Context(mesh, P.Params.from_config(cfg))
+        ctx.set_operator(P.OP_PB)
+        phi, _ = ctx.newton(np.zeros(mesh.nv), reduction=1e-9, prec=prec)
+        u = ctx.initial_state(phi)
+        steps = []
+        t1 = time.perf_counter()
+        for i in range(nsteps):
+            ctx.set_operator(P.OP_PNP_IMPLICIT_EULER, dt=s["tau"], x_old=u)
+            u, res = ctx.newton(u, prec=prec, **kw)
+            steps.append(res)
+            if not res["converged"]:
+                break
+        t2 = time.perf_counter()
+        n = 3 * mesh.nv
+        lin = sum(r_["linear_iterations"] for r_ in steps)
+        newt = sum(r_["iterations"] for r_ in steps)
+        t_as = sum(r_["assemble_seconds"] for r_ in steps)
+        t_so = sum(r_["solve_seconds"] for r_ in steps)
+        o = {"workload": f"implicit Euler PNP, {os.path.relpath(meshfile, ROOT)} refined k={refine}",
+             "dofs": n, "steps": len(steps), "all_converged": all(r_["converged"] for r_ in steps),
+             "seconds": t2 - t1, "ms_per_step": 1e3 * (t2 - t1) / max(1, len(steps)),
+             "newton_iterations": newt, "bicgstab_iterations": lin,
+             "newton_tolerances": {k: v for k, v in kw.items()},
+             "per_step": {"newton_iterations": newt / max(1, len(steps)),
+                          "bicgstab_iterations": lin / max(1, len(steps)),
+                          "assemble_s": t_as / max(1, len(steps)),
+                          "solve_s": t_so / max(1, len(steps)),
+                          "bicgstab_iters_per_s_in_solve": lin / t_so if t_so > 0 else None}}
+        if refine > 0:  # event-timed rates on the last step's system (the small mesh is
+            ctx.state_set(u)  # launch-bound: its rates say nothing about the kernels)
+            o.update(asm_bicg_rates(ctx, n, prec))
+        ctx.close()
+        o["leg_seconds"] = time.perf_counter() - t0
+        out[key] = o
+    return out
+
+
 def strong_mesh(refine):
     cfg = P.read_config(os.path.join(ROOT, "data", "pore_without_dna", "pore.cfg"))
     return cfg, P.Mesh.load(cfg.meshfile, size_scale=0.85).refine(refine)
@@ -545,6 +684,8 @@ def main():
                     help="run the AMG time-to-solution leg at N>1 too (default: N=1 only)")
     ap.add_argument("--no-ssork", action="store_true",
                     help="skip the BCGS_SSORk (natural-order SSOR) leg")
+    ap.add_argument("--no-per-config", action="store_true",
+                    help="skip the configs 1 / 2 / 4 legs (per_config, N=1 only)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the multi-GPU self-check (rccl_parity) on the config-5 system")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -572,7 +713,7 @@ def main():
         dist.init_process_group("gloo")
     prec = P.PREC_BY_NAME[args.prec]
 
-    copy_gbs = measured_copy_gbs(local)
+    stream_gbs = measured_stream_gbs(local)
     cfg, mesh = primary_mesh(args, world)
     ctx, x0, pb_res, t_setup = make_context(mesh, cfg, rank, world, local, dist)
     M = measure(ctx, mesh, args, prec, dist, world)
@@ -637,6 +778,9 @@ def main():
     if world == 1 and not args.no_ssork:
         ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters)
     ctx.close()
+    per_config = None
+    if world == 1 and not args.no_per_config:
+        per_config = per_config_legs(prec)
 
     # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
     strong = parity = None
@@ -733,6 +877,9 @@ def main():
                                         "bytes, not counted HBM bytes",
                          "hbm_gbs_from_traffic": (traffic / aw["seconds"] / 1e9) if traffic
                                                  else None,
+                         "hbm_frac_of_measured_asm_mix":
+                             (traffic / aw["seconds"] / 1e9 / stream_gbs["asm_mix"]) if traffic
+                             else None,
                          "traffic_source": ((pmc_summary() or {}).get("path", "none") +
                                             " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
                                             "separate passes; x2 calibrated in profiles/r04/calib)"),
@@ -751,7 +898,10 @@ def main():
                                  "unit": "GB/s", "frac": asit["frac"],
                                  "bytes_per_launch": asit["bytes"],
                                  "avg_launch_us": asit["seconds"] * 1e6,
-                                 "frac_of_measured_copy": asit["achieved"] / copy_gbs,
+                                 "frac_of_measured_asm_mix": asit["achieved"] / stream_gbs["asm_mix"],
+                                 "hbm_frac_of_measured_asm_mix":
+                                     (traffic / asit["seconds"] / 1e9 / stream_gbs["asm_mix"])
+                                     if traffic else None,
                                  "profile": (profile_regime("in_situ") if args.scaling == "weak"
                                              else None),
                                  "timing": f"HIP event pair per launch, each launch right after "
@@ -759,10 +909,13 @@ def main():
             "roofline_cold": {"bound": "hbm", "achieved": ac["achieved"], "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": ac["frac"], "bytes_per_launch": ac["bytes"],
                               "avg_launch_us": ac["seconds"] * 1e6,
-                              "frac_of_measured_copy": ac["achieved"] / copy_gbs,
+                              "frac_of_measured_asm_mix": ac["achieved"] / stream_gbs["asm_mix"],
+                              "hbm_frac_of_measured_asm_mix":
+                                  (traffic / ac["seconds"] / 1e9 / stream_gbs["asm_mix"])
+                                  if traffic else None,
                               "profile": profile_regime("cold") if args.scaling == "weak" else None,
                               "scrub": f"{SCRUB_BYTES >> 20} MiB read between launches"},
-            "measured_copy_gbs": copy_gbs,
+            "measured_stream_gbs": stream_gbs,
             "roofline_bicgstab": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "event_ms_per_iter": M["it_stored"]["seconds"] * 1e3,
                                   "bytes_per_iter": M["it_stored"]["bytes"],
@@ -780,9 +933,9 @@ def main():
                                                          "(the k-form SELL values and the f32 "
                                                          "factors move fewer bytes than the "
                                                          "fp64 CSR the contract counts)",
-                                  "kernels": {"spmv": M["spmv_stored"],
-                                              "ilu0_apply": M["ilu_stored"],
-                                              "blas_per_iter": M["blas"]}},
+                                  "kernels": with_stream_fracs(
+                                      {"spmv": M["spmv_stored"], "ilu0_apply": M["ilu_stored"],
+                                       "blas_per_iter": M["blas"]}, stream_gbs)},
             "cpu_baseline": cpu,
             "cpu_baseline_multithread": cpu_all,
             "setup_s": t_setup,
@@ -794,6 +947,7 @@ def main():
             "pnp_newton_time_to_solution_f64_factors": newton_f64,
             "pnp_newton_time_to_solution_amg": newton_amg,
             "bicgstab_ssork_natural": ssork,
+            "per_config": per_config,
             "strong_scaling": strong,
             "rccl_parity": parity,
         }

@@ -251,6 +251,7 @@ struct pnp_ctx {
   IluFlowDev ilu_flow[2];
   DBuf<unsigned> ilu_flow_abort;
   bool ilu_flow_used = false;  // a flow launch ran since the last check
+  long long ilu_flow_n = 0;    // flow launches issued (pnp_info; a graph capture counts once)
   // ---- reference-order mode (PNP_OPT_SEQ_ORDER, seq_order.hip) -----------------------------
   int seq_opt = 0;
   bool seq_built = false, seq_op_valid = false;
@@ -356,12 +357,13 @@ struct pnp_ctx {
     return p;
   }
   struct GraphKey {
-    int count, prec, fuse, nf, pat, f32;
+    int count, prec, fuse, nf, pat, f32, flow;
     const void *zout, *dmask;
     long long epoch;
     bool operator==(const GraphKey &o) const {
       return count == o.count && prec == o.prec && fuse == o.fuse && nf == o.nf && pat == o.pat &&
-             f32 == o.f32 && zout == o.zout && dmask == o.dmask && epoch == o.epoch;
+             f32 == o.f32 && flow == o.flow && zout == o.zout && dmask == o.dmask &&
+             epoch == o.epoch;
     }
   };
   // kernel arguments captured in a graph stay valid while the buffers and the layout do: anything
@@ -955,12 +957,15 @@ struct pnp_ctx {
                 if (k < len) {
                   const int C = col[cnt[R] + k];
                   const int fc = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
-                  // kind: 0 zero, 1 forward value, 2 backward value, 3 in the wave's registers
-                  int code = fc == -1 ? 0 : fc >= 0 ? (fc << 2 | 1) : ((-(fc + 2)) << 2 | 2);
+                  // kind: 0 zero, 1 forward value, 2 backward value, 3 in the wave's registers;
+                  // | 4: final when the chain launch begins (the other sweep's value, or a row of
+                  // this sweep's head launch), a plain load the kernel never polls
+                  int code = fc == -1 ? 0 : fc >= 0 ? (fc << 3 | 1) : ((-(fc + 2)) << 3 | 2);
                   const bool fresh = fwd ? (code & 3) == 1 : (code & 3) == 2;  // this sweep's value
+                  if (code != 0 && (!fresh || lev[C] < ltail)) code |= 4;
                   for (int h = 1; fresh && h <= H && size_t(h) <= t; h++)
                     if (G[t - h] == C) {
-                      code = h << 2 | 3;
+                      code = h << 3 | 3;
                       break;
                     }
                   ecode.push_back(code);
@@ -983,6 +988,13 @@ struct pnp_ctx {
           W.chain_wpad = wpad;
           W.chain_ok = true;
         }
+      }
+      if (chain_rows > 0 && !W.chain_ok) {
+        // no chains (rows wider than the chain kernel takes): the tail is PNP_NAT_TAIL's again
+        // (default none), not the chain threshold's -- a one-workgroup tail of ~8K rows would run
+        // every narrow level on one CU
+        ltail = nlev;
+        while (tail_rows > 0 && ltail > 0 && lptr[ltail] - lptr[ltail - 1] <= tail_rows) ltail--;
       }
       for (int l = 0; l < nlev && nat_units_ok; l++) {
         if (l == ltail) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
@@ -1040,19 +1052,34 @@ struct pnp_ctx {
   hipError_t ssor_natural(const double *d, double *vout) {
     const int nv = mesh.nv;
     hipError_t e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
-    if (e == hipSuccess) e = use_nat_flow() ? ssor_natural_flow() : ssor_natural_levels();
+    if (e == hipSuccess) e = nat_sweep();
     if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
     return e;
   }
-  // one launch for both sweeps (ssor_natural.hip, launch_ssor_natural_flow): one rank only (in-process
-  // ranks share the device, and the dataflow needs every workgroup of its grid resident);
-  // PNP_NAT_FLOW=0 keeps the level launches
+  // one launch for both sweeps (ssor_natural.hip, launch_ssor_natural_flow) whenever this context
+  // owns its GPU: one rank, or one rank of an RCCL communicator (one process per GPU, each rank
+  // sweeping its owned rows -- block Jacobi across ranks, as ISTL's NOVLP SeqSSOR on the local
+  // matrix).  The in-process local group keeps the level launches: its ranks share one device, and
+  // the dataflow needs every workgroup of its grid resident.  PNP_NAT_FLOW=0 keeps the level
+  // launches everywhere
   bool use_nat_flow() const {
     static const bool env_on = [] {
       const char *ev = std::getenv("PNP_NAT_FLOW");
       return !(ev && std::atoi(ev) == 0);
     }();
-    return env_on && !dist && nat_units_ok;
+    return nat_flow_opt == 0 ? false
+           : nat_flow_opt == 1 ? nat_units_ok
+                               : env_on && !lg && nat_units_ok;
+  }
+  int nat_flow_opt = -1;  // PNP_OPT_NAT_FLOW: -1 auto (above), 0 level launches, 1 dataflow
+  long long nat_flow_n = 0, nat_level_n = 0;  // applications per schedule (pnp_info)
+  hipError_t nat_sweep() {
+    if (use_nat_flow()) {
+      nat_flow_n++;
+      return ssor_natural_flow();
+    }
+    nat_level_n++;
+    return ssor_natural_levels();
   }
   hipError_t ssor_natural_flow() {
     pnp::NatFlow F;
@@ -1221,16 +1248,19 @@ struct pnp_ctx {
       const int m = ev ? std::atoi(ev) : 1;
       return (m >= 0 && m <= 1) ? m : 1;
     }();
-    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (mode == 0 || !dist)) {
+    // PNP_OPT_ILU_FLOW = 2 selects the ticketed form (any residency, so also ranks sharing a GPU)
+    const int fmode = ilu_flow_opt == 2 ? 0 : mode;
+    if (ilu_flow_opt && d != vout && (c_first == 0 || c_first == 1) && (fmode == 0 || !dist)) {
       IluFlowDev &D = ilu_flow[c_first];
       int rc;
       if (!D.built && (rc = ilu_flow_build(c_first, D))) return rc;
-      D.F.persistent = mode;
+      D.F.persistent = fmode;
       if (D.ok) {
         hipError_t e = pnp::launch_ilu0_flow(dl, D.F, nf, pat, lvals.p, uvals.p, d, vout, stream,
                                              f32_now());
         if (e != hipSuccess) return hipfail(e, what);
         ilu_flow_used = true;
+        ilu_flow_n++;
         return PNP_OK;
       }
     }
@@ -1958,8 +1988,8 @@ struct pnp_ctx {
       // failure turns graphs off for the rest of the solve (eager launches, same results)
       const int glen = std::min(check, 16);
       while (graphs && glen > 1 && kend - k >= glen) {
-        const GraphKey key{glen, prec, fuse ? 1 : 0, nf, pat, f32_now(), zout, dl.dmask,
-                           graph_epoch};
+        const GraphKey key{glen, prec, fuse ? 1 : 0, nf, pat, f32_now(),
+                           ilu_flow_opt * 4 + (nat_flow_opt + 1), zout, dl.dmask, graph_epoch};
         bool captured = true;
         rc = graph_run(key, [&]() -> int {
           for (int i = 0; i < key.count; i++)
@@ -2222,7 +2252,7 @@ struct pnp_ctx {
       e = pnp::launch_seq_prec_diag(n, prec == PNP_PREC_JACOBI, d, csr_diag.p, csr_val.p, v, stream);
     } else {  // SSOR_NATURAL: the natural-order sweep on the CSR view
       e = hipMemcpyAsync(nat_d.p, d, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
-      if (e == hipSuccess) e = use_nat_flow() ? ssor_natural_flow() : ssor_natural_levels();
+      if (e == hipSuccess) e = nat_sweep();
       if (e == hipSuccess)
         e = hipMemcpyAsync(v, nat_v.p, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
     }
@@ -3169,6 +3199,9 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->degree = c->degree;
   info->color_conflicts = c->L.conflicts;
   info->transport = c->comm ? 2 : (c->lg ? 1 : 0);
+  info->nat_flow_applies = c->nat_flow_n;
+  info->nat_level_applies = c->nat_level_n;
+  info->ilu_flow_applies = c->ilu_flow_n;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->y2.n + c->b.n + c->prevu.n + c->ext.n) * 8;
@@ -3607,8 +3640,13 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     return PNP_OK;
   }
   if (option == PNP_OPT_ILU_FLOW) {
-    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_FLOW takes 0 or 1");
+    if (value < 0 || value > 2) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_FLOW takes 0, 1 or 2");
     c->ilu_flow_opt = int(value);
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_NAT_FLOW) {
+    if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_NAT_FLOW takes -1, 0 or 1");
+    c->nat_flow_opt = int(value);
     return PNP_OK;
   }
   if (option == PNP_OPT_AMG_FALLBACK) {

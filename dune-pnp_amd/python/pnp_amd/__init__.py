@@ -34,7 +34,7 @@ OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSO
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG, PREC_SSOR_NATURAL = range(6)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
 (OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD, OPT_BICG_TWORED, OPT_AMG_FALLBACK,
- OPT_GRAPH, OPT_SEQ_ORDER, OPT_ILU_FLOW) = 1, 2, 3, 4, 5, 6, 7, 8
+ OPT_GRAPH, OPT_SEQ_ORDER, OPT_ILU_FLOW, OPT_NAT_FLOW) = 1, 2, 3, 4, 5, 6, 7, 8, 9
 DEVICE_PTRS, JAC_FD = 1, 2
 CREATE_ABSORB_THIN_COLOR = 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
@@ -94,7 +94,9 @@ class _Info(C.Structure):
                 ("nnz_reduced", C.c_int64), ("nslots", C.c_int64), ("device_bytes", C.c_int64),
                 ("nks", C.c_int32), ("nvb", C.c_int32), ("lslots", C.c_int64),
                 ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32),
-                ("color_conflicts", C.c_int64), ("transport", C.c_int32)]
+                ("color_conflicts", C.c_int64), ("transport", C.c_int32),
+                ("nat_flow_applies", C.c_int64), ("nat_level_applies", C.c_int64),
+                ("ilu_flow_applies", C.c_int64)]
 
 
 class _SpaceInfo(C.Structure):

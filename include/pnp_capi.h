@@ -169,6 +169,12 @@ typedef struct {
   int32_t transport;     /* 0 one rank, 1 in-process local group, 2 RCCL (also a 1-rank RCCL
                             communicator: a pnp_comm of size 1 with an RCCL id runs the
                             multi-rank code path, every reduction an ncclAllReduce) */
+  int64_t nat_flow_applies;  /* PNP_PREC_SSOR_NATURAL applications run as one dataflow launch
+                                (any context that owns its GPU: one rank, or one RCCL rank) */
+  int64_t nat_level_applies; /* ... and as level launches (the in-process local group, whose
+                                ranks share one device; or PNP_NAT_FLOW=0) */
+  int64_t ilu_flow_applies;  /* PNP_PREC_ILU0 applications launched as one dataflow launch
+                                (PNP_OPT_ILU_FLOW; a graph capture counts once) */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 
@@ -374,8 +380,20 @@ enum {
    * colour and sweep direction: every 256-row block of every colour launch is a unit taken in the
    * launches' order by an atomic ticket, and a unit waits only for the units whose rows it reads
    * (linalg.hip k_ilu0_flow).  The same arithmetic per row, so the same results bit for bit.
-   * 0: the colour launches (the environment variable PNP_ILU_FLOW=0/1 sets the default). */
-  PNP_OPT_ILU_FLOW = 8
+   * 0: the colour launches (the environment variable PNP_ILU_FLOW=0/1 sets the default).  1: the
+   * resident-grid form where the context owns its GPU (one rank), else the colour launches.
+   * 2: the ticketed form, which needs no residency (also ranks sharing one GPU).
+   * pnp_info.ilu_flow_applies counts the dataflow launches. */
+  PNP_OPT_ILU_FLOW = 8,
+  /* PNP_PREC_SSOR_NATURAL's schedule.  -1 (default): one dataflow launch per application
+   * (ssor_natural.hip) whenever the context owns its GPU -- one rank, or one rank of an RCCL
+   * communicator (one process per GPU) -- and the level launches for the in-process local group,
+   * whose ranks share one device.  0: always the level launches.  1: always the dataflow launch;
+   * with local-group ranks the caller must keep their preconditioner applications from running
+   * concurrently (the dataflow needs every workgroup of its grid resident).  Both schedules give
+   * the same results bit for bit; pnp_info.nat_flow_applies / nat_level_applies count them.  The
+   * environment variable PNP_NAT_FLOW=0 turns the automatic choice off. */
+  PNP_OPT_NAT_FLOW = 9
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 

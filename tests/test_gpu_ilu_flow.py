@@ -22,11 +22,16 @@ def h(a):
     return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def _both(ctx, fn):
+def _both(ctx, fn, flow_on=1):
+    """fn() with the colour launches, then with the dataflow form `flow_on`; the second run must
+    actually launch the dataflow kernel (pnp_info.ilu_flow_applies), and the first must not."""
     out = []
-    for flow in (0, 1):
+    for flow in (0, flow_on):
         ctx.set_option(P.OPT_ILU_FLOW, flow)
+        n0 = ctx.info()["ilu_flow_applies"]
         out.append(fn())
+        ran = ctx.info()["ilu_flow_applies"] - n0
+        assert (ran > 0) == (flow != 0), f"flow={flow}: {ran} dataflow launches"
     ctx.set_option(P.OPT_ILU_FLOW, 0)
     return out
 
@@ -73,9 +78,13 @@ def test_flow_partitioned_ranks_bitwise():
         c.jacobian(x, export=False)
         b = c.sync_vector(c.residual(x))
         out = []
-        for flow in (0, 1):
+        # 2: the ticketed form, which needs no residency -- the three in-process ranks share the
+        # GPU, where the default resident-grid form falls back to the colour launches
+        for flow in (0, 2):
             c.set_option(P.OPT_ILU_FLOW, flow)
+            n0 = c.info()["ilu_flow_applies"]
             sol, res = c.linear_solve(b, prec=P.PREC_ILU0, reduction=1e-10, maxit=20000)
+            assert (c.info()["ilu_flow_applies"] > n0) == (flow != 0)
             out.append((h(c.sync_vector(sol)), res["iterations"]))
         return out
     outs = run_ranks(3, mesh, par, fn)
