@@ -178,7 +178,11 @@ __global__ void __launch_bounds__(BLK)
 #pragma unroll
       for (int q = 0; q < kS; q++) {
         a[q] = ix[q] >= 0 ? val[ix[q]] : 0.0;
-        b[q] = c[q] == -1 ? 0ull : nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+        // a backward unit's forward-value operands were final when the launch began (the forward
+        // sweep is an earlier launch): plain, cacheable loads; only this launch's results are polled
+        b[q] = c[q] == -1 ? 0ull
+               : (bwd && c[q] >= 0) ? vf[c[q]]
+                                    : nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
       }
       bool pend = false;
 #pragma unroll
@@ -253,13 +257,7 @@ __global__ void __launch_bounds__(BLK)
     if (head) {
       // the row's own forward value is final: its diagonal entry's operand was waited for above
       double own = 0.0;
-      if (bwd) {
-        unsigned long long w;
-        while ((w = nat_ld<SCOPE>(vf + I.x)) == kNatPending &&
-               !__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        }
-        own = __longlong_as_double(w);
-      }
+      if (bwd) own = __longlong_as_double(vf[I.x]);  // final since the forward launches
       const double out = own + 1.0 * (rhs / val[I.z]);
       __hip_atomic_store(bwd ? vb + I.x : vf + I.x,
                          (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED, SCOPE);
@@ -294,6 +292,16 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
   auto opnd = [&](int c) { return c >= 0 ? vf + c : vb + (-(c + 2)); };
   auto ld = [&](const unsigned long long *q) {
     return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // a launch holds the units of one sweep; in a backward launch every forward value is final
+  // (earlier launches), so those operands are plain, cacheable loads and never polled
+  const bool bwd_launch = u0 >= nunits_f;
+  auto ld_op = [&](int c) {  // both loads unconditional (see k_ssor_nat_chain's ld_op)
+    const bool fin = bwd_launch && c >= 0;
+    unsigned long long m = fin ? ~0ull : 0ull;
+    asm volatile("" : "+v"(m));  // an opaque mask: neither load can be predicated away
+    const unsigned long long p = *(fin ? vf + c : vf), a = ld(fin || c == -1 ? vf : opnd(c));
+    return (p & m) | (a & ~m);  // c == -1 (zero operand): a dummy, never used
   };
   // two register sets per stage, used alternately (the loop below is unrolled by two), so that no
   // stage register is copied while its load is in flight
@@ -336,12 +344,12 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
       // for those loads
       asm volatile("" : "+v"(bc[S][q]), "+v"(bx[S][q]));
       ba[S][q] = val[ax[S][q] >= 0 ? ax[S][q] : 0];
-      bb[S][q] = ld(ac[S][q] == -1 ? vf : opnd(ac[S][q]));
+      bb[S][q] = ld_op(ac[S][q]);
     }
     asm volatile("" : "+v"(brow[S]), "+v"(bw8[S]));
     bd[S] = d[aI[S].x];
     bg[S] = val[aI[S].z];
-    bo[S] = ld(vf + aI[S].x);  // the row's forward value (backward units)
+    bo[S] = vf[aI[S].x];  // the row's forward value (used by backward units only; final there)
   };
   // Each row of the unit is stored as soon as ITS operands are final (ballot over its kL lanes),
   // not when the whole unit's are: a wide level's unit depends on ~24 producers, and waiting for
@@ -455,8 +463,11 @@ constexpr int kTailPad = 96 * 1024;
 // Progress: a row depends only on rows of lower levels and a group's rows are in increasing level
 // order, so the lowest uncomputed row's group is at that row and its operands are final; every
 // group's wave is resident (the host packs at most ssor_natural_chain_capacity() groups).
-// Operand codes (host): idx << 2 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
-// result idx (1..kChainH) rows back.
+// Operand codes (host): idx << 3 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
+// result idx (1..kChainH) rows back; kind | 4 (5, 6): vf / vb[idx] already final when the launch
+// begins (a forward value in the backward sweep, or a row of the head launch before this one), a
+// plain cacheable load that is never polled.  The row's own forward value (backward sweep) is
+// likewise final and plainly loaded.
 #ifndef NAT_CHAIN_D
 #define NAT_CHAIN_D 2  // build-flag A/B knob: stage-B lead in steps (stage A leads by twice that)
 #endif
@@ -480,8 +491,17 @@ __global__ void __launch_bounds__(64)
     return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto opnd = [&](int c) {  // the operand's address (kind 0 and 3: a harmless dummy)
-    const int k = c & 3, i = c >> 2;
+    const int k = c & 3, i = c >> 3;
     return k == 1 ? vf + i : k == 2 ? vb + i : vf;
+  };
+  // both loads issued unconditionally (the other one at a harmless dummy address): a per-lane
+  // choice between two load kinds would make the compiler branch and drain the pipeline per load
+  auto ld_op = [&](int c) {
+    const bool fin = (c & 4) != 0;
+    unsigned long long m = fin ? ~0ull : 0ull;
+    asm volatile("" : "+v"(m));  // an opaque mask: neither load can be predicated away
+    const unsigned long long p = *(fin ? opnd(c) : vf), a = ld(fin ? vf : opnd(c));
+    return (p & m) | (a & ~m);
   };
   int4 ra[A];
   int ca[A], xa[A];
@@ -495,9 +515,9 @@ __global__ void __launch_bounds__(64)
   };
   auto stage_b = [&](int sa, int sb) {
     av[sb] = val[xa[sa] >= 0 ? xa[sa] : 0];
-    bv[sb] = ld(opnd(ca[sa]));
+    bv[sb] = ld_op(ca[sa]);
     dv[sb] = d[ra[sa].x];
-    ov[sb] = __longlong_as_double(ld(vf + ra[sa].x));  // the forward value (backward sweep)
+    ov[sb] = bwd ? __longlong_as_double(vf[ra[sa].x]) : 0.0;  // the forward value (final)
     gv[sb] = val[ra[sa].z];
   };
 #pragma unroll
@@ -512,7 +532,7 @@ __global__ void __launch_bounds__(64)
     for (int i = 0; i < A; i++) {
       const int st = s + i;
       if (st < len) {  // uniform
-        const int c = ca[i], kind = c & 3, width = ra[i].y;
+        const int c = ca[i], kind = c & 7, width = ra[i].y;
         const bool live = lane < width;
         unsigned long long b = bv[i % D];
         bool pend = live && (kind == 1 || kind == 2) && b == kNatPending;
@@ -535,12 +555,12 @@ __global__ void __launch_bounds__(64)
             }
           }
         }
-        const int hi = c >> 2;
+        const int hi = c >> 3;
         double hv = h[0];
 #pragma unroll
         for (int q = 1; q < kChainH; q++)
           if (hi == q + 1) hv = h[q];
-        const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);
+        const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);  // 1,2,5,6
         const double pr = (live && xa[i] >= 0) ? av[i % D] * o : 0.0;
         const unsigned long long pb = __double_as_longlong(pr);
         const int plo = int(unsigned(pb)), phi = int(unsigned(pb >> 32));
