@@ -103,6 +103,10 @@ struct pnp_ctx {
   bool dist = false;
   ncclComm_t comm = nullptr;
   std::shared_ptr<LocalGroup> lg;  // test transport instead of RCCL
+  pnp_host_transport ht{};         // host-staged transport (pnp_comm.host), if ht.exchange
+  double *h_send = nullptr, *h_recv = nullptr, *h_red = nullptr;  // its pinned staging buffers
+  size_t h_red_n = 0;
+  bool host_tr() const { return ht.exchange != nullptr; }
 
   // P_k, k > 1 (pnp_create_pk): `mesh` is the node mesh (nv = Lagrange nodes, no elements) the
   // partition, layout and external vectors are built on; tmesh the triangle mesh, pks the space
@@ -225,7 +229,8 @@ struct pnp_ctx {
     }
   };
   NatDir nat_f, nat_b;
-  DBuf<double> nat_d, nat_v, nat_vf;
+  DBuf<double> nat_d, nat_v, nat_vf;  // external layout: d (level launches), vb, vf
+  DBuf<double> nat_di, nat_vi;        // internal layout temporaries (reference-order mode)
   // the one-launch dataflow sweep (launch_ssor_natural_flow): units, forward units first
   std::vector<int4> nat_units;
   DBuf<int4> d_nat_units;
@@ -326,6 +331,9 @@ struct pnp_ctx {
       }
     for (auto e : ev_pool) hipEventDestroy(e);
     if (hS) hipHostFree(hS);
+    if (h_send) hipHostFree(h_send);
+    if (h_recv) hipHostFree(h_recv);
+    if (h_red) hipHostFree(h_red);
     if (comm) ncclCommDestroy(comm);
     if (blas) rocblas_destroy_handle(blas);
     if (ev_ready) hipEventDestroy(ev_ready);
@@ -484,6 +492,7 @@ struct pnp_ctx {
   int halo_on(double *vec, int nfv, hipStream_t hs) {
     if (nranks == 1) return PNP_OK;
     if (lg) return halo_local(vec, nfv);
+    if (host_tr()) return halo_host(vec, nfv);
     if (L.nbr_ranks.empty()) return PNP_OK;
     hipEvent_t t0 = hs == stream ? tb(T_HALO) : nullptr;
     int ns = int(L.send_idx.size());
@@ -523,7 +532,7 @@ struct pnp_ctx {
     const int kd = mode == 4 ? 3 : (mode == 2 ? 2 : 1);
     const pnp::DevLayout dl_int = sub_layout(true), dl_bnd = sub_layout(false);
     int n1 = 0, n2 = 0, rc;
-    if (lg) {  // in-process transport: synchronous halo between the two halves
+    if (lg || host_tr()) {  // in-process / host-staged transport: synchronous halo between the halves
       hipEvent_t t0 = tb(T_SPMV);
       e = pnp::launch_spmv(dl_int, nf, pat, vals.p, vin, yout, mode, w, partials.p, &n1, stream, w2);
       if (e != hipSuccess) return hipfail(e, "spmv interior");
@@ -548,6 +557,36 @@ struct pnp_ctx {
     if (e != hipSuccess) return hipfail(e, "spmv boundary");
     te(T_SPMV, t1);
     *nsp = n1 + n2;
+    return PNP_OK;
+  }
+
+  // host-staged halo: pack on the device, copy to pinned host memory, the caller's exchange, copy
+  // the received ghosts back (synchronous, on the context's stream)
+  int halo_host(double *vec, int nfv) {
+    hipEvent_t t0 = tb(T_HALO);
+    const int ns = int(L.send_idx.size()), nq = int(L.nbr_ranks.size());
+    const size_t nsend = size_t(ns) * nfv, nrecv = size_t(L.n_ghost) * nfv;
+    hipError_t e = pnp::launch_pack(ns, nfv, d_send_idx.p, vec, sendbuf.p, stream);
+    if (e == hipSuccess && nsend)
+      e = hipMemcpyAsync(h_send, sendbuf.p, sizeof(double) * nsend, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hipfail(e, "halo pack");
+    std::vector<int64_t> soff(nq), scnt(nq), roff(nq), rcnt(nq);
+    for (int q = 0; q < nq; q++) {
+      soff[q] = int64_t(L.send_ptr[q]) * nfv;
+      scnt[q] = int64_t(L.send_ptr[q + 1] - L.send_ptr[q]) * nfv;
+      roff[q] = int64_t(L.recv_ptr[q]) * nfv;
+      rcnt[q] = int64_t(L.recv_ptr[q + 1] - L.recv_ptr[q]) * nfv;
+    }
+    if (ht.exchange(ht.user, nq, L.nbr_ranks.data(), h_send, soff.data(), scnt.data(), h_recv,
+                    roff.data(), rcnt.data()) != 0)
+      return fail(PNP_E_RCCL, "host transport: exchange failed");
+    if (nrecv)
+      e = hipMemcpyAsync(vec + size_t(L.n_owned) * nfv, h_recv, sizeof(double) * nrecv,
+                         hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);  // h_recv is reused by the next call
+    if (e != hipSuccess) return hipfail(e, "halo copy");
+    if (t0) te(T_HALO, t0);
     return PNP_OK;
   }
 
@@ -592,6 +631,24 @@ struct pnp_ctx {
         for (int j = 0; j < k; j++) sum[j] += lg->host[r][j];
       lg->barrier();
       e = hipMemcpyAsync(d, sum.data(), sizeof(double) * k, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      return e == hipSuccess ? PNP_OK : hipfail(e, "allreduce");
+    }
+    if (host_tr()) {
+      if (size_t(k) > h_red_n) {
+        if (h_red) hipHostFree(h_red);
+        h_red = nullptr;
+        h_red_n = 0;
+        hipError_t e = hipHostMalloc(&h_red, sizeof(double) * size_t(k));
+        if (e != hipSuccess) return hipfail(e, "allreduce staging");
+        h_red_n = size_t(k);
+      }
+      hipError_t e = hipMemcpyAsync(h_red, d, sizeof(double) * k, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return hipfail(e, "allreduce");
+      if (ht.allreduce_sum(ht.user, h_red, k) != 0)
+        return fail(PNP_E_RCCL, "host transport: allreduce failed");
+      e = hipMemcpyAsync(d, h_red, sizeof(double) * k, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) e = hipStreamSynchronize(stream);
       return e == hipSuccess ? PNP_OK : hipfail(e, "allreduce");
     }
@@ -802,6 +859,13 @@ struct pnp_ctx {
     for (int R = 0; R < n; R++)
       if (!empty(R) && diag[R] < 0) return fail(PNP_E_STATE, "natural SSOR: row without diagonal");
     if ((rc = upv(csr_diag, diag, "csr diagonal"))) return rc;
+    // the dataflow sweeps keep their results and operands in the external (lexicographic) layout
+    // R = f * nv + g, which is local in the sweep order (indexing them by internal position
+    // instead made the PNP heads 10-16 % slower, profiles/r05/nat_split_r5e.txt), but read d at
+    // the row's INTERNAL position g2l[g] * nf + f (info.w / rec.w), so that the preconditioner's
+    // input needs no scatter into an external copy (PNP config 3: 20 us per application,
+    // profiles/r05/nat_split_r5d.txt); the result is gathered out of vb afterwards
+    auto P = [&](int R) { return L.g2l[R % nv] * nf + R / nv; };
     auto schedule = [&](bool fwd, NatDir &W) -> int {
       std::vector<int> &lptr = W.lptr;
       std::vector<int> lev(n, -1), push(n, 0);
@@ -845,7 +909,7 @@ struct pnp_ctx {
         const int nl = lptr[l + 1] - lptr[l];
         for (int t = lptr[l]; t < lptr[l + 1]; t++) {
           const int R = rl[t], len = cnt[R + 1] - cnt[R];
-          info[t] = make_int4(R, len, diag[R], 0);
+          info[t] = make_int4(R, len, diag[R], P(R));
           for (int k = 0; k < len; k++) {
             const size_t q = size_t(W.eoff[l]) + size_t(k) * nl + (t - lptr[l]);
             const int C = col[cnt[R] + k];
@@ -952,20 +1016,17 @@ struct pnp_ctx {
             for (size_t t = 0; t < G.size(); t++) {
               const int R = G[t];
               const int len = cnt[R + 1] - cnt[R];
-              rec.push_back(make_int4(R, len, diag[R], 0));
+              rec.push_back(make_int4(R, len, diag[R], P(R)));
               for (int k = 0; k < wpad; k++) {
                 if (k < len) {
                   const int C = col[cnt[R] + k];
                   const int fc = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
-                  // kind: 0 zero, 1 forward value, 2 backward value, 3 in the wave's registers;
-                  // | 4: final when the chain launch begins (the other sweep's value, or a row of
-                  // this sweep's head launch), a plain load the kernel never polls
-                  int code = fc == -1 ? 0 : fc >= 0 ? (fc << 3 | 1) : ((-(fc + 2)) << 3 | 2);
+                  // kind: 0 zero, 1 forward value, 2 backward value, 3 in the wave's registers
+                  int code = fc == -1 ? 0 : fc >= 0 ? (fc << 2 | 1) : ((-(fc + 2)) << 2 | 2);
                   const bool fresh = fwd ? (code & 3) == 1 : (code & 3) == 2;  // this sweep's value
-                  if (code != 0 && (!fresh || lev[C] < ltail)) code |= 4;
                   for (int h = 1; fresh && h <= H && size_t(h) <= t; h++)
                     if (G[t - h] == C) {
-                      code = h << 3 | 3;
+                      code = h << 2 | 3;
                       break;
                     }
                   ecode.push_back(code);
@@ -1025,8 +1086,10 @@ struct pnp_ctx {
     nat_max_width = 0;
     if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
     if (nat_units_ok && (rc = upv(d_nat_units, nat_units, "natural SSOR units"))) return rc;
+    const int ni = std::max(1, nf * (L.n_owned + L.n_ghost));  // internal layout
     if ((e = nat_d.alloc(std::max(1, n))) != hipSuccess || (e = nat_v.alloc(std::max(1, n))) != hipSuccess ||
-        (e = nat_vf.alloc(std::max(1, n))) != hipSuccess || (e = nat_abort.alloc(4)) != hipSuccess ||
+        (e = nat_vf.alloc(std::max(1, n))) != hipSuccess || (e = nat_di.alloc(ni)) != hipSuccess ||
+        (e = nat_vi.alloc(ni)) != hipSuccess || (e = nat_abort.alloc(4)) != hipSuccess ||
         (e = hipMemset(nat_abort.p, 0, 16)) != hipSuccess)
       return hipfail(e, "natural SSOR vectors");
     csr_nnz = nnz;
@@ -1049,13 +1112,9 @@ struct pnp_ctx {
   }
 
   // v = SSOR_natural^{-1} d on internal-layout owned rows (ssor_natural.hip); csr_values() first
-  hipError_t ssor_natural(const double *d, double *vout) {
-    const int nv = mesh.nv;
-    hipError_t e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
-    if (e == hipSuccess) e = nat_sweep();
-    if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
-    return e;
-  }
+  // (internal layout, owned rows; d == vout allowed: the result is gathered into vout after both
+  // sweeps)
+  hipError_t ssor_natural(const double *d, double *vout) { return nat_sweep(d, vout); }
   // one launch for both sweeps (ssor_natural.hip, launch_ssor_natural_flow) whenever this context
   // owns its GPU: one rank, or one rank of an RCCL communicator (one process per GPU, each rank
   // sweeping its owned rows -- block Jacobi across ranks, as ISTL's NOVLP SeqSSOR on the local
@@ -1069,19 +1128,19 @@ struct pnp_ctx {
     }();
     return nat_flow_opt == 0 ? false
            : nat_flow_opt == 1 ? nat_units_ok
-                               : env_on && !lg && nat_units_ok;
+                               : env_on && !lg && !host_tr() && nat_units_ok;
   }
   int nat_flow_opt = -1;  // PNP_OPT_NAT_FLOW: -1 auto (above), 0 level launches, 1 dataflow
   long long nat_flow_n = 0, nat_level_n = 0;  // applications per schedule (pnp_info)
-  hipError_t nat_sweep() {
+  hipError_t nat_sweep(const double *d, double *vout) {
     if (use_nat_flow()) {
       nat_flow_n++;
-      return ssor_natural_flow();
+      return ssor_natural_flow(d, vout);
     }
     nat_level_n++;
-    return ssor_natural_levels();
+    return ssor_natural_levels(d, vout);
   }
-  hipError_t ssor_natural_flow() {
+  hipError_t ssor_natural_flow(const double *d, double *vout) {
     pnp::NatFlow F;
     F.units = d_nat_units.p;
     F.nunits = int(nat_units.size());
@@ -1094,8 +1153,13 @@ struct pnp_ctx {
     F.fwd = nat_f.view();
     F.bwd = nat_b.view();
     F.abort_word = nat_abort.p;
-    return pnp::launch_ssor_natural_flow(F, nf * mesh.nv, csr_val.p, nat_d.p, nat_vf.p, nat_v.p,
-                                         stream);
+    hipError_t e = pnp::launch_ssor_natural_flow(F, nf * mesh.nv, csr_val.p, d, nat_vf.p, nat_v.p,
+                                                 stream);
+    // the result out of the external-layout vb (storing it at internal positions from the
+    // backward kernels as well cost more than this gather: +40 against 22 us, r5f)
+    if (e == hipSuccess)
+      e = pnp::launch_gather_ext(L.n_owned, nf, mesh.nv, d_l2g.p, nat_v.p, vout, stream);
+    return e;
   }
   // a dataflow sweep that timed out (never expected: every unit waits only on earlier units, all
   // resident) leaves NaN results and a sticky word; the solve reports it as an error
@@ -1285,7 +1349,16 @@ struct pnp_ctx {
   // the level launches: one graph replay (captured on first use; PNP_NAT_GRAPH=0: eager), or eager
   // when the stream is itself being captured (a BiCGSTAB block graph then holds them), with more
   // than one rank, or after a failed capture
-  hipError_t ssor_natural_levels() {
+  // (on the context's external-layout nat_d / nat_v, so that the captured level graph's arguments
+  // stay valid whatever vectors the caller passes)
+  hipError_t ssor_natural_levels(const double *d, double *vout) {
+    const int nv = mesh.nv;
+    hipError_t e = pnp::launch_scatter_ext(L.n_owned, nf, nv, d_l2g.p, d, nat_d.p, stream);
+    if (e == hipSuccess) e = ssor_natural_levels_fixed();
+    if (e == hipSuccess) e = pnp::launch_gather_ext(L.n_owned, nf, nv, d_l2g.p, nat_v.p, vout, stream);
+    return e;
+  }
+  hipError_t ssor_natural_levels_fixed() {
     auto issue = [&] {
       hipError_t e0 = hipMemsetAsync(nat_v.p, 0, sizeof(double) * nat_v.n, stream);
       return e0 != hipSuccess ? e0
@@ -2250,11 +2323,10 @@ struct pnp_ctx {
     hipError_t e;
     if (prec == PNP_PREC_NONE || prec == PNP_PREC_JACOBI) {
       e = pnp::launch_seq_prec_diag(n, prec == PNP_PREC_JACOBI, d, csr_diag.p, csr_val.p, v, stream);
-    } else {  // SSOR_NATURAL: the natural-order sweep on the CSR view
-      e = hipMemcpyAsync(nat_d.p, d, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
-      if (e == hipSuccess) e = nat_sweep();
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(v, nat_v.p, sizeof(double) * n, hipMemcpyDeviceToDevice, stream);
+    } else {  // SSOR_NATURAL: the natural-order sweep on the CSR view (internal positions)
+      e = pnp::launch_gather_ext(L.n_owned, nf, mesh.nv, d_l2g.p, d, nat_di.p, stream);
+      if (e == hipSuccess) e = nat_sweep(nat_di.p, nat_vi.p);
+      if (e == hipSuccess) e = pnp::launch_scatter_ext(L.n_owned, nf, mesh.nv, d_l2g.p, nat_vi.p, v, stream);
     }
     return e == hipSuccess ? PNP_OK : hipfail(e, "seq preconditioner");
   }
@@ -2627,8 +2699,8 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     c->rank = comm->rank;
     c->nranks = comm->size;
     if (comm->rank < 0 || comm->rank >= comm->size ||
-        (!comm->rccl_unique_id && !comm->local_group)) {
-      g_err = "invalid pnp_comm (need an RCCL unique id or a local group)";
+        (!comm->rccl_unique_id && !comm->local_group && !comm->host)) {
+      g_err = "invalid pnp_comm (need an RCCL unique id, a local group or a host transport)";
       return PNP_E_ARG;
     }
   }
@@ -3141,7 +3213,21 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     g_err = c->err;
     return rc;
   }
-  if (c->nranks > 1 && !comm->rccl_unique_id) {  // join the in-process group
+  if (c->nranks > 1 && !comm->rccl_unique_id && !comm->local_group) {  // host-staged transport
+    if (!comm->host->exchange || !comm->host->allreduce_sum) {
+      g_err = "pnp_host_transport: exchange and allreduce_sum are required";
+      return PNP_E_ARG;
+    }
+    c->ht = *comm->host;
+    const size_t ns = 3 * std::max<size_t>(1, L.send_idx.size());
+    const size_t nr = 3 * std::max<size_t>(1, size_t(L.n_ghost));
+    if ((e = hipHostMalloc(&c->h_send, sizeof(double) * ns)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_recv, sizeof(double) * nr)) != hipSuccess) {
+      g_err = std::string("host transport staging: ") + hipGetErrorString(e);
+      return PNP_E_HIP;
+    }
+  }
+  if (c->nranks > 1 && !comm->rccl_unique_id && comm->local_group) {  // join the in-process group
     std::shared_ptr<LocalGroup> g;
     {
       std::lock_guard<std::mutex> lk(g_groups_m);
@@ -3198,7 +3284,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->ilu_f32 = c->ilu_f32;
   info->degree = c->degree;
   info->color_conflicts = c->L.conflicts;
-  info->transport = c->comm ? 2 : (c->lg ? 1 : 0);
+  info->transport = c->comm ? 2 : c->lg ? 1 : c->host_tr() ? 3 : 0;
   info->nat_flow_applies = c->nat_flow_n;
   info->nat_level_applies = c->nat_level_n;
   info->ilu_flow_applies = c->ilu_flow_n;

@@ -440,11 +440,12 @@ hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *va
                            const int *src, const unsigned char *vidx, double *out, hipStream_t s);
 // ISTL SeqSSOR (k = 1, omega = 1) in the lexicographic DOF order (ssor_natural.hip): v = 0, then
 // the forward levels and the backward levels, one launch per level.  Per sweep direction
-// (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row,
-// entry count, index of the diagonal in val, 0}; the row's entries in CSR (ascending column)
-// order as a column-major ELL of the level, entry k of position t at eoff[l] + k n_l + (t -
-// lptr[l]) (eoff: host array; n_l = the level's row count): its column (ecol) and its index into
-// the external-layout CSR values val (eidx).  d / v: external-layout vectors.
+// (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row
+// (external index), entry count, index of the diagonal in val, the row's internal position}; the
+// row's entries in CSR (ascending column) order as a column-major ELL of the level, entry k of
+// position t at eoff[l] + k n_l + (t - lptr[l]) (eoff: host array; n_l = the level's row count):
+// its column (ecol) and its index into the external-layout CSR values val (eidx).  The level
+// launches: d / v external-layout vectors.
 struct NatSweep {
   int nlev = 0;
   const int *lptr = nullptr;
@@ -458,8 +459,9 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
 // {first sweep position, rows | width << 8 | backward << 16, the level's row count, ELL index of
 // the unit's first row}, forward units (nunits_f) then backward ones, each in level order.  An
 // operand code in ecol (both forms): c >= 0 the forward value of row c, c == -1 zero, c <= -2 the
-// backward value of row -(c + 2).  vf / vb (n each): forward / backward results; abort_word[0]
-// is set when an operand wait times out.
+// backward value of row -(c + 2).  vf / vb (n each, external layout): forward / backward results;
+// d is read in the internal layout, at info.w / rec.w; abort_word[0] is set when an operand wait
+// times out.
 // rows per unit = rows per wavefront of the flow kernel (64 / its lanes per row)
 int ssor_natural_unit_rows();
 // the longest row the chain kernel takes (one entry per lane of its wave)
@@ -476,7 +478,8 @@ struct NatFlow {
   int tail_f = 0, tail_b = 0;
   int max_width = 0;  // the longest row of any unit (the pipelined head takes up to 24 entries)
   // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: the wave of group g
-  // walks rows gptr[g] .. gptr[g+1] of rec ({ext row, entry count, diagonal value index, 0}); row
+  // walks rows gptr[g] .. gptr[g+1] of rec ({external row, entry count, diagonal value index,
+  // internal position}); row
   // q's entries at q * wpad .. + count of ecode (idx << 2 | kind: 0 zero, 1 vf[idx], 2 vb[idx],
   // 3 the group's result idx rows back) and eidx (value indices, -1 padding)
   struct Chains {

@@ -28,6 +28,7 @@
 #include "kernels.h"
 
 #include <climits>
+#include <cstdint>
 #include <cstdlib>
 #include <algorithm>
 
@@ -137,15 +138,19 @@ __device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p
 }
 
 // PAD > 0: the workgroup reserves PAD bytes of LDS it never uses, so that at most one workgroup
-// runs per CU (the sparse tail grid, below)
-template <int BLK, int SCOPE, int PAD = 0>
+// runs per CU (the sparse tail grid, below).  KS: entries per lane and pass (KS * kL per row and
+// pass); rows longer than that take several passes, each a full load -> poll round trip.  The PNP
+// head runs with KS = 4 (32 entries): its phi rows have 3 (degree + 1) entries, 27 at degree 8,
+// which with 24 split every unit holding such a row into two passes.
+template <int BLK, int SCOPE, int PAD = 0, int KS = kS>
 __global__ void __launch_bounds__(BLK)
     k_ssor_nat_flow(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
                     const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
                     const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
                     const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
                     const double *__restrict__ val, const double *__restrict__ d,
-                    unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
+                    unsigned long long *vf, unsigned long long *vb, unsigned *abort_word,
+                    int spec = 0) {
   if constexpr (PAD > 0) {
     __shared__ char pad[PAD];
     if (u0 < 0) reinterpret_cast<volatile char *>(pad)[threadIdx.x] = 1;  // never: u0 >= 0
@@ -162,42 +167,45 @@ __global__ void __launch_bounds__(BLK)
     const bool head = live && j == 0;
     const int4 I = live ? info[U.x + t] : make_int4(0, 0, 0, 0);
     double rhs = 0.0;
-    for (int kb = 0; kb < width; kb += kC) {
-      int c[kS], ix[kS];
+    for (int kb = 0; kb < width; kb += KS * kL) {
+      int c[KS], ix[KS];
 #pragma unroll
-      for (int q = 0; q < kS; q++) {
+      for (int q = 0; q < KS; q++) {
         const int k = kb + j + q * kL;
         const bool in = live && k < width;
         const size_t at = size_t(U.w) + size_t(k) * U.z + t;
         c[q] = in ? ecol[at] : -1;
         ix[q] = in ? eidx[at] : -1;
       }
-      if (kb == 0 && head) rhs = d[I.x];
-      unsigned long long b[kS];
-      double a[kS];
+      if (kb == 0 && head) rhs = d[I.w];  // d: internal layout
+      unsigned long long b[KS];
+      double a[KS];
 #pragma unroll
-      for (int q = 0; q < kS; q++) {
+      for (int q = 0; q < KS; q++) {
         a[q] = ix[q] >= 0 ? val[ix[q]] : 0.0;
         // a backward unit's forward-value operands were final when the launch began (the forward
-        // sweep is an earlier launch): plain, cacheable loads; only this launch's results are polled
+        // sweep is an earlier launch): plain, cacheable loads; only this launch's results are
+        // polled (PNP config 3: backward head 464 -> 435 us, profiles/r05/nat_split_r5c.txt).
+        // With `spec`, a forward unit also tries a plain load first: a value that is not all-ones
+        // is final (each is written once), a pending one is polled as before
         b[q] = c[q] == -1 ? 0ull
-               : (bwd && c[q] >= 0) ? vf[c[q]]
-                                    : nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
+               : (c[q] >= 0 && (bwd || spec)) ? vf[c[q]]
+                                              : nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
       }
       bool pend = false;
 #pragma unroll
-      for (int q = 0; q < kS; q++) pend |= b[q] == kNatPending;
+      for (int q = 0; q < KS; q++) pend |= b[q] == kNatPending;
       if (__any(pend)) {
         const unsigned long long t0 = wall_clock64();
         // NAT_POLL_DEPTH polls in flight per pending operand: a new poll is issued every pass and
         // the oldest one consumed, so an arriving value is seen about one round trip after it
         // lands instead of up to two (depth 1: issue, wait, check)
         constexpr int PD = NAT_POLL_DEPTH;
-        unsigned long long fl[PD > 1 ? PD - 1 : 1][kS];
+        unsigned long long fl[PD > 1 ? PD - 1 : 1][KS];
 #pragma unroll
         for (int p = 0; p + 1 < PD; p++) {
 #pragma unroll
-          for (int q = 0; q < kS; q++)
+          for (int q = 0; q < KS; q++)
             fl[p][q] = b[q] == kNatPending
                            ? nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)))
                            : 0ull;
@@ -207,14 +215,14 @@ __global__ void __launch_bounds__(BLK)
           __builtin_amdgcn_s_sleep(1);
           pend = false;
           if constexpr (PD > 1) {
-            unsigned long long nw[kS];
+            unsigned long long nw[KS];
 #pragma unroll
-            for (int q = 0; q < kS; q++)
+            for (int q = 0; q < KS; q++)
               nw[q] = b[q] == kNatPending
                           ? nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)))
                           : 0ull;
 #pragma unroll
-            for (int q = 0; q < kS; q++)
+            for (int q = 0; q < KS; q++)
               if (b[q] == kNatPending) {
                 b[q] = fl[0][q];
                 pend |= b[q] == kNatPending;
@@ -222,12 +230,12 @@ __global__ void __launch_bounds__(BLK)
 #pragma unroll
             for (int p = 0; p + 2 < PD; p++)
 #pragma unroll
-              for (int q = 0; q < kS; q++) fl[p][q] = fl[p + 1][q];
+              for (int q = 0; q < KS; q++) fl[p][q] = fl[p + 1][q];
 #pragma unroll
-            for (int q = 0; q < kS; q++) fl[PD - 2][q] = nw[q];
+            for (int q = 0; q < KS; q++) fl[PD - 2][q] = nw[q];
           } else {
 #pragma unroll
-            for (int q = 0; q < kS; q++)
+            for (int q = 0; q < KS; q++)
               if (b[q] == kNatPending) {
                 b[q] = nat_ld<SCOPE>(c[q] >= 0 ? vf + c[q] : vb + (-(c[q] + 2)));
                 pend |= b[q] == kNatPending;
@@ -239,17 +247,17 @@ __global__ void __launch_bounds__(BLK)
                                                     __HIP_MEMORY_SCOPE_AGENT);
           if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
-            for (int q = 0; q < kS; q++)
+            for (int q = 0; q < KS; q++)
               if (b[q] == kNatPending) b[q] = 0x7FF8000000000000ull;  // NaN: drain the grid
             break;
           }
         }
       }
-      double pr[kS];
+      double pr[KS];
 #pragma unroll
-      for (int q = 0; q < kS; q++) pr[q] = ix[q] >= 0 ? a[q] * __longlong_as_double(b[q]) : 0.0;
+      for (int q = 0; q < KS; q++) pr[q] = ix[q] >= 0 ? a[q] * __longlong_as_double(b[q]) : 0.0;
 #pragma unroll
-      for (int k = 0; k < kC; k++) {
+      for (int k = 0; k < KS * kL; k++) {
         const double p = __shfl(pr[k / kL], base + k % kL, 64);
         if (head && kb + k < width) rhs -= p;
       }
@@ -293,16 +301,6 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
   auto ld = [&](const unsigned long long *q) {
     return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  // a launch holds the units of one sweep; in a backward launch every forward value is final
-  // (earlier launches), so those operands are plain, cacheable loads and never polled
-  const bool bwd_launch = u0 >= nunits_f;
-  auto ld_op = [&](int c) {  // both loads unconditional (see k_ssor_nat_chain's ld_op)
-    const bool fin = bwd_launch && c >= 0;
-    unsigned long long m = fin ? ~0ull : 0ull;
-    asm volatile("" : "+v"(m));  // an opaque mask: neither load can be predicated away
-    const unsigned long long p = *(fin ? vf + c : vf), a = ld(fin || c == -1 ? vf : opnd(c));
-    return (p & m) | (a & ~m);  // c == -1 (zero operand): a dummy, never used
-  };
   // two register sets per stage, used alternately (the loop below is unrolled by two), so that no
   // stage register is copied while its load is in flight
   int4 aU[2], aI[2];
@@ -344,12 +342,12 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
       // for those loads
       asm volatile("" : "+v"(bc[S][q]), "+v"(bx[S][q]));
       ba[S][q] = val[ax[S][q] >= 0 ? ax[S][q] : 0];
-      bb[S][q] = ld_op(ac[S][q]);
+      bb[S][q] = ld(ac[S][q] == -1 ? vf : opnd(ac[S][q]));
     }
     asm volatile("" : "+v"(brow[S]), "+v"(bw8[S]));
-    bd[S] = d[aI[S].x];
+    bd[S] = d[aI[S].w];  // d: internal layout
     bg[S] = val[aI[S].z];
-    bo[S] = vf[aI[S].x];  // the row's forward value (used by backward units only; final there)
+    bo[S] = ld(vf + aI[S].x);  // the row's forward value (backward units)
   };
   // Each row of the unit is stored as soon as ITS operands are final (ballot over its kL lanes),
   // not when the whole unit's are: a wide level's unit depends on ~24 producers, and waiting for
@@ -433,6 +431,23 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
+// vf[0..n) = vb[0..n) = the all-ones pending pattern, 16-B stores where both are 16-B aligned
+__global__ void __launch_bounds__(kB)
+    k_nat_pending(int n, double2 *vf2, double2 *vb2, double *vf, double *vb) {
+  const int i = blockIdx.x * kB + threadIdx.x;  // one pair of elements per lane
+  const double p = __longlong_as_double(~0ll);
+  const bool al = ((reinterpret_cast<uintptr_t>(vf) | reinterpret_cast<uintptr_t>(vb)) & 15) == 0;
+  if (al && 2 * i + 1 < n) {
+    vf2[i] = make_double2(p, p);
+    vb2[i] = make_double2(p, p);
+  } else {
+    for (int k = 2 * i; k < 2 * i + 2 && k < n; k++) {
+      vf[k] = p;
+      vb[k] = p;
+    }
+  }
+}
+
 constexpr int kTailBlk = 1024;  // the tail workgroup: 16 waves on one CU
 // The sparse tail grid (PNP_NAT_TAIL_WPC = 1, 2 or 4 waves per CU): the tail levels on a grid of
 // at most one workgroup per CU (96 KB of LDS reserved each), so that a consumer CU's memory queue
@@ -463,11 +478,8 @@ constexpr int kTailPad = 96 * 1024;
 // Progress: a row depends only on rows of lower levels and a group's rows are in increasing level
 // order, so the lowest uncomputed row's group is at that row and its operands are final; every
 // group's wave is resident (the host packs at most ssor_natural_chain_capacity() groups).
-// Operand codes (host): idx << 3 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
-// result idx (1..kChainH) rows back; kind | 4 (5, 6): vf / vb[idx] already final when the launch
-// begins (a forward value in the backward sweep, or a row of the head launch before this one), a
-// plain cacheable load that is never polled.  The row's own forward value (backward sweep) is
-// likewise final and plainly loaded.
+// Operand codes (host): idx << 2 | kind, kind 0: zero, 1: vf[idx], 2: vb[idx], 3: the group's
+// result idx (1..kChainH) rows back.
 #ifndef NAT_CHAIN_D
 #define NAT_CHAIN_D 2  // build-flag A/B knob: stage-B lead in steps (stage A leads by twice that)
 #endif
@@ -491,17 +503,8 @@ __global__ void __launch_bounds__(64)
     return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto opnd = [&](int c) {  // the operand's address (kind 0 and 3: a harmless dummy)
-    const int k = c & 3, i = c >> 3;
+    const int k = c & 3, i = c >> 2;
     return k == 1 ? vf + i : k == 2 ? vb + i : vf;
-  };
-  // both loads issued unconditionally (the other one at a harmless dummy address): a per-lane
-  // choice between two load kinds would make the compiler branch and drain the pipeline per load
-  auto ld_op = [&](int c) {
-    const bool fin = (c & 4) != 0;
-    unsigned long long m = fin ? ~0ull : 0ull;
-    asm volatile("" : "+v"(m));  // an opaque mask: neither load can be predicated away
-    const unsigned long long p = *(fin ? opnd(c) : vf), a = ld(fin ? vf : opnd(c));
-    return (p & m) | (a & ~m);
   };
   int4 ra[A];
   int ca[A], xa[A];
@@ -515,9 +518,9 @@ __global__ void __launch_bounds__(64)
   };
   auto stage_b = [&](int sa, int sb) {
     av[sb] = val[xa[sa] >= 0 ? xa[sa] : 0];
-    bv[sb] = ld_op(ca[sa]);
-    dv[sb] = d[ra[sa].x];
-    ov[sb] = bwd ? __longlong_as_double(vf[ra[sa].x]) : 0.0;  // the forward value (final)
+    bv[sb] = ld(opnd(ca[sa]));
+    dv[sb] = d[ra[sa].w];  // d: internal layout
+    ov[sb] = __longlong_as_double(ld(vf + ra[sa].x));  // the forward value (backward sweep)
     gv[sb] = val[ra[sa].z];
   };
 #pragma unroll
@@ -532,7 +535,7 @@ __global__ void __launch_bounds__(64)
     for (int i = 0; i < A; i++) {
       const int st = s + i;
       if (st < len) {  // uniform
-        const int c = ca[i], kind = c & 7, width = ra[i].y;
+        const int c = ca[i], kind = c & 3, width = ra[i].y;
         const bool live = lane < width;
         unsigned long long b = bv[i % D];
         bool pend = live && (kind == 1 || kind == 2) && b == kNatPending;
@@ -555,12 +558,12 @@ __global__ void __launch_bounds__(64)
             }
           }
         }
-        const int hi = c >> 3;
+        const int hi = c >> 2;
         double hv = h[0];
 #pragma unroll
         for (int q = 1; q < kChainH; q++)
           if (hi == q + 1) hv = h[q];
-        const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);  // 1,2,5,6
+        const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);
         const double pr = (live && xa[i] >= 0) ? av[i % D] * o : 0.0;
         const unsigned long long pb = __double_as_longlong(pr);
         const int plo = int(unsigned(pb)), phi = int(unsigned(pb >> 32));
@@ -604,8 +607,12 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     int per_flow = 0, per_pipe = 0;
+    int per_flow4 = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_flow,
                                                  k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>, kB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_flow4, k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT, 0, 4>, kB, 0);
+    per_flow = std::min(per_flow, per_flow4);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pipe, k_ssor_nat_pipe<kB>, kB, 0);
     per = std::min(per_flow, per_pipe);  // one grid size for both head kernels: all resident
     // 4 workgroups per CU (16 waves): fewer pollers than the occupancy allows and enough for
@@ -627,12 +634,26 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     const char *ev = std::getenv("PNP_NAT_PIPE");
     return !(ev && std::atoi(ev) == 0);
   }();
+  // PNP_NAT_FLOW_KS4=0: rows of 25-32 entries in two passes of 24 (A/B knob)
+  static const bool ks4 = [] {
+    const char *ev = std::getenv("PNP_NAT_FLOW_KS4");
+    return !(ev && std::atoi(ev) == 0);
+  }();
+  // PNP_NAT_SPEC=1: forward head units try plain loads first (A/B knob, default off)
+  static const int spec = [] {
+    const char *ev = std::getenv("PNP_NAT_SPEC");
+    return (ev && std::atoi(ev) != 0) ? 1 : 0;
+  }();
   static const int tail_wpc = [] {
     const char *ev = std::getenv("PNP_NAT_TAIL_WPC");
     return ev ? std::max(0, std::atoi(ev)) : 0;
   }();
-  hipError_t e = hipMemsetAsync(vf, 0xFF, sizeof(double) * size_t(n), s);
-  if (e == hipSuccess) e = hipMemsetAsync(vb, 0xFF, sizeof(double) * size_t(n), s);
+  // both result vectors to the pending pattern in one launch (two memsets cost four fill launches,
+  // ~23 us at config 3, profiles/r05/nat_split_r5d.txt)
+  if (n > 0)
+    hipLaunchKernelGGL(k_nat_pending, dim3((n + 2 * kB - 1) / (2 * kB)), dim3(kB), 0, s, n,
+                       reinterpret_cast<double2 *>(vf), reinterpret_cast<double2 *>(vb), vf, vb);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   auto vfu = reinterpret_cast<unsigned long long *>(vf);
   auto vbu = reinterpret_cast<unsigned long long *>(vb);
@@ -644,10 +665,16 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
         hipLaunchKernelGGL(k_ssor_nat_pipe<kB>, dim3(blocks), dim3(kB), 0, s, F.units, u0, ut,
                            F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx, F.bwd.info, F.bwd.ecol,
                            F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+      else if (F.max_width <= 4 * kL && ks4)
+        hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT, 0, 4>), dim3(blocks),
+                           dim3(kB), 0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol,
+                           F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
+                           F.abort_word, spec);
       else
         hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB),
                            0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
-                           F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+                           F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
+                           F.abort_word, spec);
     }
     if (u1 > ut && C.ngroups > 0)
       hipLaunchKernelGGL(k_ssor_nat_chain, dim3(C.ngroups), dim3(64), 0, s, C.gptr, C.rec, C.ecode,
@@ -658,7 +685,8 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
 #define NAT_TAIL_GRID(W)                                                                          \
   hipLaunchKernelGGL((k_ssor_nat_flow<64 * W, __HIP_MEMORY_SCOPE_AGENT, kTailPad>), dim3(blocks), \
                      dim3(64 * W), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,     \
-                     F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu, F.abort_word)
+                     F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,           \
+                     F.abort_word)
       if (per == 1) NAT_TAIL_GRID(1);
       else if (per == 2) NAT_TAIL_GRID(2);
       else NAT_TAIL_GRID(4);

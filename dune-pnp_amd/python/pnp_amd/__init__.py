@@ -82,9 +82,53 @@ class _Config(C.Structure):
                 ("defaulted", C.c_uint32)]
 
 
+_EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
+                           C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                           C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64))
+_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(C.c_double), C.c_int32)
+
+
+class _HostTransport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("exchange", _EXCHANGE_FN),
+                ("allreduce_sum", _ALLREDUCE_FN)]
+
+
 class _Comm(C.Structure):
     _fields_ = [("rank", C.c_int32), ("size", C.c_int32), ("rccl_unique_id", C.c_void_p),
-                ("local_group", C.c_char_p)]
+                ("local_group", C.c_char_p), ("host", C.POINTER(_HostTransport))]
+
+
+def _host_transport(obj):
+    """pnp_host_transport over a Python object with
+         exchange(nbr, sends, recv_counts) -> list of received arrays  (sends: list of arrays)
+         allreduce_sum(buf)  (in place, a float64 numpy array)
+    e.g. tools / tests built on torch.distributed (gloo).  Exceptions become a failed call."""
+    def exchange(_u, nq, nbr, sbuf, soff, scnt, rbuf, roff, rcnt):
+        try:
+            peers = [nbr[q] for q in range(nq)]
+            sends = [np.ctypeslib.as_array(sbuf, shape=(max(1, soff[q] + scnt[q]),))
+                     [soff[q]:soff[q] + scnt[q]].copy() for q in range(nq)]
+            got = obj.exchange(peers, sends, [rcnt[q] for q in range(nq)])
+            for q in range(nq):
+                if rcnt[q]:
+                    dst = np.ctypeslib.as_array(rbuf, shape=(roff[q] + rcnt[q],))
+                    dst[roff[q]:roff[q] + rcnt[q]] = got[q]
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the library as a failed exchange
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def allreduce(_u, buf, k):
+        try:
+            obj.allreduce_sum(np.ctypeslib.as_array(buf, shape=(k,)))
+            return 0
+        except Exception:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            return 1
+    fx, fa = _EXCHANGE_FN(exchange), _ALLREDUCE_FN(allreduce)
+    return _HostTransport(None, fx, fa), (fx, fa)
 
 
 class _Info(C.Structure):
@@ -432,14 +476,20 @@ class Context:
     """One GPU (one rank): mesh + parameters resident in HBM, one operator at a time."""
 
     def __init__(self, mesh: Mesh, params: Params, device=0, rank=0, size=1, unique_id=None,
-                 local_group=None, degree=1):
+                 local_group=None, degree=1, host_transport=None):
         """degree 2 / 3: the Lagrange P_k space (pnp_create_pk, the reference's PDEGREE); its
-        vectors have nfields x nn entries over the nodes of space()."""
+        vectors have nfields x nn entries over the nodes of space().  host_transport: an object
+        with exchange / allreduce_sum (see _host_transport) -- the host-staged transport
+        (pnp_comm.host) for ranks in separate processes without RCCL."""
         self.mesh, self.params = mesh, params
         self._uid = C.create_string_buffer(unique_id, 128) if unique_id else None
         self._grp = local_group.encode() if local_group else None
+        self._ht = None
+        if host_transport is not None:
+            ht, keep = _host_transport(host_transport)
+            self._ht = (ht, keep)  # callbacks must outlive the context
         comm = _Comm(rank, size, C.cast(self._uid, C.c_void_p).value if self._uid else None,
-                     self._grp)
+                     self._grp, C.pointer(self._ht[0]) if self._ht else None)
         h = C.c_void_p()
         m = mesh.c()
         _check(lib().pnp_create_pk(C.byref(m), C.byref(params.c), int(degree), int(device),

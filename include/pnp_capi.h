@@ -123,6 +123,23 @@ typedef struct {
 int pnp_config_read(const char *path, pnp_config *out);
 
 /* ---- context ------------------------------------------------------------------------------- */
+/* Host-staged transport (pnp_comm.host): the halo exchange and the reductions go through the
+ * caller's own communicator (an MPI, gloo or socket layer of the host program -- the reference's
+ * MPI under UG's loadBalance, src/pnp_solver_main.cc:93-108), with the bytes staged through
+ * pinned host memory.  For processes that cannot use RCCL (several ranks on one GPU, a host
+ * without xGMI peers, a debugging run); the partition, halo layout, owner masks and solver are the
+ * RCCL path's.  Both callbacks are collective and blocking and return 0 on success. */
+typedef struct {
+  void *user;
+  /* for q < nnbr: send scount[q] doubles at sbuf + soff[q] to rank nbr[q] and receive rcount[q]
+     doubles from it into rbuf + roff[q] (the same neighbour list on both sides of every pair) */
+  int32_t (*exchange)(void *user, int32_t nnbr, const int32_t *nbr, const double *sbuf,
+                      const int64_t *soff, const int64_t *scount, double *rbuf,
+                      const int64_t *roff, const int64_t *rcount);
+  /* buf[0..k) = its sum over all ranks, in place (every rank calls with the same k) */
+  int32_t (*allreduce_sum)(void *user, double *buf, int32_t k);
+} pnp_host_transport;
+
 typedef struct {
   int32_t rank, size;          /* this process' rank / number of GPUs (size 1: no RCCL) */
   const void *rccl_unique_id;  /* 128-byte ncclUniqueId from rank 0 (ignored when size == 1) */
@@ -131,6 +148,8 @@ typedef struct {
                                   the communicator (one host thread per rank; device-to-device
                                   copies + host barriers instead of RCCL).  Same partition, halo
                                   and reduction code paths as RCCL. */
+  const pnp_host_transport *host; /* if non-NULL (and no RCCL id / local group): the host-staged
+                                  transport above, borrowed for the context's lifetime */
 } pnp_comm;
 
 int pnp_create(const pnp_mesh *mesh, const pnp_params *params, int32_t device,
@@ -168,7 +187,8 @@ typedef struct {
                               sweeps (SSOR, ILU(0)) leave out, see DESIGN.md §3 */
   int32_t transport;     /* 0 one rank, 1 in-process local group, 2 RCCL (also a 1-rank RCCL
                             communicator: a pnp_comm of size 1 with an RCCL id runs the
-                            multi-rank code path, every reduction an ncclAllReduce) */
+                            multi-rank code path, every reduction an ncclAllReduce), 3 the
+                            host-staged transport (pnp_comm.host) */
   int64_t nat_flow_applies;  /* PNP_PREC_SSOR_NATURAL applications run as one dataflow launch
                                 (any context that owns its GPU: one rank, or one RCCL rank) */
   int64_t nat_level_applies; /* ... and as level launches (the in-process local group, whose

@@ -1,5 +1,5 @@
 """Split a rocprofv3 kernel trace of natural-SSOR applications (PNP_NAT_CHAIN set) into its four
-launches per application -- forward head (k_ssor_nat_flow), forward chains (k_ssor_nat_chain),
+launches per application -- forward head (k_ssor_nat_flow or _pipe), forward chains (k_ssor_nat_chain),
 backward head, backward chains -- and print the average and spread of each, per run segment
 (a segment = consecutive applications with the same grid sizes).
 usage: python tools/nat_split.py <kernel_trace.csv>"""
@@ -12,7 +12,7 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     seq = [(r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), r.get("Grid_Size_X", r.get("Grid_Size", "")))
-           for r in rows if "k_ssor_nat_flow" in r["Kernel_Name"] or "k_ssor_nat_chain" in r["Kernel_Name"]]
+           for r in rows if any(k in r["Kernel_Name"] for k in ("k_ssor_nat_flow", "k_ssor_nat_pipe", "k_ssor_nat_chain"))]
     apps, cur = [], []
     for name, dur, grid in seq:
         kind = "chain" if "k_ssor_nat_chain" in name else "flow"
