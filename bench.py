@@ -75,6 +75,24 @@ def pmc_traffic(kernel_prefix):
 
 
 ASM_REGIMES = os.path.join(ROOT, "profiles", "r04", "final", "asm_regimes_config3_final.json")
+BICG_SPLIT = os.path.join(ROOT, "profiles", "r05", "bicg_split_final.json")
+
+
+def profile_bicg(config):
+    """The committed per-config BiCGSTAB kernel split (tools/prof_bicg.py under rocprofv3
+    --kernel-trace, split by tools/bicg_split.py): per kernel class the trace's device time per unit,
+    the event timers' time of the same pass and the fraction of 8 TB/s on the stored-format bytes;
+    None when absent."""
+    for path in (BICG_SPLIT, BICG_SPLIT.replace("_final", "_r5a")):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for ph in d["phases"]:
+            if ph["config"] == config:
+                return dict(ph["classes"], source=os.path.relpath(path, ROOT))
+    return None
 
 
 def profile_regime(name):
@@ -93,23 +111,29 @@ def profile_regime(name):
 BLAS_KERNELS = ("k_update_fwd0", "k_update_xr", "k_update_p", "k_reduce")
 
 
-def pmc_blas_bytes():
+PMC_DOFS = 2214099  # the committed PMC summaries profile config 3 (tools/prof_target.py 4)
+
+
+def pmc_blas_bytes(dofs=PMC_DOFS):
     """HBM-side bytes per BiCGSTAB iteration of the vector-update and reduction kernels (the
     device timers' `blas` class), from the committed PMC summary: per kernel its mean bytes per
     launch x its launches per iteration (the summary records the iterations its run made), FETCH_SIZE
-    x 2 as calibrated in profiles/r04/calib (every access width the hot path uses).  None when no
-    summary records its iteration count."""
+    x 2 as calibrated in profiles/r04/calib (every access width the hot path uses), scaled from the
+    profiled system's DOFs to `dofs` (the update kernels stream whole vectors: bytes per DOF are
+    size-independent).  None when no summary records its iteration count."""
     d = pmc_summary()
     if not d or not d.get("bicgstab_iterations"):
         return None
     it = d["bicgstab_iterations"]
+    scale = dofs / float(d.get("dofs", PMC_DOFS))
     tot, parts = 0.0, {}
     for name, v in d["kernels"].items():
         if any(k in name for k in BLAS_KERNELS):
-            b = v["traffic_bytes"] * v["launches_fetch"] / it
+            b = v["traffic_bytes"] * v["launches_fetch"] / it * scale
             parts[name.split("(")[0].replace("void pnp::(anonymous namespace)::", "")] = b
             tot += b
-    return {"bytes": tot, "per_kernel": parts, "source": d["path"]}
+    return {"bytes": tot, "per_kernel": parts, "source": d["path"],
+            "scaled_from_dofs": float(d.get("dofs", PMC_DOFS))}
 
 
 def tile_mesh(mesh, n):
@@ -309,7 +333,7 @@ def byte_models(info, nf, N_local, T_local, prec):
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
     if info["ilu_f32"] and info["nvb"] == 7:
         ilu -= 16 * V  # the forward steps read only the 12-B lower tail of each diagonal block
-    pb = pmc_blas_bytes()
+    pb = pmc_blas_bytes(N_local)
     # the update kernels' counted bytes (PMC); ~24 vector passes (the contract's 192 N) only when
     # no committed summary has them
     blas = pb["bytes"] if pb else 192 * N_local
@@ -802,7 +826,9 @@ def main():
                   "roofline_assembly_warm": S["asm_warm"], "roofline_assembly_cold": S["asm_cold"],
                   "roofline_bicgstab_stored": S["it_stored"], "spmv_stored": S["spmv_stored"],
                   "roofline_assembly_in_situ": S["asm_situ"],
-                  "ilu0_apply_stored": S["ilu_stored"], "colors": S["info"]["ncolors"],
+                  "ilu0_apply_stored": S["ilu_stored"], "blas_per_iter": S["blas"],
+                  "kernels_profile": profile_bicg(5) if world == 1 else None,
+                  "colors": S["info"]["ncolors"],
                   "ghost_vertices": S["info"]["nv_ghost"], "setup_s": s_setup,
                   "halo_ms_per_iter": S["timers"]["halo_ms"] / args.bicg_iters,
                   "allreduce_ms_per_iter": S["timers"]["allreduce_ms"] / args.bicg_iters}
@@ -935,7 +961,13 @@ def main():
                                                          "fp64 CSR the contract counts)",
                                   "kernels": with_stream_fracs(
                                       {"spmv": M["spmv_stored"], "ilu0_apply": M["ilu_stored"],
-                                       "blas_per_iter": M["blas"]}, stream_gbs)},
+                                       "blas_per_iter": M["blas"]}, stream_gbs),
+                                  "kernels_profile": (profile_bicg(3) if args.scaling == "weak"
+                                                      and world == 1 else None),
+                                  "kernels_timing": "event pairs around each unit's launches "
+                                                    "(launch gaps included); kernels_profile: "
+                                                    "the same pass's device time per unit from "
+                                                    "the committed kernel trace"},
             "cpu_baseline": cpu,
             "cpu_baseline_multithread": cpu_all,
             "setup_s": t_setup,

@@ -892,26 +892,34 @@ struct pnp_ctx {
       std::vector<int> fill(lptr.begin(), lptr.end() - 1), rl(std::max(1, lptr[nlev]));
       for (int R = 0; R < n; R++)
         if (lev[R] >= 0) rl[fill[lev[R]]++] = R;
-      // per level a column-major ELL of its rows' entries (CSR order), width = its longest row,
-      // padding slots with value index -1
+      // per level an ELL of its rows' entries (CSR order), width = its longest row, padding
+      // slots with value index -1, stored unit by unit: the level's rows in groups of UR (the
+      // dataflow units), each group's entries k-major, entry k of the group's row r at
+      // (group * width + k) * UR + r.  A unit's slots are then one contiguous run of lines that no
+      // other unit touches (column-major over the whole level, 4 units shared every line of a
+      // slot, fetched once per XCD that ran one of them: the PNP head missed L2 ~16.7 M times per
+      // launch, profiles/r05/nat_pmc_mem_r5a.json)
+      const int UR = pnp::ssor_natural_unit_rows();
       std::vector<int4> info(std::max(1, lptr[nlev]));
+      std::vector<int> lwidth(nlev, 0);
       W.eoff.assign(nlev + 1, 0);
       for (int l = 0; l < nlev; l++) {
         int w = 0;
         for (int t = lptr[l]; t < lptr[l + 1]; t++) w = std::max(w, cnt[rl[t] + 1] - cnt[rl[t]]);
-        W.eoff[l + 1] = W.eoff[l] + (long long)w * (lptr[l + 1] - lptr[l]);
+        lwidth[l] = w;
+        W.eoff[l + 1] = W.eoff[l] + (long long)w * UR * ((lptr[l + 1] - lptr[l] + UR - 1) / UR);
       }
       // operand codes (NatSweep): the forward sweep reads the new value of an earlier row (C < R)
       // and zero for the row itself and later rows; the backward sweep reads the forward value of
       // rows C <= R and the new backward value of later rows; rows of other ranks read zero
       std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), -1), eidx(ecol.size(), -1);
       for (int l = 0; l < nlev; l++) {
-        const int nl = lptr[l + 1] - lptr[l];
         for (int t = lptr[l]; t < lptr[l + 1]; t++) {
-          const int R = rl[t], len = cnt[R + 1] - cnt[R];
+          const int R = rl[t], len = cnt[R + 1] - cnt[R], tl = t - lptr[l];
           info[t] = make_int4(R, len, diag[R], P(R));
           for (int k = 0; k < len; k++) {
-            const size_t q = size_t(W.eoff[l]) + size_t(k) * nl + (t - lptr[l]);
+            const size_t q =
+                size_t(W.eoff[l]) + (size_t(tl / UR) * lwidth[l] + k) * UR + size_t(tl % UR);
             const int C = col[cnt[R] + k];
             ecol[q] = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
             eidx[q] = cnt[R] + k;
@@ -919,8 +927,9 @@ struct pnp_ctx {
         }
       }
       // dataflow units for the one-launch sweep: up to ssor_natural_unit_rows() consecutive rows of one level,
-      // {first sweep position, rows | width << 8, the level's row count, ELL index of the unit's
-      // first row}; forward units in level order, then backward units in level order.  The
+      // {first sweep position, rows | width << 8, the ELL stride between a row's entries (UR), ELL
+      // index of the unit's first row}; forward units in level order, then backward units in level
+      // order.  The
       // sweep's tail -- the levels from the last one wider than PNP_NAT_TAIL rows to its end --
       // can run in one workgroup (ssor_natural.hip); default 0 (no tail): one CU is slower
       // (PNP config 3: 2.36 ms per application without, 3.29 / 4.83 ms with 512 / 1024-row tails,
@@ -1059,17 +1068,15 @@ struct pnp_ctx {
       }
       for (int l = 0; l < nlev && nat_units_ok; l++) {
         if (l == ltail) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
-        const int nl = lptr[l + 1] - lptr[l];
-        const long long w = nl > 0 ? (W.eoff[l + 1] - W.eoff[l]) / nl : 0;
-        const int urows = pnp::ssor_natural_unit_rows();
-        for (int t0 = lptr[l]; t0 < lptr[l + 1]; t0 += urows) {
-          const long long e0 = W.eoff[l] + (t0 - lptr[l]);
+        const long long w = lwidth[l];
+        for (int t0 = lptr[l]; t0 < lptr[l + 1]; t0 += UR) {
+          const long long e0 = W.eoff[l] + (t0 - lptr[l]) / UR * w * UR;
           if (w > 255 || W.eoff[l + 1] > INT32_MAX) {
             nat_units_ok = false;
             break;
           }
-          const int rows = std::min(urows, lptr[l + 1] - t0);
-          nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), nl, int(e0)));
+          const int rows = std::min(UR, lptr[l + 1] - t0);
+          nat_units.push_back(make_int4(t0, rows | int(w) << 8 | (fwd ? 0 : 1 << 16), UR, int(e0)));
           nat_max_width = std::max(nat_max_width, int(w));
         }
       }

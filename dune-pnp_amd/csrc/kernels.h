@@ -442,10 +442,11 @@ hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *va
 // the forward levels and the backward levels, one launch per level.  Per sweep direction
 // (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row
 // (external index), entry count, index of the diagonal in val, the row's internal position}; the
-// row's entries in CSR (ascending column) order as a column-major ELL of the level, entry k of
-// position t at eoff[l] + k n_l + (t - lptr[l]) (eoff: host array; n_l = the level's row count):
-// its column (ecol) and its index into the external-layout CSR values val (eidx).  The level
-// launches: d / v external-layout vectors.
+// row's entries in CSR (ascending column) order as an ELL of the level stored unit-major: with
+// tl = t - lptr[l], entry k at eoff[l] + (tl / U * w_l + k) * U + tl % U (U =
+// ssor_natural_unit_rows(), w_l the level's width; eoff: host array): its column (ecol) and its
+// index into the external-layout CSR values val (eidx).  The level launches: d / v
+// external-layout vectors.
 struct NatSweep {
   int nlev = 0;
   const int *lptr = nullptr;
@@ -456,8 +457,8 @@ struct NatSweep {
 hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
                                const double *d, double *v, hipStream_t s);
 // The same two sweeps as ONE launch (dataflow): units of up to ssor_natural_unit_rows() rows of one level, int4
-// {first sweep position, rows | width << 8 | backward << 16, the level's row count, ELL index of
-// the unit's first row}, forward units (nunits_f) then backward ones, each in level order.  An
+// {first sweep position, rows | width << 8 | backward << 16, the ELL stride between a row's
+// entries (U), ELL index of the unit's first row}, forward units (nunits_f) then backward ones, each in level order.  An
 // operand code in ecol (both forms): c >= 0 the forward value of row c, c == -1 zero, c <= -2 the
 // backward value of row -(c + 2).  vf / vb (n each, external layout): forward / backward results;
 // d is read in the internal layout, at info.w / rec.w; abort_word[0] is set when an operand wait

@@ -1,9 +1,13 @@
-// Reference-order mode (PNP_OPT_SEQ_ORDER): the reference's sequential CPU arithmetic, operation
-// for operation and in its order, on the GPU, so that a Newton / BiCGSTAB run here takes the same
-// iterates -- and the same iteration counts on chaotic systems -- as the reference's single-rank
-// program.  A parity mode, not a speed mode: the fast path (assemble.hip, linalg.hip) sums in the
-// GPU's orders and its iteration counts agree with the reference's only as distributions where
-// BiCGSTAB is chaotic.
+// Reference-order mode (PNP_OPT_SEQ_ORDER): the CPU oracle's sequential restatement of the
+// reference's arithmetic, operation for operation and in its order, on the GPU, so that a Newton /
+// BiCGSTAB run here takes the same iterates -- and the same iteration counts on chaotic systems --
+// as the oracle's single-rank run.  A parity mode, not a speed mode: the fast path (assemble.hip,
+// linalg.hip) sums in the GPU's orders and its iteration counts agree with the oracle's only as
+// distributions where BiCGSTAB is chaotic.  One known difference from the DUNE
+// program remains in the rounding order: PDELab's local assembler adds alpha_boundary's terms into
+// the element's local vector before it scatters, and its one-step operator weights every
+// accumulated term, while this file (as the oracle) adds all volume terms, then the boundary
+// terms, then scales; parity with the DUNE program itself is unpinned.
 //
 // What "the reference's order" is, per step (this file is compiled with -ffp-contract=off: no
 // fused multiply-add anywhere, as on the reference's x86-64 build):

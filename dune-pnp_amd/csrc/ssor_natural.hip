@@ -38,9 +38,10 @@ namespace {
 constexpr int kB = 256;
 
 // A level is a short chain of dependent memory round trips per row, whatever its size, so the
-// sweep is laid out to keep that chain at two: the level's entries are a column-major ELL of its
-// rows (NatSweep: coalesced column / value-index loads that need nothing but the position, padding
-// marked by index -1), and each row is served by kL lanes, lane j loading entries j, j + kL, ...
+// sweep is laid out to keep that chain at two: the level's entries are an ELL of its rows, stored
+// unit-major (NatSweep: groups of kUR rows, each group's entries k-major -- coalesced column /
+// value-index loads that need nothing but the position, padding marked by index -1), and each row
+// is served by kL lanes, lane j loading entries j, j + kL, ...
 // (kS per pass) and forming their products.  Round trip 1: the row record and the ELL slots; round
 // trip 2: d, the diagonal and the gathered values.  The row's first lane then subtracts the
 // products in column order, taken from the other lanes by shuffles: the oracle's operations in
@@ -51,6 +52,7 @@ constexpr int kB = 256;
 #define NAT_KL 8  // lanes per row (build-flag A/B knob)
 #endif
 constexpr int kL = NAT_KL, kS = (24 + kL - 1) / kL, kC = kS * kL;  // PNP rows: <= 21 entries
+constexpr int kUR = 64 / kL;  // rows per dataflow unit (one wavefront): the ELL's group size
 __global__ void __launch_bounds__(kB)
     k_ssor_nat_level(const int4 *__restrict__ info, const int *__restrict__ ecol,
                      const int *__restrict__ eidx, int n, int width,
@@ -68,8 +70,9 @@ __global__ void __launch_bounds__(kB)
     for (int u = 0; u < kS; u++) {
       const int k = kb + j + u * kL;
       const bool in = live && k < width;
-      c[u] = in ? ecol[size_t(k) * n + t] : -1;
-      ix[u] = in ? eidx[size_t(k) * n + t] : -1;
+      const size_t at = (size_t(t / kUR) * width + k) * kUR + size_t(t % kUR);  // unit-major ELL
+      c[u] = in ? ecol[at] : -1;
+      ix[u] = in ? eidx[at] : -1;
     }
     if (kb == 0 && head) rhs = d[I.x];
     double pr[kS];
@@ -589,7 +592,7 @@ __global__ void __launch_bounds__(64)
 }
 }  // namespace
 
-int ssor_natural_unit_rows() { return 64 / kL; }
+int ssor_natural_unit_rows() { return kUR; }
 int ssor_natural_chain_width() { return 64; }
 int ssor_natural_chain_history() { return kChainH; }
 int ssor_natural_chain_capacity() {
@@ -707,7 +710,8 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
   for (const NatSweep *W : {&fwd, &bwd})
     for (int l = 0; l < W->nlev; l++) {
       const int n = W->lptr[l + 1] - W->lptr[l];
-      const int width = n > 0 ? int((W->eoff[l + 1] - W->eoff[l]) / n) : 0;
+      const int nu = (n + kUR - 1) / kUR;  // the level's unit-major ELL (NatSweep)
+      const int width = n > 0 ? int((W->eoff[l + 1] - W->eoff[l]) / ((long long)nu * kUR)) : 0;
       hipLaunchKernelGGL(k_ssor_nat_level, dim3((n * kL + kB - 1) / kB), dim3(kB), 0, s,
                          W->info + W->lptr[l], W->ecol + W->eoff[l], W->eidx + W->eoff[l], n,
                          width, val, d, v);

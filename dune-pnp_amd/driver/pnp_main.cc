@@ -15,9 +15,9 @@
 //                  PNP_PREC_SSOR_NATURAL; bcgs_ssork_mc: the multicolour sweep, same method, other order)
 //                 [--degree k]   (md / pb modes: PDEGREE, src/instationary_pnp_from_pb_md.hh:26-28;
 //                                 the dune_pnp_<solver>_<k> programs of src/Makefile.am:43-111)
-//                 [--reference-order]  (--reference-solvers with PNP_OPT_SEQ_ORDER: the reference's
-//                                 sequential arithmetic, so every Newton step's BiCGSTAB count is its
-//                                 single-rank program's; Newton prints its per-step lines)
+//                 [--reference-order]  (--reference-solvers with PNP_OPT_SEQ_ORDER: the CPU oracle's
+//                                 sequential arithmetic, so every Newton step's BiCGSTAB count is the
+//                                 oracle's; parity with the DUNE program itself unpinned)
 //                 [--reference-solvers]  (stationary / pb / instationary: the reference's own
 //                                 choices, src/stationary_pnp_from_pb.hh:168-169,329-331 -- PB with
 //                                 ISTLBackend_NOVLP_BCGS_SSORk = --pb-prec ssor_natural, PNP with
@@ -60,8 +60,8 @@ static void usage() {
       "                [--linear-solver bcgs_ssork|bcgs_ssork_mc|bcgs_noprec|cg_noprec|cg_jacobi|cg_amg_ssor]\n"
       "                [--abs-limit a] [--dump-steps n1,n2,...] [--degree 1|2|3]\n"
       "                [--reference-solvers]  (PB: ISTL SeqSSOR in DOF order, PNP: no preconditioner)\n"
-      "                [--reference-order]    (the same solvers in the reference's summation orders,\n"
-      "                                        PNP_OPT_SEQ_ORDER: per-step iteration counts as the reference's)\n");
+      "                [--reference-order]    (the same solvers in the CPU oracle's summation orders,\n"
+      "                                        PNP_OPT_SEQ_ORDER: per-step iteration counts as the oracle's)\n");
 }
 
 static void write_vector(const std::string &path, const V &v, int nv) {
@@ -266,7 +266,8 @@ int main(int argc, char **argv) {
                                       "and instationary drivers are P1: src/stationary_pnp_from_pb.hh:206-208)");
     pnp_gpu::Context ctx(mesh, params, device, world > 1 ? &comm : nullptr, degree);
     // PNP_OPT_SEQ_ORDER: element-order assembly, ISTL's sequential mv / dot / updates, so every
-    // Newton step takes the reference program's BiCGSTAB iteration count (one rank, P1)
+    // Newton step takes the CPU oracle's BiCGSTAB iteration count (one rank, P1; the DUNE
+    // program's own rounding order is unpinned)
     if (ref_order) pnp_gpu::check(pnp_set_option(ctx.get(), PNP_OPT_SEQ_ORDER, 1), ctx.get());
     const int newton_verbosity = rank == 0 ? (ref_order ? 2 : 1) : 0;
     int nv = ctx.nv();  // DOF nodes of the P_degree space
