@@ -483,60 +483,6 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
     __syncthreads();
     if (!live) return;
   }
-  double R[NF], D[NK], P[NK], F[NK];
-#pragma unroll
-  for (int f = 0; f < NF; f++) R[f] = 0;
-#pragma unroll
-  for (int v = 0; v < NK; v++) D[v] = P[v] = F[v] = 0;
-  if constexpr (LDSG == 2) {
-    // just-in-time: each element reads its two neighbour records from LDS when it needs them (an
-    // LDS round trip, hidden by the other waves), instead of holding the fan's records in
-    // registers from the start: ~40 VGPRs fewer, so 4 waves per SIMD fit in 128 VGPRs with 4
-    // workgroups' records (4 x <= 30 KiB) in the CU's 160 KiB of LDS
-    auto rec = [&](int k, double2 &p, double *u, double &x0, double &x1) {
-      const double *r = srec + size_t(cj[k]) * RW;
-      p = make_double2(r[0], r[1]);
-#pragma unroll
-      for (int f = 0; f < NF; f++) u[f] = r[2 + f];
-      x0 = AUX0 ? r[2 + NF] : 0.0;
-      x1 = AUX1 ? r[3 + NF] : 0.0;
-    };
-#pragma unroll
-    for (int s = 1; s < NS; s++) {
-      if (s < len) {
-        const bool has_next = s + 1 < len;
-        const int sn = (s + 1 < NS) ? s + 1 : 1;  // static slot of v_{s+1}
-        const bool elem = (has_next || closed) && !((brk >> s) & 1);
-        if (elem) {
-          double2 ps, pt;
-          double us[NF], ut[NF], as0, as1, at0, at1;
-          rec(s, ps, us, as0, as1);
-          rec(has_next ? sn : 1, pt, ut, at0, at1);  // v_{s+1}, or v_1 when a closed fan wraps
-          Geo G;
-          geometry(pi2.x, pi2.y, ps.x, ps.y, pt.x, pt.y, G);
-          double Ct[NK];
-#pragma unroll
-          for (int v = 0; v < NK; v++) Ct[v] = 0;
-          element<OP, JAC>(a, G, pi2.y, ps.y, pt.y, ui, us, ut, ai, as0, at0, aq, as1, at1, R, D,
-                           P, Ct);
-          if constexpr (JAC) {
-            if (s == 1 && closed) {
-#pragma unroll
-              for (int v = 0; v < NK; v++) F[v] = P[v];
-            } else {
-              store_block<OP>(vc, lane, s, P);
-            }
-#pragma unroll
-            for (int v = 0; v < NK; v++) P[v] = Ct[v];
-          }
-        } else if constexpr (JAC) {
-          store_block<OP>(vc, lane, s, P);
-#pragma unroll
-          for (int v = 0; v < NK; v++) P[v] = 0;
-        }
-      }
-    }
-  } else {
   double2 pn[NS];
   double un[NS][NF], a0[NS], a1[NS];
   auto gather = [&](int k) {
@@ -556,6 +502,12 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   };
 #pragma unroll
   for (int k = 1; k < SPLIT; k++) gather(k);
+
+  double R[NF], D[NK], P[NK], F[NK];
+#pragma unroll
+  for (int f = 0; f < NF; f++) R[f] = 0;
+#pragma unroll
+  for (int v = 0; v < NK; v++) D[v] = P[v] = F[v] = 0;
   // STAGE: blocks finished before the second-half gathers are issued (slots 1 .. SPLIT-3) wait
   // in LDS and go out right after those gathers: vmcnt retires loads and stores in issue order,
   // so a gather issued behind a store also waits for the store (A/B knob PNP_ASM_GA=6)
@@ -622,7 +574,6 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
       }
     }
   }
-  }  // gathered walk
   if constexpr (JAC) {
     if (closed) {
 #pragma unroll
@@ -780,13 +731,6 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
     const char *e = getenv("PNP_ASM_COLD_HINT");
     return !(e && e[0] == '0');
   }();
-  // the LDS walk with just-in-time neighbour reads at 4 waves per SIMD (LDSG = 2), when 4
-  // workgroups' records fit the CU's LDS (38 KiB each); PNP_ASM_JIT=0: the register-gathered LDS
-  // walk at 3 waves (A/B)
-  static const bool jit = [] {
-    const char *e = getenv("PNP_ASM_JIT");
-    return !(e && e[0] == '0');
-  }();
   const auto lds_walk = [&](int nk) {
     return lds_env == 1 ||
            (lds_env < 0 && (size_t(L.n_owned) * 7 * size_t(nk) * 8 > (size_t(512) << 20) ||
@@ -812,11 +756,6 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
-    else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uown && jit &&  \
-             size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 38 * 1024)                    \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, (OPK == OP_PNP_IE ? 3 : 4), 9, 9, 0, 2>), \
-                         grid, block,                                                    \
-                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
     else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uown &&       \
              size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
       hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \

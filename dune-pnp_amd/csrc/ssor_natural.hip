@@ -142,9 +142,9 @@ __device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p
 
 // PAD > 0: the workgroup reserves PAD bytes of LDS it never uses, so that at most one workgroup
 // runs per CU (the sparse tail grid, below).  KS: entries per lane and pass (KS * kL per row and
-// pass); rows longer than that take several passes, each a full load -> poll round trip.  The PNP
-// head runs with KS = 4 (32 entries): its phi rows have 3 (degree + 1) entries, 27 at degree 8,
-// which with 24 split every unit holding such a row into two passes.
+// pass); rows longer than that take several passes, each a full load -> poll round trip.  KS = 4
+// (32 entries) takes PNP's phi rows (3 (degree + 1) entries, 27 at degree 8) in one pass, but was
+// slower at config 3 (PNP_NAT_FLOW_KS4, off by default).
 template <int BLK, int SCOPE, int PAD = 0, int KS = kS>
 __global__ void __launch_bounds__(BLK)
     k_ssor_nat_flow(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
@@ -637,10 +637,11 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     const char *ev = std::getenv("PNP_NAT_PIPE");
     return !(ev && std::atoi(ev) == 0);
   }();
-  // PNP_NAT_FLOW_KS4=0: rows of 25-32 entries in two passes of 24 (A/B knob)
+  // PNP_NAT_FLOW_KS4=1: rows of 25-32 entries in one pass of 32 instead of two of 24 (A/B knob,
+  // off: PNP config 3 1.584 against 1.553 ms per application, profiles/r05/nat_ks4_r5h.log)
   static const bool ks4 = [] {
     const char *ev = std::getenv("PNP_NAT_FLOW_KS4");
-    return !(ev && std::atoi(ev) == 0);
+    return ev && std::atoi(ev) == 1;
   }();
   // PNP_NAT_SPEC=1: forward head units try plain loads first (A/B knob, default off)
   static const int spec = [] {

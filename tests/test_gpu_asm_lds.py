@@ -3,9 +3,7 @@ and frozen fields gathered once per workgroup into LDS) against the direct-gathe
 The walk is chosen once per process (PNP_ASM_LDS=1 / 0; unset: the LDS walk past the Infinity
 Cache, i.e. at config 5), so each variant runs in a child process.  Only where the neighbour
 values come from differs, so residuals, Jacobians and the BiCGSTAB trajectory on them must be
-bitwise the same, for every operator (NK = 5, 6, 1) on two meshes, residual-only and fused.
-The LDS walk exists twice: records read from LDS just in time per element at 4 waves per SIMD
-(the default) and gathered from LDS into registers up front at 3 (PNP_ASM_JIT=0)."""
+bitwise the same, for every operator (NK = 5, 6, 1) on two meshes, residual-only and fused."""
 import json
 import os
 import subprocess
@@ -45,8 +43,8 @@ print("RESULT " + json.dumps(out))
 """
 
 
-def run(lds, jit=1):
-    env = dict(os.environ, PNP_ASM_LDS=str(lds), PNP_ASM_JIT=str(jit))
+def run(lds):
+    env = dict(os.environ, PNP_ASM_LDS=str(lds))
     code = CHILD.replace("HERE", repr(HERE))
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300, cwd=HERE)
@@ -56,10 +54,7 @@ def run(lds, jit=1):
 
 
 def test_lds_assembly_bitwise_equals_direct_assembly():
-    """LDS walk with just-in-time record reads at 4 waves/SIMD (the default LDS walk, LDSG = 2),
-    the register-gathered LDS walk (PNP_ASM_JIT=0) and the direct-gather walk."""
-    a, c, b = run(1), run(1, jit=0), run(0)
-    assert a.keys() == b.keys() == c.keys() and len(a) == 7
+    a, b = run(1), run(0)
+    assert a.keys() == b.keys() and len(a) == 7
     for k in a:
         assert a[k] == b[k], k
-        assert c[k] == b[k], k
