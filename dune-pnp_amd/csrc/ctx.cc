@@ -200,11 +200,11 @@ struct pnp_ctx {
     std::vector<int> lptr;
     std::vector<long long> eoff;
     DBuf<int4> info;
-    DBuf<int> ecol, eidx;
+    DBuf<int> ecol;
     // the tail as chains (PNP_NAT_CHAIN): lane-group row lists, rows, padded entries
     bool chain_ok = false;
     int chain_groups = 0, chain_wpad = 0;
-    DBuf<int> cgptr, cecode, ceidx;
+    DBuf<int> cgptr, cecode;
     DBuf<int4> crec;
     pnp::NatFlow::Chains chains() const {
       pnp::NatFlow::Chains c;
@@ -214,7 +214,6 @@ struct pnp_ctx {
       c.gptr = cgptr.p;
       c.rec = crec.p;
       c.ecode = cecode.p;
-      c.eidx = ceidx.p;
       return c;
     }
     pnp::NatSweep view() const {
@@ -224,7 +223,6 @@ struct pnp_ctx {
       w.eoff = eoff.data();
       w.info = info.p;
       w.ecol = ecol.p;
-      w.eidx = eidx.p;
       return w;
     }
   };
@@ -912,17 +910,16 @@ struct pnp_ctx {
       // operand codes (NatSweep): the forward sweep reads the new value of an earlier row (C < R)
       // and zero for the row itself and later rows; the backward sweep reads the forward value of
       // rows C <= R and the new backward value of later rows; rows of other ranks read zero
-      std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), -1), eidx(ecol.size(), -1);
+      std::vector<int> ecol(std::max<long long>(1, W.eoff[nlev]), -1);
       for (int l = 0; l < nlev; l++) {
         for (int t = lptr[l]; t < lptr[l + 1]; t++) {
           const int R = rl[t], len = cnt[R + 1] - cnt[R], tl = t - lptr[l];
-          info[t] = make_int4(R, len, diag[R], P(R));
+          info[t] = make_int4(R, len | (diag[R] - cnt[R]) << 8, cnt[R], P(R));
           for (int k = 0; k < len; k++) {
             const size_t q =
                 size_t(W.eoff[l]) + (size_t(tl / UR) * lwidth[l] + k) * UR + size_t(tl % UR);
             const int C = col[cnt[R] + k];
             ecol[q] = empty(C) ? -1 : fwd ? (C < R ? C : -1) : (C <= R ? C : -(C + 2));
-            eidx[q] = cnt[R] + k;
           }
         }
       }
@@ -1018,14 +1015,14 @@ struct pnp_ctx {
             std::stable_sort(G.begin(), G.end(), [&](int a, int b) { return lev[a] < lev[b]; });
         const int wpad = wmax;
         if (wpad <= pnp::ssor_natural_chain_width()) {
-          std::vector<int> gptr(1, 0), ecode, eidx;
+          std::vector<int> gptr(1, 0), ecode;
           std::vector<int4> rec;
           for (const auto &G : grows) {
             const int H = pnp::ssor_natural_chain_history();
             for (size_t t = 0; t < G.size(); t++) {
               const int R = G[t];
               const int len = cnt[R + 1] - cnt[R];
-              rec.push_back(make_int4(R, len, diag[R], P(R)));
+              rec.push_back(make_int4(R, len | (diag[R] - cnt[R]) << 8, cnt[R], P(R)));
               for (int k = 0; k < wpad; k++) {
                 if (k < len) {
                   const int C = col[cnt[R] + k];
@@ -1039,10 +1036,8 @@ struct pnp_ctx {
                       break;
                     }
                   ecode.push_back(code);
-                  eidx.push_back(cnt[R] + k);
                 } else {
                   ecode.push_back(0);
-                  eidx.push_back(-1);
                 }
               }
             }
@@ -1051,8 +1046,7 @@ struct pnp_ctx {
           int rc2;
           if ((rc2 = upv(W.cgptr, gptr, "natural SSOR chains")) ||
               (rc2 = upv(W.crec, rec, "natural SSOR chains")) ||
-              (rc2 = upv(W.cecode, ecode, "natural SSOR chains")) ||
-              (rc2 = upv(W.ceidx, eidx, "natural SSOR chains")))
+              (rc2 = upv(W.cecode, ecode, "natural SSOR chains")))
             return rc2;
           W.chain_groups = int(grows.size());
           W.chain_wpad = wpad;
@@ -1083,10 +1077,8 @@ struct pnp_ctx {
       if (ltail >= nlev) (fwd ? nat_tail_f : nat_tail_b) = int(nat_units.size());
       if (fwd) nat_units_f = int(nat_units.size());
       int rc2;
-      if ((rc2 = upv(W.info, info, "natural SSOR rows")) ||
-          (rc2 = upv(W.ecol, ecol, "natural SSOR columns")))
-        return rc2;
-      return upv(W.eidx, eidx, "natural SSOR entries");
+      if ((rc2 = upv(W.info, info, "natural SSOR rows"))) return rc2;
+      return upv(W.ecol, ecol, "natural SSOR columns");
     };
     nat_units.clear();
     nat_units_ok = true;

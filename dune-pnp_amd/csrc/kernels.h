@@ -441,18 +441,18 @@ hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *va
 // ISTL SeqSSOR (k = 1, omega = 1) in the lexicographic DOF order (ssor_natural.hip): v = 0, then
 // the forward levels and the backward levels, one launch per level.  Per sweep direction
 // (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row
-// (external index), entry count, index of the diagonal in val, the row's internal position}; the
-// row's entries in CSR (ascending column) order as an ELL of the level stored unit-major: with
-// tl = t - lptr[l], entry k at eoff[l] + (tl / U * w_l + k) * U + tl % U (U =
-// ssor_natural_unit_rows(), w_l the level's width; eoff: host array): its column (ecol) and its
-// index into the external-layout CSR values val (eidx).  The level launches: d / v
-// external-layout vectors.
+// (external index), entry count | the diagonal's offset in the row << 8, index of the row's first
+// entry in the external-layout CSR values val (its entries are contiguous there), the row's
+// internal position}; the operand codes of the row's entries (ecol, CSR order) as an ELL of the
+// level stored unit-major: with tl = t - lptr[l], entry k at eoff[l] + (tl / U * w_l + k) * U +
+// tl % U (U = ssor_natural_unit_rows(), w_l the level's width; eoff: host array).  The level
+// launches: d / v external-layout vectors.
 struct NatSweep {
   int nlev = 0;
   const int *lptr = nullptr;
   const long long *eoff = nullptr;
   const int4 *info = nullptr;
-  const int *ecol = nullptr, *eidx = nullptr;
+  const int *ecol = nullptr;
 };
 hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const double *val,
                                const double *d, double *v, hipStream_t s);
@@ -479,13 +479,12 @@ struct NatFlow {
   int tail_f = 0, tail_b = 0;
   int max_width = 0;  // the longest row of any unit (the pipelined head takes up to 24 entries)
   // the tails as chains (ssor_natural.hip k_ssor_nat_chain), when ngroups > 0: the wave of group g
-  // walks rows gptr[g] .. gptr[g+1] of rec ({external row, entry count, diagonal value index,
-  // internal position}); row
-  // q's entries at q * wpad .. + count of ecode (idx << 2 | kind: 0 zero, 1 vf[idx], 2 vb[idx],
-  // 3 the group's result idx rows back) and eidx (value indices, -1 padding)
+  // walks rows gptr[g] .. gptr[g+1] of rec (as NatSweep::info); row q's entries at q * wpad ..
+  // + count of ecode (idx << 2 | kind: 0 zero, 1 vf[idx], 2 vb[idx], 3 the group's result idx
+  // rows back)
   struct Chains {
     int ngroups = 0, wpad = 0;
-    const int *gptr = nullptr, *ecode = nullptr, *eidx = nullptr;
+    const int *gptr = nullptr, *ecode = nullptr;
     const int4 *rec = nullptr;
   } chain_f, chain_b;
   NatSweep fwd, bwd;

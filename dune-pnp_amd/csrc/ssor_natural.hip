@@ -55,13 +55,14 @@ constexpr int kL = NAT_KL, kS = (24 + kL - 1) / kL, kC = kS * kL;  // PNP rows: 
 constexpr int kUR = 64 / kL;  // rows per dataflow unit (one wavefront): the ELL's group size
 __global__ void __launch_bounds__(kB)
     k_ssor_nat_level(const int4 *__restrict__ info, const int *__restrict__ ecol,
-                     const int *__restrict__ eidx, int n, int width,
+                     int n, int width,
                      const double *__restrict__ val, const double *__restrict__ d,
                      double *__restrict__ v) {
   const int g = blockIdx.x * kB + threadIdx.x, t = g / kL, j = g % kL;
   const bool live = t < n;  // whole rows per wavefront: kL divides 64
   const bool head = live && j == 0;
-  const int4 I = head ? info[t] : make_int4(0, 0, 0, 0);
+  const int4 I = live ? info[t] : make_int4(0, 0, 0, 0);  // every lane: the row's first entry
+  const int len = I.y & 255;
   const int base = (threadIdx.x % 64) - j;  // the row's first lane in the wavefront
   double rhs = 0.0;
   for (int kb = 0; kb < width; kb += kC) {  // uniform: width = the level's longest row
@@ -72,7 +73,7 @@ __global__ void __launch_bounds__(kB)
       const bool in = live && k < width;
       const size_t at = (size_t(t / kUR) * width + k) * kUR + size_t(t % kUR);  // unit-major ELL
       c[u] = in ? ecol[at] : -1;
-      ix[u] = in ? eidx[at] : -1;
+      ix[u] = (in && k < len) ? I.z + k : -1;  // the row's entries are contiguous in val
     }
     if (kb == 0 && head) rhs = d[I.x];
     double pr[kS];
@@ -89,7 +90,7 @@ __global__ void __launch_bounds__(kB)
       if (head && kb + k < width) rhs -= p;
     }
   }
-  if (head) v[I.x] += 1.0 * (rhs / val[I.z]);
+  if (head) v[I.x] += 1.0 * (rhs / val[I.z + (I.y >> 8)]);
 }
 
 // ---- one launch for both sweeps: a dataflow over the level-ordered units ------------------------
@@ -149,8 +150,7 @@ template <int BLK, int SCOPE, int PAD = 0, int KS = kS>
 __global__ void __launch_bounds__(BLK)
     k_ssor_nat_flow(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
                     const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
-                    const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
-                    const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
+                    const int4 *__restrict__ info_b, const int *__restrict__ ecol_b,
                     const double *__restrict__ val, const double *__restrict__ d,
                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word,
                     int spec = 0) {
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(BLK)
     const bool bwd = u >= nunits_f;  // uniform
     const int rows = U.y & 255, width = (U.y >> 8) & 255;
     const int4 *info = bwd ? info_b : info_f;
-    const int *ecol = bwd ? ecol_b : ecol_f, *eidx = bwd ? eidx_b : eidx_f;
+    const int *ecol = bwd ? ecol_b : ecol_f;
     const bool live = t < rows;
     const bool head = live && j == 0;
     const int4 I = live ? info[U.x + t] : make_int4(0, 0, 0, 0);
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(BLK)
         const bool in = live && k < width;
         const size_t at = size_t(U.w) + size_t(k) * U.z + t;
         c[q] = in ? ecol[at] : -1;
-        ix[q] = in ? eidx[at] : -1;
+        ix[q] = (in && k < (I.y & 255)) ? I.z + k : -1;  // the row's entries: contiguous in val
       }
       if (kb == 0 && head) rhs = d[I.w];  // d: internal layout
       unsigned long long b[KS];
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(BLK)
       // the row's own forward value is final: its diagonal entry's operand was waited for above
       double own = 0.0;
       if (bwd) own = __longlong_as_double(vf[I.x]);  // final since the forward launches
-      const double out = own + 1.0 * (rhs / val[I.z]);
+      const double out = own + 1.0 * (rhs / val[I.z + (I.y >> 8)]);
       __hip_atomic_store(bwd ? vb + I.x : vf + I.x,
                          (unsigned long long)__double_as_longlong(out), __ATOMIC_RELAXED, SCOPE);
     }
@@ -290,8 +290,7 @@ template <int BLK>
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
     k_ssor_nat_pipe(const int4 *__restrict__ units, int u0, int u1, int nunits_f,
                     const int4 *__restrict__ info_f, const int *__restrict__ ecol_f,
-                    const int *__restrict__ eidx_f, const int4 *__restrict__ info_b,
-                    const int *__restrict__ ecol_b, const int *__restrict__ eidx_b,
+                    const int4 *__restrict__ info_b, const int *__restrict__ ecol_b,
                     const double *__restrict__ val, const double *__restrict__ d,
                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
   const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
@@ -307,7 +306,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
   // two register sets per stage, used alternately (the loop below is unrolled by two), so that no
   // stage register is copied while its load is in flight
   int4 aU[2], aI[2];
-  int ac[2][kS], ax[2][kS];
+  int ac[2][kS];
   int bc[2][kS], bx[2][kS], brow[2], bw8[2], bwid[2];
   double ba[2][kS], bd[2], bg[2];
   unsigned long long bb[2][kS], bo[2];
@@ -319,13 +318,12 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
     const int rows = aU[S].y & 255, width = (aU[S].y >> 8) & 255;
     const int tt = t < rows ? t : rows - 1;
     aI[S] = (bw ? info_b : info_f)[aU[S].x + tt];
-    const int *ec = bw ? ecol_b : ecol_f, *ei = bw ? eidx_b : eidx_f;
+    const int *ec = bw ? ecol_b : ecol_f;
 #pragma unroll
     for (int q = 0; q < kS; q++) {
       const int k = j + q * kL, kk = k < width ? k : width - 1;
       const size_t at = size_t(aU[S].w) + size_t(kk) * aU[S].z + tt;
       ac[S][q] = ec[at];
-      ax[S][q] = ei[at];
     }
   };
   // stage B: what the compute needs, from stage A's registers of the same set
@@ -339,17 +337,18 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
     for (int q = 0; q < kS; q++) {
       const bool in = live && j + q * kL < width;
       bc[S][q] = in ? ac[S][q] : -1;
-      bx[S][q] = in ? ax[S][q] : -1;
+      // the row's entries are contiguous in val from aI.z
+      bx[S][q] = (in && j + q * kL < (aI[S].y & 255)) ? aI[S].z + j + q * kL : -1;
       // materialised here: the compiler would otherwise sink the selects below the next stage A
       // load into ac / ax, keep both generations live and copy them at the loop latch, waiting
       // for those loads
       asm volatile("" : "+v"(bc[S][q]), "+v"(bx[S][q]));
-      ba[S][q] = val[ax[S][q] >= 0 ? ax[S][q] : 0];
+      ba[S][q] = val[bx[S][q] >= 0 ? bx[S][q] : 0];
       bb[S][q] = ld(ac[S][q] == -1 ? vf : opnd(ac[S][q]));
     }
     asm volatile("" : "+v"(brow[S]), "+v"(bw8[S]));
     bd[S] = d[aI[S].w];  // d: internal layout
-    bg[S] = val[aI[S].z];
+    bg[S] = val[aI[S].z + (aI[S].y >> 8)];
     bo[S] = ld(vf + aI[S].x);  // the row's forward value (backward units)
   };
   // Each row of the unit is stored as soon as ITS operands are final (ballot over its kL lanes),
@@ -493,7 +492,7 @@ constexpr int kChainD = NAT_CHAIN_D, kChainA = 2 * kChainD, kChainH = NAT_CHAIN_
 
 __global__ void __launch_bounds__(64)
     k_ssor_nat_chain(const int *__restrict__ gptr, const int4 *__restrict__ rec,
-                     const int *__restrict__ ecode, const int *__restrict__ eidx, int wpad,
+                     const int *__restrict__ ecode, int wpad,
                      const double *__restrict__ val, const double *__restrict__ d,
                      unsigned long long *vf, unsigned long long *vb, int bwd,
                      unsigned *abort_word) {
@@ -510,21 +509,21 @@ __global__ void __launch_bounds__(64)
     return k == 1 ? vf + i : k == 2 ? vb + i : vf;
   };
   int4 ra[A];
-  int ca[A], xa[A];
+  int ca[A];
   double av[D], dv[D], ov[D], gv[D];
   unsigned long long bv[D];
   auto stage_a = [&](int s, int slot) {
     const int p = p0 + (s < len ? s : len - 1);
     ra[slot] = rec[p];
     ca[slot] = ecode[size_t(p) * wpad + kl];
-    xa[slot] = eidx[size_t(p) * wpad + kl];
   };
   auto stage_b = [&](int sa, int sb) {
-    av[sb] = val[xa[sa] >= 0 ? xa[sa] : 0];
+    // lane k's entry: the row's entries are contiguous in val from rec.z
+    av[sb] = val[lane < (ra[sa].y & 255) ? ra[sa].z + lane : 0];
     bv[sb] = ld(opnd(ca[sa]));
     dv[sb] = d[ra[sa].w];  // d: internal layout
     ov[sb] = __longlong_as_double(ld(vf + ra[sa].x));  // the forward value (backward sweep)
-    gv[sb] = val[ra[sa].z];
+    gv[sb] = val[ra[sa].z + (ra[sa].y >> 8)];
   };
 #pragma unroll
   for (int i = 0; i < A; i++) stage_a(i, i);
@@ -538,7 +537,7 @@ __global__ void __launch_bounds__(64)
     for (int i = 0; i < A; i++) {
       const int st = s + i;
       if (st < len) {  // uniform
-        const int c = ca[i], kind = c & 3, width = ra[i].y;
+        const int c = ca[i], kind = c & 3, width = ra[i].y & 255;
         const bool live = lane < width;
         unsigned long long b = bv[i % D];
         bool pend = live && (kind == 1 || kind == 2) && b == kNatPending;
@@ -567,7 +566,7 @@ __global__ void __launch_bounds__(64)
         for (int q = 1; q < kChainH; q++)
           if (hi == q + 1) hv = h[q];
         const double o = kind == 0 ? 0.0 : kind == 3 ? hv : __longlong_as_double(b);
-        const double pr = (live && xa[i] >= 0) ? av[i % D] * o : 0.0;
+        const double pr = live ? av[i % D] * o : 0.0;  // lane < the row's entry count
         const unsigned long long pb = __double_as_longlong(pr);
         const int plo = int(unsigned(pb)), phi = int(unsigned(pb >> 32));
         double rhs = dv[i % D];
@@ -667,29 +666,27 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
       const int blocks = std::min(grid, (ut - u0 + kB / 64 - 1) / (kB / 64));
       if (F.max_width <= kC && pipe)
         hipLaunchKernelGGL(k_ssor_nat_pipe<kB>, dim3(blocks), dim3(kB), 0, s, F.units, u0, ut,
-                           F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx, F.bwd.info, F.bwd.ecol,
-                           F.bwd.eidx, val, d, vfu, vbu, F.abort_word);
+                           F.nunits_f, F.fwd.info, F.fwd.ecol, F.bwd.info, F.bwd.ecol, val, d,
+                           vfu, vbu, F.abort_word);
       else if (F.max_width <= 4 * kL && ks4)
         hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT, 0, 4>), dim3(blocks),
                            dim3(kB), 0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol,
-                           F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
-                           F.abort_word, spec);
+                           F.bwd.info, F.bwd.ecol, val, d, vfu, vbu, F.abort_word, spec);
       else
         hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(blocks), dim3(kB),
-                           0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol, F.fwd.eidx,
-                           F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
-                           F.abort_word, spec);
+                           0, s, F.units, u0, ut, F.nunits_f, F.fwd.info, F.fwd.ecol,
+                           F.bwd.info, F.bwd.ecol, val, d, vfu, vbu, F.abort_word, spec);
     }
     if (u1 > ut && C.ngroups > 0)
       hipLaunchKernelGGL(k_ssor_nat_chain, dim3(C.ngroups), dim3(64), 0, s, C.gptr, C.rec, C.ecode,
-                         C.eidx, C.wpad, val, d, vfu, vbu, bwd, F.abort_word);
+                         C.wpad, val, d, vfu, vbu, bwd, F.abort_word);
     else if (u1 > ut && tail_wpc > 0) {
       const int per = tail_wpc >= 4 ? 4 : tail_wpc >= 2 ? 2 : 1;
       const int blocks = std::min(cus, (u1 - ut + per - 1) / per);
 #define NAT_TAIL_GRID(W)                                                                          \
   hipLaunchKernelGGL((k_ssor_nat_flow<64 * W, __HIP_MEMORY_SCOPE_AGENT, kTailPad>), dim3(blocks), \
                      dim3(64 * W), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,     \
-                     F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,           \
+                     F.bwd.info, F.bwd.ecol, val, d, vfu, vbu,                                   \
                      F.abort_word)
       if (per == 1) NAT_TAIL_GRID(1);
       else if (per == 2) NAT_TAIL_GRID(2);
@@ -698,7 +695,7 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     } else if (u1 > ut)
       hipLaunchKernelGGL((k_ssor_nat_flow<kTailBlk, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3(1),
                          dim3(kTailBlk), 0, s, F.units, ut, u1, F.nunits_f, F.fwd.info, F.fwd.ecol,
-                         F.fwd.eidx, F.bwd.info, F.bwd.ecol, F.bwd.eidx, val, d, vfu, vbu,
+                         F.bwd.info, F.bwd.ecol, val, d, vfu, vbu,
                          F.abort_word);
   };
   sweep(0, F.tail_f, F.nunits_f, F.chain_f, 0);
@@ -714,7 +711,7 @@ hipError_t launch_ssor_natural(const NatSweep &fwd, const NatSweep &bwd, const d
       const int nu = (n + kUR - 1) / kUR;  // the level's unit-major ELL (NatSweep)
       const int width = n > 0 ? int((W->eoff[l + 1] - W->eoff[l]) / ((long long)nu * kUR)) : 0;
       hipLaunchKernelGGL(k_ssor_nat_level, dim3((n * kL + kB - 1) / kB), dim3(kB), 0, s,
-                         W->info + W->lptr[l], W->ecol + W->eoff[l], W->eidx + W->eoff[l], n,
+                         W->info + W->lptr[l], W->ecol + W->eoff[l], n,
                          width, val, d, v);
     }
   return hipGetLastError();
