@@ -522,13 +522,15 @@ def rccl_parity(sctx, smesh, scfg, x0, rank, world, local, dist):
     return out
 
 
-def ssork_natural_leg(ctx, mesh, x0, nit):
+def ssork_natural_leg(ctx, mesh, x0, nit, dist=None, world=1):
     """The reference's default linear solver, BCGS_SSORk (BiCGSTAB + ISTL SeqSSOR in the
-    reference's DOF order, PNP_PREC_SSOR_NATURAL: bitwise the oracle's SeqSSOR), on the config-3
-    PNP system at x0 and on the PB system at its potential: one preconditioner application (device
-    timers: forward + backward sweep, scatter and gather) and one BiCGSTAB iteration (two
-    applications, two SpMVs, the reductions), after two untimed iterations (N=1 only: the one-launch
-    dataflow schedule needs the whole device)."""
+    reference's DOF order, PNP_PREC_SSOR_NATURAL: bitwise the oracle's SeqSSOR on one rank; each
+    rank sweeps its owned rows at N > 1, the NOVLP backend's block SeqSSOR), on the PNP system at x0
+    and on the PB system at its potential: one preconditioner application (device timers) and one
+    BiCGSTAB iteration (two applications, two SpMVs, the reductions), after two untimed
+    iterations.  Every rank that owns its GPU runs the one-launch dataflow schedule (its rank's
+    `schedule` field counts the applications per schedule); at N > 1 the per-rank ms per
+    application and the slowest rank's iteration time."""
     out = {}
     nv = mesh.nv
     for name, op, x in (("pnp", P.OP_PNP, x0), ("pb", P.OP_PB, x0[:nv])):
@@ -536,14 +538,28 @@ def ssork_natural_leg(ctx, mesh, x0, nit):
         ctx.state_set(x)
         ctx.assemble_state(1)
         ctx.bicgstab_iterations(2, P.PREC_SSOR_NATURAL)
+        barrier_sync(dist, world)
         t0 = time.perf_counter()
         ctx.bicgstab_iterations(nit, P.PREC_SSOR_NATURAL)
-        wall = (time.perf_counter() - t0) / nit
+        barrier_sync(dist, world)
+        wall = max_over_ranks(dist, world, (time.perf_counter() - t0) / nit)
+        info0 = ctx.info()
         ctx.timers(enable=True, reset=True)
         ctx.bicgstab_iterations(nit, P.PREC_SSOR_NATURAL)
         tm = ctx.timers(enable=False)
         ctx.timers(reset=True)
-        out[name] = {"dofs": int(len(x)), "ms_per_apply": tm["prec_ms"] / max(1, tm["prec_launches"]),
+        info1 = ctx.info()
+        mine = {"ms_per_apply": tm["prec_ms"] / max(1, tm["prec_launches"]),
+                "dataflow_applies": info1["nat_flow_applies"] - info0["nat_flow_applies"],
+                "level_applies": info1["nat_level_applies"] - info0["nat_level_applies"]}
+        if world > 1:
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+        else:
+            allr = [mine]
+        out[name] = {"dofs": int(len(x)), "ms_per_apply": max(a["ms_per_apply"] for a in allr),
+                     "ms_per_apply_per_rank": [a["ms_per_apply"] for a in allr],
+                     "dataflow_applies_per_rank": [a["dataflow_applies"] for a in allr],
                      "ms_per_iter": 1e3 * wall, "iters_per_s": 1.0 / wall}
     ctx.set_operator(P.OP_PNP)
     out["schedule"] = ("forward and backward sweep each: the wide levels as dataflow units, the "
@@ -799,8 +815,8 @@ def main():
                                         "on the coarse levels)",
                       "amg_rows": ctx.amg_info()["rows"]}
     ssork = None
-    if world == 1 and not args.no_ssork:
-        ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters)
+    if not args.no_ssork:
+        ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters, dist, world)
     ctx.close()
     per_config = None
     if world == 1 and not args.no_per_config:

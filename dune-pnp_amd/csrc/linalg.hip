@@ -1585,22 +1585,38 @@ __device__ void derive(Scalars *S, int stage);
 // One workgroup of kRedBlock threads; each thread issues its (up to kRedU) partial loads back to
 // back before adding, so the ~3K partials of a config-3 SpMV cost one memory round trip instead
 // of the ~11 dependent ones of a 256-thread strided loop (13.8 -> see DESIGN.md, reductions).
-constexpr int kRedBlock = 1024, kRedU = 4;
-
+// 12 partials per thread and pass (6 for 4-5 values per partial): the ~8,600 partials of a
+// config-3 SpMV are one pass (4 took three dependent passes); a thread still adds its partials in
+// index order (tid, tid + 1024, ...), so every sum is bitwise the 4-per-pass one's.
+constexpr int kRedBlock = 1024;
 template <int K>
-__device__ __forceinline__ void accum_partials(const double *__restrict__ p, int np, double *acc) {
+constexpr int red_unroll() { return K <= 3 ? 12 : 6; }  // <= 128 VGPRs at 1024 threads
+
+// the partials of two arrays (KB = 0: one) in the same passes, so the second array's loads are
+// in flight with the first's; acc[0 .. KA) sums pa, acc[KA ..) sums pb, each in index order
+template <int KA, int KB>
+__device__ __forceinline__ void accum_partials(const double *__restrict__ pa, int npa,
+                                               const double *__restrict__ pb, int npb,
+                                               double *acc) {
+  constexpr int kRedU = red_unroll<KA + KB>();
+  const int np = npa > npb ? npa : npb;
   for (int i0 = threadIdx.x; i0 < np; i0 += kRedU * kRedBlock) {
-    double v[kRedU][K];
+    double va[kRedU][KA], vb[kRedU][KB > 0 ? KB : 1];
 #pragma unroll
     for (int u = 0; u < kRedU; u++) {
       const int i = i0 + u * kRedBlock;
 #pragma unroll
-      for (int j = 0; j < K; j++) v[u][j] = i < np ? p[size_t(i) * K + j] : 0.0;
+      for (int j = 0; j < KA; j++) va[u][j] = i < npa ? pa[size_t(i) * KA + j] : 0.0;
+#pragma unroll
+      for (int j = 0; j < KB; j++) vb[u][j] = i < npb ? pb[size_t(i) * KB + j] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < kRedU; u++)
+    for (int u = 0; u < kRedU; u++) {
 #pragma unroll
-      for (int j = 0; j < K; j++) acc[j] += v[u][j];
+      for (int j = 0; j < KA; j++) acc[j] += va[u][j];
+#pragma unroll
+      for (int j = 0; j < KB; j++) acc[KA + j] += vb[u][j];
+    }
   }
 }
 
@@ -1616,8 +1632,7 @@ __global__ __launch_bounds__(kRedBlock) void k_reduce(const double *__restrict__
   double acc[KA + KB];
 #pragma unroll
   for (int j = 0; j < KA + KB; j++) acc[j] = 0;
-  accum_partials<KA>(pa, npa, acc);
-  if constexpr (KB > 0) accum_partials<KB>(pb, npb, acc + KA);
+  accum_partials<KA, KB>(pa, npa, pb, npb, acc);
   double out[KA + KB];
   block_sum<KA + KB, kRedBlock>(acc, out);
   if (threadIdx.x == 0) {

@@ -136,10 +136,14 @@ def test_pnp_newton_ssor_natural_converges_like_the_oracle():
     assert res["iterations"] == ro.iterations
 
 
-def test_ssor_natural_on_two_ranks_is_block_jacobi():
+@pytest.mark.parametrize("flow", [0, 1])
+def test_ssor_natural_on_two_ranks_is_block_jacobi(flow):
     """Two in-process ranks: each rank sweeps its owned rows in the lexicographic order, columns of
     the other rank's DOFs read zero -- the block-Jacobi SeqSSOR of the reference's NOVLP backend.
-    Checked against the oracle's SeqSSOR on the matrix with the cross-rank couplings removed."""
+    Checked against the oracle's SeqSSOR on the matrix with the cross-rank couplings removed.
+    flow = 0: the level launches (the local group's default); flow = 1: the one-launch dataflow
+    schedule that RCCL ranks run (PNP_OPT_NAT_FLOW = 1; the two ranks' applications serialised,
+    since the dataflow needs the whole device), on each rank's partitioned schedule."""
     import threading
     z, mesh, par, orc = golden("pore_small_k0")
     x = z["newton_pnp_x0"]
@@ -151,11 +155,17 @@ def test_ssor_natural_on_two_ranks_is_block_jacobi():
         lay = P.Layout(mesh, r, 2)
         owner[lay.l2g[:lay.n_owned]] = r
 
+    lock = threading.Lock()
+
     def run(rank):
-        ctx = P.Context(mesh, par, rank=rank, size=2, local_group="ssor_nat2")
+        ctx = P.Context(mesh, par, rank=rank, size=2, local_group="ssor_nat2_%d" % flow)
+        ctx.set_option(P.OPT_NAT_FLOW, flow if flow else -1)
         ctx.set_operator(P.OP_PNP)
         ctx.jacobian(x, export=False)
-        out[rank] = ctx.prec_apply(d, P.PREC_SSOR_NATURAL)
+        with lock:
+            out[rank] = ctx.prec_apply(d, P.PREC_SSOR_NATURAL)
+        info = ctx.info()
+        assert (info["nat_flow_applies"] > 0) == bool(flow), info
         ctx.close()
 
     th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
