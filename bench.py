@@ -74,7 +74,7 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-ASM_REGIMES = os.path.join(ROOT, "profiles", "r04", "final", "asm_regimes_config3_final.json")
+ASM_REGIMES = os.path.join(ROOT, "profiles", "r05", "final", "asm_regimes_config3.json")
 BICG_SPLIT = os.path.join(ROOT, "profiles", "r05", "bicg_split_final.json")
 
 
@@ -343,14 +343,26 @@ def byte_models(info, nf, N_local, T_local, prec):
             "it_stored": 2 * spmv + (2 * ilu if pre else 0) + blas}
 
 
-def make_context(mesh, cfg, rank, world, local, dist):
+TRANSPORT = "rccl"  # --transport: rccl (one GPU per rank) or host (pnp_comm.host over gloo)
+
+
+def new_context(mesh, par, rank, world, local, dist):
+    """This rank's context: RCCL at N > 1 (the unique id broadcast from rank 0), or with
+    --transport host the host-staged transport over the gloo group (ranks may share a GPU:
+    rehearses the N > 1 bench on a one-GPU box)."""
+    if world > 1 and TRANSPORT == "host":
+        return P.Context(mesh, par, device=local, rank=rank, size=world,
+                         host_transport=P.TorchDistTransport(dist))
     uid = None
     if world > 1:
         obj = [P.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
-    ctx = P.Context(mesh, P.Params.from_config(cfg), device=local, rank=rank, size=world,
-                    unique_id=uid)
+    return P.Context(mesh, par, device=local, rank=rank, size=world, unique_id=uid)
+
+
+def make_context(mesh, cfg, rank, world, local, dist):
+    ctx = new_context(mesh, P.Params.from_config(cfg), rank, world, local, dist)
     # Boltzmann initial state: PB Newton, then the BCExtension interpolation
     t_setup = time.perf_counter()
     ctx.set_operator(P.OP_PB)
@@ -503,7 +515,7 @@ def rccl_parity(sctx, smesh, scfg, x0, rank, world, local, dist):
         er = float(np.max(np.abs(r_d - r1)) / np.max(np.abs(r1)))
         eu = float(np.max(np.abs(u_d - u1)) / np.max(np.abs(u1)))
         out = {"system": f"config 5 ({3 * smesh.nv} DOFs), x0 = Boltzmann initial state",
-               "ranks": world, "transport": ["plain", "local", "rccl"][allr[0]["transport"]],
+               "ranks": world, "transport": ["plain", "local", "rccl", "host"][allr[0]["transport"]],
                "rccl_ranks_seen": allr[0]["nranks"],
                "residual_rel_err": er, "solution_rel_err": eu,
                "newton_converged": [res_d["converged"], res1["converged"]],
@@ -733,18 +745,25 @@ def main():
                     help="refinement of the CPU sample (4: the config-3 mesh itself)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cfg", default=os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="N > 1: RCCL (default, one GPU per rank) or the host-staged transport over "
+                         "gloo (pnp_comm.host; ranks may share a GPU: a one-box rehearsal)")
     ap.add_argument("--newton-reduction", type=float, default=None,
                     help="time-to-solution leg: Newton reduction (default: the config's)")
     ap.add_argument("--min-linear-reduction", type=float, default=None,
                     help="time-to-solution leg: min linear reduction (default: the config's)")
     args = ap.parse_args()
 
+    global TRANSPORT
+    TRANSPORT = args.transport
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(1)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # torch only times the copy-rate calibration and syncs around the timed regions: bind it to
-    # this rank's GPU (its default is device 0, whatever LOCAL_RANK the library runs on)
+    # torch only syncs around the timed regions: bind it to this rank's GPU (its default is device
+    # 0, whatever LOCAL_RANK the library runs on); the host transport may put several ranks on one
     import torch
+    if args.transport == "host":
+        local = local % max(1, torch.cuda.device_count())
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     dist = None

@@ -98,6 +98,37 @@ class _Comm(C.Structure):
                 ("local_group", C.c_char_p), ("host", C.POINTER(_HostTransport))]
 
 
+class TorchDistTransport:
+    """A host transport (pnp_comm.host) over an initialised torch.distributed process group (gloo):
+    point-to-point halo exchange, all_reduce sums.  For ranks that cannot use RCCL -- several
+    processes on one GPU (tests/test_gpu_dist_host.py, `bench.py --transport host`)."""
+
+    def __init__(self, dist=None):
+        import torch
+        if dist is None:
+            import torch.distributed as dist
+        self.dist, self.torch = dist, torch
+        self.calls = {"exchange": 0, "allreduce": 0}
+
+    def exchange(self, peers, sends, rcounts):
+        self.calls["exchange"] += 1
+        reqs, outs = [], []
+        for q, peer in enumerate(peers):
+            buf = self.torch.empty(int(rcounts[q]), dtype=self.torch.float64)
+            outs.append(buf)
+            if len(sends[q]):
+                reqs.append(self.dist.isend(self.torch.from_numpy(sends[q]), peer))
+            if rcounts[q]:
+                reqs.append(self.dist.irecv(buf, peer))
+        for r in reqs:
+            r.wait()
+        return [o.numpy() for o in outs]
+
+    def allreduce_sum(self, buf):
+        self.calls["allreduce"] += 1
+        self.dist.all_reduce(self.torch.from_numpy(buf))  # shares the staging memory
+
+
 def _host_transport(obj):
     """pnp_host_transport over a Python object with
          exchange(nbr, sends, recv_counts) -> list of received arrays  (sends: list of arrays)

@@ -19,33 +19,6 @@ sys.path.insert(0, os.path.join(ROOT, "dune-pnp_amd", "python"))
 import pnp_amd as P  # noqa: E402
 
 
-class GlooTransport:
-    """pnp_host_transport over torch.distributed (gloo): point-to-point halo, all_reduce sums."""
-
-    def __init__(self, dist, torch):
-        self.dist, self.torch = dist, torch
-        self.calls = {"exchange": 0, "allreduce": 0}
-
-    def exchange(self, peers, sends, rcounts):
-        self.calls["exchange"] += 1
-        reqs, outs = [], []
-        for q, peer in enumerate(peers):
-            buf = self.torch.empty(int(rcounts[q]), dtype=self.torch.float64)
-            outs.append(buf)
-            if len(sends[q]):
-                reqs.append(self.dist.isend(self.torch.from_numpy(sends[q]), peer))
-            if rcounts[q]:
-                reqs.append(self.dist.irecv(buf, peer))
-        for r in reqs:
-            r.wait()
-        return [o.numpy() for o in outs]
-
-    def allreduce_sum(self, buf):
-        self.calls["allreduce"] += 1
-        t = self.torch.from_numpy(buf)  # shares the staging memory
-        self.dist.all_reduce(t)
-
-
 def driver(ctx, mesh, cfg):
     s = cfg.system
     ctx.set_operator(P.OP_PB)
@@ -66,14 +39,13 @@ def driver(ctx, mesh, cfg):
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     refine = int(sys.argv[5]) if len(sys.argv) > 5 else 2
-    import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     cfg = P.read_config(os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
     mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(refine)
     par = P.Params.from_config(cfg)
-    tr = GlooTransport(dist, torch)
+    tr = P.TorchDistTransport(dist)
     t0 = time.perf_counter()
     ctx = P.Context(mesh, par, device=0, rank=rank, size=world, host_transport=tr)
     info = ctx.info()
