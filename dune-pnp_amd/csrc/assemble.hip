@@ -160,9 +160,13 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
       if (a.cylindrical) f *= (P[q][0] * yi + P[q][1] * yb + P[q][2] * yc) * 2 * PI;
       double u = P[q][0] * ui[0] + P[q][1] * ub[0] + P[q][2] * uc[0];
       W += f;
-      Ri += f * sinh(u) * P[q][0];
+      // sinh and cosh from one exp and one reciprocal (the library's sinh and cosh each cost about
+      // two exps, and the PB launch is issue-bound on them); the sinh term's error is absolute,
+      // ~eps * e^|u|, against residual terms of at least that size
+      const double e = exp(u), ei = 1.0 / e;
+      Ri += f * (0.5 * (e - ei)) * P[q][0];
       if constexpr (JAC) {
-        double ch = f * cosh(u) * P[q][0];
+        double ch = f * (0.5 * (e + ei)) * P[q][0];
         Jii += ch * P[q][0];
         Jib += ch * P[q][1];
         Jic += ch * P[q][2];

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <queue>
+#include <random>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -4305,6 +4306,75 @@ extern "C" int pnp_bicgstab_iterations(pnp_ctx *c, int32_t n, int32_t prec, pnp_
   int rc = c->bicgstab(c->b.p, c->z.p, o, *res, n);
   c->amg_symmetric = true;
   return rc;
+}
+
+extern "C" int pnp_probe_slot_stores(pnp_ctx *c, int32_t tile_elems, int32_t reps,
+                                     pnp_store_probe *out) {
+  if (!c || !out || tile_elems <= 0 || reps <= 0) return PNP_E_ARG;
+  if (c->degree < 2) return c->fail(PNP_E_ARG, "pnp_probe_slot_stores: P_k contexts only");
+  hipSetDevice(c->device);
+  std::memset(out, 0, sizeof *out);
+  const int nl = c->pks.nl, no = c->L.n_owned;
+  // pk_build's local elements: ascending global id, every element with an owned node
+  std::vector<int> first(no, -1), last(no, -1);
+  int ne = 0;
+  for (int e = 0; e < c->tmesh.nt; e++) {
+    const int *g = &c->pks.enode[size_t(e) * nl];
+    bool mine = false;
+    for (int a = 0; a < nl; a++) {
+      const int l = c->L.g2l[g[a]];
+      mine = mine || (l >= 0 && l < no);
+    }
+    if (!mine) continue;
+    for (int a = 0; a < nl; a++) {
+      const int l = c->L.g2l[g[a]];
+      if (l < 0 || l >= no) continue;
+      if (first[l] < 0) first[l] = ne;
+      last[l] = ne;
+    }
+    ne++;
+  }
+  std::vector<int> tile(no), tsort(no), rnd(no);
+  long long slots = 0;
+  for (int r = 0; r < no; r++) {
+    tile[r] = tsort[r] = rnd[r] = r;
+    slots += pnp::meta_len(c->L.rowmeta[r]);
+    out->rows_whole += first[r] / tile_elems == last[r] / tile_elems;
+  }
+  std::stable_sort(tile.begin(), tile.end(), [&](int a, int b) { return first[a] < first[b]; });
+  std::stable_sort(tsort.begin(), tsort.end(),
+                   [&](int a, int b) { return first[a] / tile_elems < first[b] / tile_elems; });
+  std::mt19937 rng(20261018);
+  std::shuffle(rnd.begin(), rnd.end(), rng);
+  const std::vector<int> *hv[3] = {&tile, &tsort, &rnd};
+  DBuf<int> d_ord[3];
+  DBuf<double> val;
+  for (int k = 0; k < 3; k++) {
+    CK(d_ord[k].alloc(std::max(1, no)), "probe order");
+    CK(hipMemcpy(d_ord[k].p, hv[k]->data(), sizeof(int) * no, hipMemcpyHostToDevice), "probe order");
+  }
+  CK(val.alloc(std::max<size_t>(1, size_t(c->L.chunk_off[c->L.nchunks]))), "probe slots");
+  const int *orders[4] = {nullptr, d_ord[0].p, d_ord[1].p, d_ord[2].p};
+  double *res[4] = {&out->us_sell, &out->us_tile, &out->us_tile_sorted, &out->us_random};
+  for (int k = 0; k < 4; k++) {
+    for (int w = 0; w < 2; w++) CK(pnp::launch_slot_store_probe(c->dl, orders[k], val.p, c->stream), "probe");
+    hipEvent_t e0 = c->ev_get(), e1 = c->ev_get();
+    hipEventRecord(e0, c->stream);
+    for (int i = 0; i < reps; i++) CK(pnp::launch_slot_store_probe(c->dl, orders[k], val.p, c->stream), "probe");
+    hipEventRecord(e1, c->stream);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    float t = 0;
+    if (e == hipSuccess) hipEventElapsedTime(&t, e0, e1);
+    c->ev_pool.push_back(e0);
+    c->ev_pool.push_back(e1);
+    CK(e, "probe");
+    *res[k] = 1e3 * t / reps;
+  }
+  out->slot_bytes = 8 * slots;
+  out->rows = no;
+  out->tiles = (ne + tile_elems - 1) / tile_elems;
+  out->elements = ne;
+  return PNP_OK;
 }
 
 extern "C" int pnp_cache_scrub(pnp_ctx *c, int64_t bytes) {

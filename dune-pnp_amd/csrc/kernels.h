@@ -558,5 +558,9 @@ hipError_t launch_pk_mass_apply(const DevLayout &L, const PkDev &P, const double
 // calcIonFlux: seg = {local element, local face, group}; out[2s], out[2s+1]
 hipError_t launch_pk_ion_flux(const DevLayout &L, const PkDev &P, int ns, const int4 *seg,
                               const double *x, int cyl, double pi, double *out, hipStream_t s);
+// pnp_probe_slot_stores: every SELL slot of every owned row written once, row order[t] by thread t
+// (order null: SELL order); val holds chunk_off[nchunks] doubles
+hipError_t launch_slot_store_probe(const DevLayout &L, const int *order, double *val,
+                                   hipStream_t s);
 
 }  // namespace pnp

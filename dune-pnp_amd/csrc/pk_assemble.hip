@@ -114,6 +114,18 @@ struct PkArgs {
   double l_b, c0, pi, dt, z;
 };
 
+// PBOperator's sinh / cosh from one exp and one reciprocal (as assemble.hip's P1 element): where
+// a point needs both, the exp and the division are shared; the sinh's error is absolute,
+// ~eps * e^|u|, against residual terms of at least that size
+__device__ __forceinline__ double pb_sinh(double u) {
+  const double e = exp(u);
+  return 0.5 * (e - 1.0 / e);
+}
+__device__ __forceinline__ double pb_cosh(double u) {
+  const double e = exp(u);
+  return 0.5 * (e + 1.0 / e);
+}
+
 // quadrature factor of the reference: weight * integrationElement (* 2 PI y when cylindrical)
 template <int NL>
 __device__ __forceinline__ double factor(const PkGeo &G, const PkPoint<NL> &P, int cyl, double pi) {
@@ -148,7 +160,7 @@ __device__ void pk_jac_row(const PkGeo &G, const PkArgs &a, int ra, const double
         double u = 0.0;
 #pragma unroll
         for (int i = 0; i < NL; i++) u += xl[i] * P.phi[i];
-        c = 8 * PI * a.l_b * a.c0 * cosh(u) * P.phi[ra];
+        c = 8 * PI * a.l_b * a.c0 * pb_cosh(u) * P.phi[ra];
       }
       double ga0, ga1;
       grad(G, P, ra, ga0, ga1);
@@ -221,7 +233,7 @@ __device__ double pk_row_residual(const PkGeo &G, const PkArgs &a, int ra, const
           cm += f1[i] * P.phi[i];
         }
       }
-      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
       double g0, g1;
       grad(G, P, ra, g0, g1);
       r += (gu0 * g0 + gu1 * g1 + s * P.phi[ra]) * f;
@@ -293,8 +305,8 @@ __device__ void pk_row_both(const PkGeo &G, const PkArgs &a, int ra, const doubl
           cm += f1[i] * P.phi[i];
         }
       }
-      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
-      const double c = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * cosh(u) * P.phi[ra] : 0.0;
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+      const double c = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_cosh(u) * P.phi[ra] : 0.0;
       double ga0, ga1;
       grad(G, P, ra, ga0, ga1);
       r += (gu0 * ga0 + gu1 * ga1 + s * P.phi[ra]) * f;
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(kB) void k_pk_elem_res(PkDev D, const double *__res
           cm += f1[i] * P.phi[i];
         }
       }
-      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+      const double s = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
 #pragma unroll
       for (int ra = 0; ra < NL; ra++)
         r[ra] += (gu0 * g[ra][0] + gu1 * g[ra][1] + s * P.phi[ra]) * f;
@@ -648,8 +660,8 @@ void k_pk_elem_jac(PkDev D, const double *__restrict__ xy, const double *__restr
         QV(5 * q) = factor(G, P, a.cyl, PI);
         QV(1 + 5 * q) = gu0;
         QV(2 + 5 * q) = gu1;
-        QV(3 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
-        QV(4 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * cosh(u) : 0.0;
+        QV(3 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_sinh(u) : 1 * a.l_b * 4 * PI * (cm - cp);
+        QV(4 + 5 * q) = a.kind == OP_PB ? 8 * PI * a.l_b * a.c0 * pb_cosh(u) : 0.0;
       }
     } else {
 #pragma unroll 1
@@ -1048,6 +1060,28 @@ hipError_t launch_pk_ion_flux(const DevLayout &L, const PkDev &P, int ns, const 
     hipLaunchKernelGGL(k_pk_ion_flux<3>, g, b, 0, s, ns, seg, P.ne, P.enode, L.xy, x, cyl, pi, out);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// Store-pattern probe (pnp_probe_slot_stores): thread t writes every SELL slot of row order[t]
+// (order null: row t), one 8-B store per slot, as the gather pass stores a finished row.  With the
+// rows in SELL order a wave's stores of one slot fill 512 contiguous bytes; in a tile order they
+// land wherever the tile's rows sit in the colour-major SELL.
+__global__ void __launch_bounds__(256) k_slot_store_probe(int n, const int *order, DevLayout L,
+                                                          double *val) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int r = order ? order[t] : t;
+  const int len = int(L.rowmeta[r] & 63);
+  double *p = val + L.chunk_off[r >> 6] + (r & 63);
+  for (int sl = 0; sl < len; sl++) p[64 * sl] = double(t) + sl;
+}
+
+hipError_t launch_slot_store_probe(const DevLayout &L, const int *order, double *val,
+                                   hipStream_t s) {
+  if (L.n_owned == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_slot_store_probe, dim3((L.n_owned + 255) / 256), dim3(256), 0, s,
+                     L.n_owned, order, L, val);
   return hipGetLastError();
 }
 

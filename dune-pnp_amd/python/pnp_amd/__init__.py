@@ -179,6 +179,13 @@ class _SpaceInfo(C.Structure):
                 ("nlocal", C.c_int32)]
 
 
+class _StoreProbe(C.Structure):
+    _fields_ = [("us_sell", C.c_double), ("us_tile", C.c_double), ("us_tile_sorted", C.c_double),
+                ("us_random", C.c_double),
+                ("slot_bytes", C.c_int64), ("rows", C.c_int64), ("rows_whole", C.c_int64),
+                ("tiles", C.c_int64), ("elements", C.c_int64)]
+
+
 class _OpArgs(C.Structure):
     _fields_ = [("kind", C.c_int32), ("dt", C.c_double), ("z", C.c_double),
                 ("field", C.c_int32), ("phi", C.c_void_p), ("cp", C.c_void_p),
@@ -768,6 +775,13 @@ class Context:
         v = C.c_int64()
         self._ck(lib().pnp_get_option(self.h, int(option), C.byref(v)))
         return v.value
+
+    def probe_slot_stores(self, tile_elems=256, reps=20):
+        """pnp_probe_slot_stores (P_k contexts): the SELL slot stores of one Jacobian in SELL,
+        spatial-tile and random row order; dict of the pnp_store_probe fields."""
+        o = _StoreProbe()
+        self._ck(lib().pnp_probe_slot_stores(self.h, int(tile_elems), int(reps), C.byref(o)))
+        return {k: getattr(o, k) for k, _ in _StoreProbe._fields_}
 
     def cache_scrub(self, nbytes=1 << 30):
         """Evict the caches (read nbytes of scratch on the context's stream) before a cold timing."""

@@ -504,6 +504,23 @@ int pnp_assemble_state_timed(pnp_ctx *ctx, int32_t n, double *ms);
 /* n BiCGSTAB iterations (no convergence stop) on J z = r of the last assembly */
 int pnp_bicgstab_iterations(pnp_ctx *ctx, int32_t n, int32_t prec, pnp_solve_result *res);
 
+/* Store-pattern probe of a P_k context (measurement hook, no reference counterpart): the time of
+ * writing every SELL slot of every owned row once, one thread per row, with the rows taken in
+ * (a) SELL order -- what the Jacobian's gather pass does -- (b) a spatial tile order: tiles of
+ * `tile_elems` consecutive local elements (ascending element id), each row in the tile of its
+ * first incident element, in the order the tile's elements reach them, as an element-tiled
+ * assembly that kept whole rows in LDS would store them, (c) the same tiles with each tile's rows
+ * sorted into SELL order (the best such a tile can do), and (d) a seeded random order.  Averages
+ * over `reps` launches after two untimed ones, one HIP event pair each; rows_whole counts the rows
+ * whose incident elements all lie in one tile (the rows such a tile could finish without
+ * spilling). */
+typedef struct {
+  double us_sell, us_tile, us_tile_sorted, us_random;
+  int64_t slot_bytes;  /* 8 B x (sum of row lengths): the bytes each launch stores */
+  int64_t rows, rows_whole, tiles, elements;
+} pnp_store_probe;
+int pnp_probe_slot_stores(pnp_ctx *ctx, int32_t tile_elems, int32_t reps, pnp_store_probe *out);
+
 /* read `bytes` of a context-owned scratch buffer on the context's stream, then synchronise:
  * evicts the matrix and vectors from the L2s and the Infinity Cache before a cache-cold timing
  * (dirty lines are written back here, outside the timed launch) */
