@@ -206,6 +206,9 @@ int orc_pk_build(const orc_mesh *m, int k, orc_pk *S);
 void orc_pk_free(orc_pk *S);
 /* Lagrange basis of degree k on the local nodes at (xi, eta): phi[nl], dphi[nl][2] */
 void orc_pk_basis(int k, double xi, double eta, double *phi, double *dphi);
+/* the simplex rule of an intorder on the reference triangle (order <= 2: 3 points, 3: 4, else the
+ * 7-point order-5 rule): n points into xi / eta / w (room for 7), returns n */
+int orc_quadrature_rule(int order, double *xi, double *eta, double *w);
 void orc_pk_dirichlet_mask(const orc_mesh *m, const orc_pk *S, const orc_params *p, int field,
                            uint8_t *mask);
 void orc_pk_residual(const orc_mesh *m, const orc_pk *S, const orc_params *p,

@@ -286,6 +286,17 @@ static void rule_of(int order, prule *R) {
   }
 }
 
+int orc_quadrature_rule(int order, double *xi, double *eta, double *w) {
+  prule R;
+  rule_of(order, &R);
+  for (int q = 0; q < R.n; q++) {
+    xi[q] = R.xi[q];
+    eta[q] = R.eta[q];
+    w[q] = R.w[q];
+  }
+  return R.n;
+}
+
 /* ---- element geometry ---------------------------------------------------------------------- */
 typedef struct {
   double x0, y0, J00, J01, J10, J11, adet;

@@ -320,6 +320,13 @@ class PkSpace:
         return u
 
 
+def quadrature_rule(order):
+    """(xi, eta, w) of the oracle's simplex rule for an intorder (orc_quadrature_rule)."""
+    xi, eta, w = np.zeros(7), np.zeros(7), np.zeros(7)
+    n = lib().orc_quadrature_rule(int(order), _p(xi), _p(eta), _p(w))
+    return xi[:n], eta[:n], w[:n]
+
+
 def bicgstab(A, b, prec=PREC_NONE, reduction=1e-8, maxit=20000, x0=None):
     """ISTL-semantics BiCGStab on a scipy CSR matrix (sorted indices)."""
     return _krylov("orc_bicgstab", A, b, prec, reduction, maxit, x0)

@@ -354,3 +354,21 @@ def test_pk_md_driver_matches_oracle_loop(tmp_path):
         scale = max(np.abs(ip).max(), np.abs(im).max(), 1e-30)
         assert np.abs(got[:, 0] - ip).max() <= 1e-8 * scale
         assert np.abs(got[:, 2] - im).max() <= 1e-8 * scale
+
+
+def test_slot_store_probe_counts():
+    """pnp_probe_slot_stores: every owned row and every local element is
+    counted, each order writes the stored slots once (at most the padded SELL, at least one slot per
+    row), and a tile owns at most all rows."""
+    mesh, ctx, _ = setup("pore_small", 2)
+    ctx.set_operator(P.OP_PB)
+    ctx.jacobian(np.zeros(ctx.nn), export=False)
+    info = ctx.info()
+    r = ctx.probe_slot_stores(16, reps=2)
+    assert r["rows"] == ctx.nn and r["elements"] == mesh.nt
+    assert r["tiles"] == (mesh.nt + 15) // 16
+    assert 8 * ctx.nn <= r["slot_bytes"] <= 8 * info["nslots"]
+    assert 0 < r["rows_whole"] <= r["rows"]
+    assert all(r[k] > 0 for k in ("us_sell", "us_tile", "us_tile_sorted", "us_random"))
+    with pytest.raises(P.PnpError):
+        ctx.probe_slot_stores(0)

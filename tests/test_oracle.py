@@ -336,3 +336,26 @@ def test_all_core_assembly_matches_serial(kind):
     J1 = P.jacobian(op, x, fd=True)
     np.testing.assert_allclose(r, r1, rtol=0, atol=1e-12 * np.max(np.abs(r1)))
     assert abs(A - J1).max() <= 1e-12 * abs(J1).max()
+
+
+@pytest.mark.parametrize("order,npts", [(2, 3), (3, 4), (5, 7)])
+def test_quadrature_rules_are_exact_to_their_order(order, npts):
+    """The simplex rules the oracle (and, through the 1e-12 parity tests, the kernels) use for the
+    reference's intorders: each integrates every monomial xi^a eta^b with a + b <= order exactly
+    over the reference triangle (a! b! / (a + b + 2)!) and some monomial of degree order + 1 not
+    (the rule is of that order, no more).  Which order-2 / order-3 point set dune-geometry's
+    SimplexQuadraturePoints<2> picks is not pinned by any reference fixture: PNP
+    and Poisson integrands are polynomials the rule integrates exactly, so they do not depend on
+    it; PB's sinh and the cylindrical PnpT mass do, at the rule's truncation error."""
+    from math import factorial
+    xi, eta, w = O.quadrature_rule(order)
+    assert len(w) == npts
+    assert abs(w.sum() - 0.5) <= 1e-15
+    assert np.all((xi > 0) & (eta > 0) & (xi + eta < 1))  # interior points
+    for deg in range(order + 2):
+        errs = [abs(np.sum(w * xi ** a * eta ** (deg - a)) -
+                    factorial(a) * factorial(deg - a) / factorial(deg + 2)) for a in range(deg + 1)]
+        if deg <= order:
+            assert max(errs) <= 1e-15, (deg, errs)
+        else:
+            assert max(errs) > 1e-6, (deg, errs)
