@@ -139,8 +139,9 @@ __global__ __launch_bounds__(kB) void k_dinv(int nb, const int *__restrict__ dpo
   for (int k = 0; k < NB; k++) dinv[size_t(i) * NB + k] = X[k];
 }
 
-// coarsest level: column-major dense copy of the block-CSR matrix (the inverse is computed by
-// rocSOLVER getrf/getri in place, ctx.cc amg_setup)
+// coarsest level: ROW-major dense copy of the block-CSR matrix A, i.e. A^T column-major.
+// rocSOLVER getrf/getri (column-major, in place, ctx.cc amg_setup) then leave (A^T)^-1 =
+// (A^-1)^T column-major = A^-1 row-major, the layout k_coarse_apply streams row by row.
 __global__ __launch_bounds__(kB) void k_coarse_dense(int nb, int nf, const int *__restrict__ rp,
                                                      const int *__restrict__ col,
                                                      const double *__restrict__ v,
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(kB) void k_coarse_dense(int nb, int nf, const int *
   const int n = nb * nf, nbb = nf * nf;
   for (int q = rp[r]; q < rp[r + 1]; q++)
     for (int e = 0; e < nbb; e++)  // entry (r*nf + e/nf, col*nf + e%nf)
-      dense[size_t(col[q] * nf + e % nf) * n + r * nf + e / nf] = v[size_t(q) * nbb + e];
+      dense[size_t(r * nf + e / nf) * n + col[q] * nf + e % nf] = v[size_t(q) * nbb + e];
 }
 
 // ---- V-cycle kernels ------------------------------------------------------------------------
@@ -336,30 +337,58 @@ __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
   jacobi_task<NF, LPR, CORR>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega, out);
 }
 
-// coarsest: x = Ainv b (ainv column-major n x n, n <= kAmgMaxDense): 16 rows per workgroup, the
-// columns split over 64 lane groups (each reads 128-B row segments of a column), partial sums
-// combined in LDS; n / 16 workgroups (~170 at n = 2772) stream the 61 MB inverse
-constexpr int kCaRows = 16, kCaParts = 64;
-__global__ __launch_bounds__(kCaRows * kCaParts) void k_coarse_apply(int n,
-                                                                     const double *__restrict__ ainv,
-                                                                     const double *__restrict__ b,
-                                                                     double *__restrict__ x) {
+// coarsest: x = Ainv b, Ainv row-major n x n (n <= kAmgMaxDense; see k_coarse_dense).  One wave
+// per row: its 64 lanes stream the row in 1-KB pieces (VEC2, n even: 16-B loads, each row
+// 16-B aligned) or 512-B pieces (n odd) against b staged in LDS, four accumulators per lane, then
+// a fixed cross-lane tree -- the same sums in the same order every call.  The column-major form
+// before it (16 rows per 1,024-thread workgroup: 169 workgroups at n = 2,694, each load four 128-B
+// segments) took 25 us per call at config 3, 2.3 TB/s on the 58-MB inverse
+// (profiles/r05/amg/split_r5o.txt).
+constexpr int kCaWaves = 4;
+template <int VEC2>
+__global__ __launch_bounds__(64 * kCaWaves) void k_coarse_apply(int n,
+                                                               const double *__restrict__ ainv,
+                                                               const double *__restrict__ b,
+                                                               double *__restrict__ x) {
   __shared__ double bs[kAmgMaxDense];
-  __shared__ double part[kCaParts][kCaRows];
-  for (int j = threadIdx.x; j < n; j += kCaRows * kCaParts) bs[j] = b[j];
+  for (int j = threadIdx.x; j < n; j += 64 * kCaWaves) bs[j] = b[j];
   __syncthreads();
-  const int r = threadIdx.x % kCaRows, q = threadIdx.x / kCaRows;
-  const int i = blockIdx.x * kCaRows + r;
-  double s = 0;
-  if (i < n)
-    for (int j = q; j < n; j += kCaParts) s += ainv[size_t(j) * n + i] * bs[j];
-  part[q][r] = s;
-  __syncthreads();
-  if (q == 0 && i < n) {
-    double t = 0;
-    for (int k = 0; k < kCaParts; k++) t += part[k][r];
-    x[i] = t;
+  const int l = threadIdx.x % 64, i = blockIdx.x * kCaWaves + threadIdx.x / 64;
+  if (i >= n) return;
+  const double *__restrict__ row = ainv + size_t(i) * n;
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  if constexpr (VEC2) {
+    const double2 *__restrict__ r2 = reinterpret_cast<const double2 *>(row);
+    const int n2 = n / 2;
+    int p = l;
+#pragma unroll 4
+    for (; p + 64 < n2; p += 128) {
+      const double2 u = r2[p], w = r2[p + 64];
+      s0 = __builtin_fma(u.x, bs[2 * p], s0);
+      s1 = __builtin_fma(u.y, bs[2 * p + 1], s1);
+      s2 = __builtin_fma(w.x, bs[2 * p + 128], s2);
+      s3 = __builtin_fma(w.y, bs[2 * p + 129], s3);
+    }
+    if (p < n2) {
+      const double2 u = r2[p];
+      s0 = __builtin_fma(u.x, bs[2 * p], s0);
+      s1 = __builtin_fma(u.y, bs[2 * p + 1], s1);
+    }
+  } else {
+    int j = l;
+#pragma unroll 2
+    for (; j + 192 < n; j += 256) {
+      s0 = __builtin_fma(row[j], bs[j], s0);
+      s1 = __builtin_fma(row[j + 64], bs[j + 64], s1);
+      s2 = __builtin_fma(row[j + 128], bs[j + 128], s2);
+      s3 = __builtin_fma(row[j + 192], bs[j + 192], s3);
+    }
+    for (; j < n; j += 64) s0 = __builtin_fma(row[j], bs[j], s0);
   }
+  double t = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if (l == 0) x[i] = t;
 }
 
 // (Running the small levels -- pre-smoothing, residual, restriction, coarsest solve,
@@ -368,7 +397,8 @@ __global__ __launch_bounds__(kCaRows * kCaParts) void k_coarse_apply(int n,
 // per V-cycle for the levels <= 256 rows (profiles/r01/ab_amg_tail_*.log): one CU cannot hide the
 // dependent gathers that ~4.5 us launches spread over the whole chip.)
 
-// level 0 prolongation: y = x0 + e1[agg0]
+// level 0 prolongation: y = x0 + e1[agg0] (x0 null: the cycle without level-0 pre-smoothing,
+// x0 = 0, y = e1[agg0] -- no 17.7-MB memset of x0 per cycle at config 3)
 template <int NF>
 __global__ __launch_bounds__(kB) void k_prolong0(int n, const int *__restrict__ agg,
                                                  const double *__restrict__ x0,
@@ -377,11 +407,13 @@ __global__ __launch_bounds__(kB) void k_prolong0(int n, const int *__restrict__ 
   const int i = blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   double a[NF], c[NF];
-  load_nf<NF>(x0, size_t(i), a);
   load_nf<NF>(e1, size_t(agg[i]), c);
+  if (x0) {
+    load_nf<NF>(x0, size_t(i), a);
 #pragma unroll
-  for (int f = 0; f < NF; f++) a[f] += c[f];
-  store_nf<NF>(y, size_t(i), a);
+    for (int f = 0; f < NF; f++) c[f] = a[f] + c[f];
+  }
+  store_nf<NF>(y, size_t(i), c);
 }
 
 inline dim3 g1(long long n) { return dim3(unsigned((n + kB - 1) / kB)); }
@@ -465,8 +497,11 @@ hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s) {
   if (n > kAmgMaxDense) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_coarse_apply, dim3((n + kCaRows - 1) / kCaRows), dim3(kCaRows * kCaParts), 0,
-                     s, n, ainv, b, x);
+  const dim3 g((n + kCaWaves - 1) / kCaWaves), blk(64 * kCaWaves);
+  if (n % 2 == 0)
+    hipLaunchKernelGGL(k_coarse_apply<1>, g, blk, 0, s, n, ainv, b, x);
+  else
+    hipLaunchKernelGGL(k_coarse_apply<0>, g, blk, 0, s, n, ainv, b, x);
   return hipGetLastError();
 }
 

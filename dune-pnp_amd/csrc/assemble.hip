@@ -96,6 +96,13 @@ struct OpTraits {
   static constexpr int NK = nks_of(PAT);
 };
 
+// PBOperator: a vertex's e^{u/5} and e^{-u/5}, the factors element() builds the quadrature
+// points' e^u from
+__device__ __forceinline__ void pb_fifth(double u, double &e, double &ei) {
+  e = exp(0.2 * u);
+  ei = 1.0 / e;
+}
+
 // Contributions of element (i, b, c) to row i: residual res[NF], blocks (i,i), (i,b), (i,c).
 template <int OP, int JAC>
 __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double yi, double yb,
@@ -153,20 +160,25 @@ __device__ __forceinline__ void element(const AsmArgs &a, const Geo &G, double y
     double gu1 = ui[0] * G.gi1 + ub[0] * G.gb1 + uc[0] * G.gc1;
     double gg = gu0 * G.gi0 + gu1 * G.gi1;
     double beta = 8 * PI * a.l_b * a.c0;
+    // sinh and cosh at each point from e^u and e^-u (the library's sinh and cosh each cost about
+    // two exps; the PB launch is issue-bound on them).  The walk passes each vertex's e^{u/5} and
+    // e^{-u/5} (pi_, pb_, pc_ / qi, qb, qc), computed once per vertex of the fan: the three
+    // off-centre points are fifths, (0.2, 0.6, 0.2) and its rotations, so there e^u is a product
+    // of them; only the centroid takes an exp and a division of its own.  Errors: a few ulps of
+    // e^|u|, absolute in the sinh term, against residual terms of at least that size.
+    const double Eq = pi_ * pb_ * pc_, Iq = qi * qb * qc;
+    const double eu[4] = {exp(P[0][0] * ui[0] + P[0][1] * ub[0] + P[0][2] * uc[0]), Eq * pb_ * pb_,
+                          Eq * pc_ * pc_, Eq * pi_ * pi_};
+    const double ei[4] = {1.0 / eu[0], Iq * qb * qb, Iq * qc * qc, Iq * qi * qi};
     double W = 0, Ri = 0, Jii = 0, Jib = 0, Jic = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       double f = w[q] * G.adet;
       if (a.cylindrical) f *= (P[q][0] * yi + P[q][1] * yb + P[q][2] * yc) * 2 * PI;
-      double u = P[q][0] * ui[0] + P[q][1] * ub[0] + P[q][2] * uc[0];
       W += f;
-      // sinh and cosh from one exp and one reciprocal (the library's sinh and cosh each cost about
-      // two exps, and the PB launch is issue-bound on them); the sinh term's error is absolute,
-      // ~eps * e^|u|, against residual terms of at least that size
-      const double e = exp(u), ei = 1.0 / e;
-      Ri += f * (0.5 * (e - ei)) * P[q][0];
+      Ri += f * (0.5 * (eu[q] - ei[q])) * P[q][0];
       if constexpr (JAC) {
-        double ch = f * (0.5 * (e + ei)) * P[q][0];
+        double ch = f * (0.5 * (eu[q] + ei[q])) * P[q][0];
         Jii += ch * P[q][0];
         Jib += ch * P[q][1];
         Jic += ch * P[q][2];
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
   double ai = 0, aq = 0;
   if constexpr (OP == OP_DIFF || OP == OP_DIFF_IE || OP == OP_POISSON) ai = a.aux0[row];
   if constexpr (OP == OP_POISSON) aq = a.aux1[row];
+  if constexpr (OP == OP_PB) pb_fifth(ui[0], ai, aq);  // element(): e^{u/5}, e^{-u/5} per vertex
 
   double R[NF], D[NK], P[NK], F[NK];  // block coefficients, see OpTraits::NK
 #pragma unroll
@@ -295,6 +308,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
       return cix[k * kRows];
   };
   load_nb(col(1), pc, uc, ac0, ac1);
+  if constexpr (OP == OP_PB) pb_fifth(uc[0], ac0, ac1);
   {
     const int t1 = next_slot(1);
     if (t1 > 0) load_nb(t1 == 1 ? col(1) : col(2), pn, un, an0, an1);
@@ -321,6 +335,9 @@ __global__ __launch_bounds__(256, MINW) void k_assemble(DevLayout L, AsmArgs a) 
       }
     }
     const bool elem = t > 0 && !((brk >> s) & 1);
+    // v_t's e^{u/5} for this element and, rotated into v_s, the next one
+    if constexpr (OP == OP_PB)
+      if (t > 0) pb_fifth(un[0], an0, an1);
     if (elem) {
       Geo G;
       geometry(pi2.x, pi2.y, pc.x, pc.y, pn.x, pn.y, G);
@@ -441,6 +458,7 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   double ai = 0, aq = 0;
   if constexpr (AUX0) ai = a.aux0[row];
   if constexpr (AUX1) aq = a.aux1[row];
+  if constexpr (OP == OP_PB) pb_fifth(ui[0], ai, aq);  // element(): e^{u/5}, e^{-u/5} per vertex
   if constexpr (LDSG) {
     const int u0 = L.uptr[blk], cnt = L.uown[blk];  // the fan neighbours (own rows come after)
     // up to ASM_SU list entries per thread: their list loads, then their gathers, then the LDS
@@ -506,6 +524,8 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
   };
 #pragma unroll
   for (int k = 1; k < SPLIT; k++) gather(k);
+  // PB: slot k's e^{u/5} goes to a0[k] / a1[k] when element k - 1 needs it (slot 1: up front)
+  if constexpr (OP == OP_PB) pb_fifth(un[1][0], a0[1], a1[1]);
 
   double R[NF], D[NK], P[NK], F[NK];
 #pragma unroll
@@ -547,6 +567,8 @@ __global__ __launch_bounds__(256, MINW) void k_assemble_ga(DevLayout L, AsmArgs 
       const bool has_next = s + 1 < len;
       const int sn = (s + 1 < NS) ? s + 1 : 1;  // static slot of v_{s+1}
       const bool elem = (has_next || closed) && !((brk >> s) & 1);
+      if constexpr (OP == OP_PB)
+        if (has_next) pb_fifth(un[sn][0], a0[sn], a1[sn]);
       if (elem) {
         // v_t = v_{s+1}, or v_1 when a closed fan wraps
         const double2 pt = has_next ? pn[sn] : pn[1];

@@ -1801,7 +1801,7 @@ struct pnp_ctx {
       e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_x0.p, amg_t.p, 3, d, partials.p, &nsp,
                            stream);
     } else {
-      e = hipMemsetAsync(amg_x0.p, 0, sizeof(double) * nn, stream);
+      e = hipSuccess;  // x0 = 0: the restriction takes d, the prolongation no x0
     }
     if (e == hipSuccess)
       e = pnp::launch_amg_restrict(nf, amg_d[0]->nb, amg_d[0]->mptr.p, amg_d[0]->mem.p,
@@ -1838,7 +1838,9 @@ struct pnp_ctx {
       }
     }
     // level 0: prolongation, post-smoothing x += M^{-1} (d - A x)
-    if (e == hipSuccess) e = pnp::launch_amg_prolong0(nf, n, amg_d[0]->agg.p, amg_x0.p, res, amg_y.p, stream);
+    if (e == hipSuccess)
+      e = pnp::launch_amg_prolong0(nf, n, amg_d[0]->agg.p, pre0 ? amg_x0.p : nullptr, res,
+                                   amg_y.p, stream);
     if (e == hipSuccess)
       e = pnp::launch_spmv(dl, nf, pat, vals.p, amg_y.p, amg_r.p, 3, d, partials.p, &nsp, stream);
     if (e != hipSuccess) return hipfail(e, "amg v-cycle");
