@@ -45,7 +45,8 @@ hipError_t launch_amg_galerkin(int nf, long long nq, const long long *cptr, cons
                                const double *fv, double *cv, hipStream_t s);
 hipError_t launch_amg_dinv(int nf, int nb, const int *dpos, const double *v, double *dinv,
                            hipStream_t s);
-// dense (column-major, n = nb*nf, zero-filled here) copy of the coarsest block-CSR matrix
+// dense (row-major, n = nb*nf, zero-filled here) copy of the coarsest block-CSR matrix, i.e. its
+// transpose column-major for rocSOLVER (see k_coarse_dense)
 hipError_t launch_amg_coarse_dense(int nf, int nb, const int *rp, const int *col, const double *v,
                                    double *dense, hipStream_t s);
 // bn[J] = sum over the members i of aggregate J of (a - sub)_i (sub may be null); xn = omega
@@ -53,15 +54,19 @@ hipError_t launch_amg_coarse_dense(int nf, int nb, const int *rp, const int *col
 hipError_t launch_amg_restrict(int nf, int nbn, const int *mptr, const int *mem, const double *a,
                                const double *sub, double *bn, const double *dinvn, double omega,
                                double *xn, hipStream_t s);
-// r = b - A x on a coarse level
+// r = b - A x on a coarse level (vf non-null: the level's single-precision values instead of v)
 hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const double *v,
-                            const double *x, const double *b, double *r, hipStream_t s);
+                            const float *vf, const double *x, const double *b, double *r,
+                            hipStream_t s);
+// vf[i] = float(v[i]) (a coarse level's values for the V-cycle, PNP_AMG_F32)
+hipError_t launch_amg_to_f32(long long n, const double *v, float *vf, hipStream_t s);
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s);
-// e == nullptr: a plain damped block-Jacobi sweep (no correction; agg unused)
+// e == nullptr: a plain damped block-Jacobi sweep (no correction; agg unused); vf as above
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
-                           const int *agg, const double *x, const double *e, const double *b,
-                           const double *dinv, double omega, double *out, hipStream_t s);
+                           const float *vf, const int *agg, const double *x, const double *e,
+                           const double *b, const double *dinv, double omega, double *out,
+                           hipStream_t s);
 hipError_t launch_amg_prolong0(int nf, int n, const int *agg, const double *x0, const double *e1,
                                double *y, hipStream_t s);
 

@@ -14,6 +14,9 @@
 // levels, an exact dense solve (Gauss-Jordan inverse, one workgroup) on the coarsest.
 // Restriction is fused with the residual and the next level's pre-smoothing; prolongation is
 // fused into the post-smoothing sweep.  Everything here is HBM/latency bound, fp64.
+#include <algorithm>
+#include <type_traits>
+
 #include "amg.h"
 
 namespace pnp {
@@ -155,13 +158,13 @@ __global__ __launch_bounds__(kB) void k_coarse_dense(int nb, int nf, const int *
 }
 
 // ---- V-cycle kernels ------------------------------------------------------------------------
-template <int NF>
-__device__ __forceinline__ void bmv_acc(const double *__restrict__ B, const double (&x)[NF],
+template <int NF, typename VT = double>
+__device__ __forceinline__ void bmv_acc(const VT *__restrict__ B, const double (&x)[NF],
                                         double (&y)[NF]) {
 #pragma unroll
   for (int f = 0; f < NF; f++)
 #pragma unroll
-    for (int g = 0; g < NF; g++) y[f] += B[f * NF + g] * x[g];
+    for (int g = 0; g < NF; g++) y[f] += double(B[f * NF + g]) * x[g];
 }
 
 // The coarse levels are small (68K .. 17 rows at config 3) with ~10-20 blocks per row, so one
@@ -182,10 +185,10 @@ __device__ __forceinline__ void lanes_sum(double (&v)[NF]) {
 // (live or not: the cross-lane adds need all).
 
 // r = b - A x on a coarse level (block-CSR)
-template <int NF, int LPR>
+template <int NF, int LPR, typename VT>
 __device__ __forceinline__ void resid_task(int I, int q, bool live, const int *__restrict__ rp,
                                            const int *__restrict__ col,
-                                           const double *__restrict__ v,
+                                           const VT *__restrict__ v,
                                            const double *__restrict__ x,
                                            const double *__restrict__ b, double *__restrict__ r) {
   constexpr int NB = NF * NF;
@@ -196,7 +199,7 @@ __device__ __forceinline__ void resid_task(int I, int q, bool live, const int *_
     for (int k = rp[I] + q; k < rp[I + 1]; k += LPR) {
       double xj[NF];
       load_nf<NF>(x, size_t(col[k]), xj);
-      bmv_acc<NF>(v + size_t(k) * NB, xj, acc);
+      bmv_acc<NF, VT>(v + size_t(k) * NB, xj, acc);
     }
   lanes_sum<NF, LPR>(acc);
   if (!live || q != 0) return;
@@ -250,10 +253,10 @@ __device__ __forceinline__ void restrict_task(int J, int q, bool live, const int
 
 // one damped block-Jacobi sweep, with the coarse correction folded in when CORR:
 //   xc(j) = x[j] (+ e[agg[j]]),  out[I] = xc(I) + omega Dinv_I (b_I - sum_j A_Ij xc(j))
-template <int NF, int LPR, int CORR>
+template <int NF, int LPR, int CORR, typename VT>
 __device__ __forceinline__ void jacobi_task(int I, int q, bool live, const int *__restrict__ rp,
                                             const int *__restrict__ col,
-                                            const double *__restrict__ v,
+                                            const VT *__restrict__ v,
                                             const int *__restrict__ agg,
                                             const double *__restrict__ x,
                                             const double *__restrict__ e,
@@ -275,7 +278,7 @@ __device__ __forceinline__ void jacobi_task(int I, int q, bool live, const int *
 #pragma unroll
         for (int f = 0; f < NF; f++) xj[f] += ej[f];
       }
-      bmv_acc<NF>(v + size_t(k) * NB, xj, acc);
+      bmv_acc<NF, VT>(v + size_t(k) * NB, xj, acc);
     }
   lanes_sum<NF, LPR>(acc);
   if (!live || q != 0) return;
@@ -299,15 +302,15 @@ __device__ __forceinline__ void jacobi_task(int I, int q, bool live, const int *
   store_nf<NF>(out, size_t(I), xi);
 }
 
-template <int NF, int LPR>
+template <int NF, int LPR, typename VT>
 __global__ __launch_bounds__(kB) void k_resid(int nb, const int *__restrict__ rp,
                                               const int *__restrict__ col,
-                                              const double *__restrict__ v,
+                                              const VT *__restrict__ v,
                                               const double *__restrict__ x,
                                               const double *__restrict__ b,
                                               double *__restrict__ r) {
   const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR;
-  resid_task<NF, LPR>(I, gt % LPR, I < nb, rp, col, v, x, b, r);
+  resid_task<NF, LPR, VT>(I, gt % LPR, I < nb, rp, col, v, x, b, r);
 }
 
 template <int NF, int LPR>
@@ -323,10 +326,10 @@ __global__ __launch_bounds__(kB) void k_restrict(int nbn, const int *__restrict_
 }
 
 // post-smoothing sweep (CORR = 1: with the coarse correction e folded in; 0: plain sweep)
-template <int NF, int LPR, int CORR>
+template <int NF, int LPR, int CORR, typename VT>
 __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
                                              const int *__restrict__ col,
-                                             const double *__restrict__ v,
+                                             const VT *__restrict__ v,
                                              const int *__restrict__ agg,
                                              const double *__restrict__ x,
                                              const double *__restrict__ e,
@@ -334,7 +337,8 @@ __global__ __launch_bounds__(kB) void k_post(int nb, const int *__restrict__ rp,
                                              const double *__restrict__ dinv, double omega,
                                              double *__restrict__ out) {
   const int gt = blockIdx.x * kB + threadIdx.x, I = gt / LPR;
-  jacobi_task<NF, LPR, CORR>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega, out);
+  jacobi_task<NF, LPR, CORR, VT>(I, gt % LPR, I < nb, rp, col, v, agg, x, e, b, dinv, omega,
+                                 out);
 }
 
 // coarsest: x = Ainv b, Ainv row-major n x n (n <= kAmgMaxDense; see k_coarse_dense).  One wave
@@ -396,6 +400,14 @@ __global__ __launch_bounds__(64 * kCaWaves) void k_coarse_apply(int n,
 // lost: 120 us for the levels <= 2048 rows against ~50 us of separate launches, and still +11 us
 // per V-cycle for the levels <= 256 rows (profiles/r01/ab_amg_tail_*.log): one CU cannot hide the
 // dependent gathers that ~4.5 us launches spread over the whole chip.)
+
+// single-precision copy of a coarse level's block values (the V-cycle's sweeps and residuals read
+// it; the Galerkin products, the diagonal inverses and the coarsest solve keep fp64)
+__global__ __launch_bounds__(kB) void k_to_f32(long long n, const double *__restrict__ v,
+                                               float *__restrict__ vf) {
+  for (long long i = blockIdx.x * (long long)kB + threadIdx.x; i < n; i += (long long)gridDim.x * kB)
+    vf[i] = float(v[i]);
+}
 
 // level 0 prolongation: y = x0 + e1[agg0] (x0 null: the cycle without level-0 pre-smoothing,
 // x0 = 0, y = e1[agg0] -- no 17.7-MB memset of x0 per cycle at config 3)
@@ -487,10 +499,22 @@ hipError_t launch_amg_restrict(int nf, int nbn, const int *mptr, const int *mem,
 }
 
 hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const double *v,
-                            const double *x, const double *b, double *r, hipStream_t s) {
+                            const float *vf, const double *x, const double *b, double *r,
+                            hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid<NFc, kLpr>), g1((long long)nb * kLpr), dim3(kB),
-                                         0, s, nb, rp, col, v, x, b, r));
+  if (vf)
+    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid<NFc, kLpr, float>), g1((long long)nb * kLpr),
+                                           dim3(kB), 0, s, nb, rp, col, vf, x, b, r));
+  else
+    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_resid<NFc, kLpr, double>), g1((long long)nb * kLpr),
+                                           dim3(kB), 0, s, nb, rp, col, v, x, b, r));
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_to_f32(long long n, const double *v, float *vf, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const long long g = std::min<long long>((n + kB - 1) / kB, 4096);
+  hipLaunchKernelGGL(k_to_f32, dim3(unsigned(g)), dim3(kB), 0, s, n, v, vf);
   return hipGetLastError();
 }
 
@@ -506,18 +530,22 @@ hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, d
 }
 
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
-                           const int *agg, const double *x, const double *e, const double *b,
-                           const double *dinv, double omega, double *out, hipStream_t s) {
+                           const float *vf, const int *agg, const double *x, const double *e,
+                           const double *b, const double *dinv, double omega, double *out,
+                           hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  if (e)
-    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr, 1>), g1((long long)nb * kLpr),
-                                           dim3(kB), 0, s, nb, rp, col, v, agg, x, e, b, dinv,
-                                           omega, out));
-  else
-    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr, 0>), g1((long long)nb * kLpr),
-                                           dim3(kB), 0, s, nb, rp, col, v, agg, x, e, b, dinv,
-                                           omega, out));
-  return hipGetLastError();
+  auto go = [&](auto corr, auto vt, const auto *vv) -> hipError_t {
+    constexpr int CORR = decltype(corr)::value;
+    using VT = decltype(vt);
+    AMG_NF_DISPATCH(nf, hipLaunchKernelGGL((k_post<NFc, kLpr, CORR, VT>),
+                                           g1((long long)nb * kLpr), dim3(kB), 0, s, nb, rp, col,
+                                           vv, agg, x, e, b, dinv, omega, out));
+    return hipGetLastError();
+  };
+  if (e && vf) return go(std::integral_constant<int, 1>(), float(), vf);
+  if (e) return go(std::integral_constant<int, 1>(), double(), v);
+  if (vf) return go(std::integral_constant<int, 0>(), float(), vf);
+  return go(std::integral_constant<int, 0>(), double(), v);
 }
 
 hipError_t launch_amg_prolong0(int nf, int n, const int *agg, const double *x0, const double *e1,

@@ -293,7 +293,18 @@ struct pnp_ctx {
     DBuf<int> rp, col, dpos, mptr, mem, agg, csrc;
     DBuf<long long> cptr;
     DBuf<double> v, dinv, b, x, x2;
+    DBuf<float> vf;  // single-precision values for the V-cycle's sweeps (amg_f32; null: fp64)
   };
+  // PNP_AMG_F32 (default 1): the coarse levels' sweeps and residuals read single-precision block
+  // values (the arithmetic, the Galerkin products, the diagonal inverses and the coarsest solve
+  // stay fp64), as the ILU(0) factors do; 0 keeps fp64 (A/B)
+  static bool amg_f32() {
+    static const bool v = [] {
+      const char *e = std::getenv("PNP_AMG_F32");
+      return !(e && e[0] == '0');
+    }();
+    return v;
+  }
   std::vector<std::unique_ptr<AmgDev>> amg_d;  // amg_d[k] = level k + 1
   bool amg_built = false, amg_valid = false;
   int amg_nf = 0;
@@ -1718,7 +1729,9 @@ struct pnp_ctx {
       const size_t nb2 = size_t(nf) * nf;
       for (auto &D : amg_d) {
         hipError_t e;
-        if ((e = D->v.alloc(std::max<size_t>(1, D->col.n) * nb2)) != hipSuccess ||
+        if ((amg_f32() && D.get() != amg_d.back().get() &&
+             (e = D->vf.alloc(std::max<size_t>(1, D->col.n) * nb2)) != hipSuccess) ||
+            (e = D->v.alloc(std::max<size_t>(1, D->col.n) * nb2)) != hipSuccess ||
             (e = D->dinv.alloc(size_t(D->nb) * nb2)) != hipSuccess ||
             (e = D->b.alloc(size_t(D->nb) * nf)) != hipSuccess ||
             (e = D->x.alloc(size_t(D->nb) * nf)) != hipSuccess ||
@@ -1752,11 +1765,16 @@ struct pnp_ctx {
     for (int k = 0; k + 1 < K && e == hipSuccess; k++)
       e = pnp::launch_amg_dinv(nf, amg_d[k]->nb, amg_d[k]->dpos.p, amg_d[k]->v.p,
                                amg_d[k]->dinv.p, stream);
+    for (int k = 0; k + 1 < K && e == hipSuccess; k++)
+      if (amg_d[k]->vf.p)
+        e = pnp::launch_amg_to_f32((long long)amg_d[k]->col.n * nf * nf, amg_d[k]->v.p,
+                                   amg_d[k]->vf.p, stream);
     if (e == hipSuccess)
       e = pnp::launch_amg_coarse_dense(nf, amg_d[K - 1]->nb, amg_d[K - 1]->rp.p,
                                        amg_d[K - 1]->col.p, amg_d[K - 1]->v.p, amg_ainv.p, stream);
     if (e != hipSuccess) return hipfail(e, "amg setup");
-    {  // coarsest inverse in place: LU with partial pivoting, then the inverse (column-major)
+    {  // coarsest inverse in place: LU with partial pivoting, then the inverse -- of A^T column-
+       // major, which leaves A^-1 row-major for k_coarse_apply
       if (!blas) {
         if (rocblas_create_handle(&blas) != rocblas_status_success)
           return fail(PNP_E_HIP, "rocblas_create_handle failed");
@@ -1810,13 +1828,14 @@ struct pnp_ctx {
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
       for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more pre-smoothing
-        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, nullptr, C.x.p, nullptr,
-                                 C.b.p, C.dinv.p, om, C.x2.p, stream);
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, nullptr, C.x.p,
+                                 nullptr, C.b.p, C.dinv.p, om, C.x2.p, stream);
         std::swap(C.x.p, C.x2.p);
       }
       // residual of level k+1 into its x2 (free until its post-smoothing), then restriction
       if (e == hipSuccess)
-        e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.x.p, C.b.p, C.x2.p, stream);
+        e = pnp::launch_amg_resid(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, C.x.p, C.b.p,
+                                  C.x2.p, stream);
       if (e == hipSuccess)
         e = pnp::launch_amg_restrict(nf, N.nb, N.mptr.p, N.mem.p, C.x2.p, nullptr, N.b.p,
                                      N.dinv.p, om, k + 2 < K ? N.x.p : nullptr, stream);
@@ -1827,13 +1846,13 @@ struct pnp_ctx {
     const double *res = amg_d[K - 1]->x.p;  // the solution of the level just finished
     for (int k = K - 2; k >= 0 && e == hipSuccess; k--) {
       AmgDev &C = *amg_d[k];
-      e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, amg_d[k + 1]->agg.p, C.x.p, res,
-                               C.b.p, C.dinv.p, om, C.x2.p, stream);
+      e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, amg_d[k + 1]->agg.p,
+                               C.x.p, res, C.b.p, C.dinv.p, om, C.x2.p, stream);
       res = C.x2.p;
       for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more post-smoothing
         double *out = res == C.x2.p ? C.x.p : C.x2.p;
-        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, nullptr, res, nullptr, C.b.p,
-                                 C.dinv.p, om, out, stream);
+        e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, nullptr, res,
+                                 nullptr, C.b.p, C.dinv.p, om, out, stream);
         res = out;
       }
     }

@@ -34,10 +34,12 @@ def interleave(A, nv, nf):
     return A[perm][:, perm].tocsr(), perm
 
 
-def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True):
+def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True, f32=True):
     """The V-cycle of amg.hip restated: Jacobi (pointwise) smoothing on level 0, `sweeps` damped
     block-Jacobi sweeps before and after the correction on the coarse levels, exact solve on the
-    coarsest."""
+    coarsest.  f32 (PNP_AMG_F32, the default): the coarse levels' sweeps and residuals multiply by
+    the block values rounded to single precision; the Galerkin products, the diagonal inverses and
+    the coarsest solve use the fp64 values."""
     As, Ps = [A0], []
     for agg in aggs:
         n = As[-1].shape[0] // nf
@@ -46,6 +48,11 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True):
         Ps.append(Pm)
         As.append((Pm.T @ As[-1] @ Pm).tocsr())
     K = len(aggs)
+    Ad = As  # fp64: Galerkin (above), diagonal inverses, coarsest solve
+    if f32:
+        As = [A if k in (0, K) else sp.csr_matrix(
+            (A.data.astype(np.float32).astype(np.float64), A.indices, A.indptr), shape=A.shape)
+            for k, A in enumerate(Ad)]
 
     def dinv(A):
         nb = A.shape[0] // nf
@@ -58,7 +65,7 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True):
     def bj(A, Di, r):
         return np.einsum("bij,bj->bi", Di, r.reshape(-1, nf)).ravel()
 
-    Dis = [None] + [dinv(As[k]) for k in range(1, K)]
+    Dis = [None] + [dinv(Ad[k]) for k in range(1, K)]
     diag0 = A0.diagonal()
     x0 = d / diag0 if pre0 else np.zeros_like(d)
     b, x = [None] * (K + 1), [None] * (K + 1)
@@ -71,7 +78,7 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True):
         b[k + 1] = Ps[k].T @ (b[k] - As[k] @ x[k])
         if k + 1 < K:
             x[k + 1] = omega * bj(As[k + 1], Dis[k + 1], b[k + 1])
-    e = np.linalg.solve(As[K].toarray(), b[K])
+    e = np.linalg.solve(Ad[K].toarray(), b[K])
     for k in range(K - 1, 0, -1):
         xc = x[k] + Ps[k] @ e
         e = xc + omega * bj(As[k], Dis[k], b[k] - As[k] @ xc)
@@ -121,7 +128,8 @@ def test_amg_vcycle_matches_numpy_restatement(kind, sweeps, pre0):
     assert aggs[0].min() >= 0 and aggs[0].max() + 1 == info["rows"][1]
     Ji, perm = interleave(J, nv, nf)
     vn = np.empty_like(d)
-    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps, bool(pre0))
+    f32 = os.environ.get("PNP_AMG_F32", "1") != "0"
+    vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps, bool(pre0), f32)
     assert np.max(np.abs(v - vn)) <= 1e-10 * np.max(np.abs(vn))
 
 
