@@ -62,6 +62,11 @@ hipError_t launch_amg_resid(int nf, int nb, const int *rp, const int *col, const
 hipError_t launch_amg_to_f32(long long n, const double *v, float *vf, hipStream_t s);
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s);
+// single-precision copy of the row-major inverse, rows padded to ld (a multiple of 4, zeros), and
+// the GEMV on it (PNP_AMG_F32)
+hipError_t launch_amg_inverse_to_f32(int n, int ld, const double *a, float *af, hipStream_t s);
+hipError_t launch_amg_coarse_apply_f32(int n, int ld, const float *ainv, const double *b,
+                                       double *x, hipStream_t s);
 // e == nullptr: a plain damped block-Jacobi sweep (no correction; agg unused); vf as above
 hipError_t launch_amg_post(int nf, int nb, const int *rp, const int *col, const double *v,
                            const float *vf, const int *agg, const double *x, const double *e,

@@ -518,6 +518,60 @@ hipError_t launch_amg_to_f32(long long n, const double *v, float *vf, hipStream_
   return hipGetLastError();
 }
 
+// the same GEMV on a single-precision copy of the inverse (PNP_AMG_F32), rows padded to ld
+// (a multiple of 4) so each lane's 16-B loads carry four columns; fp64 arithmetic, the same
+// accumulator and tree shape
+__global__ __launch_bounds__(64 * kCaWaves) void k_coarse_apply_f32(int n, int ld,
+                                                                   const float *__restrict__ ainv,
+                                                                   const double *__restrict__ b,
+                                                                   double *__restrict__ x) {
+  __shared__ double bs[kAmgMaxDense + 4];
+  for (int j = threadIdx.x; j < ld; j += 64 * kCaWaves) bs[j] = j < n ? b[j] : 0.0;
+  __syncthreads();
+  const int l = threadIdx.x % 64, i = blockIdx.x * kCaWaves + threadIdx.x / 64;
+  if (i >= n) return;
+  const float4 *__restrict__ r4 = reinterpret_cast<const float4 *>(ainv + size_t(i) * ld);
+  const int n4 = ld / 4;
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 4
+  for (int p = l; p < n4; p += 64) {
+    const float4 u = r4[p];
+    s0 = __builtin_fma(double(u.x), bs[4 * p], s0);
+    s1 = __builtin_fma(double(u.y), bs[4 * p + 1], s1);
+    s2 = __builtin_fma(double(u.z), bs[4 * p + 2], s2);
+    s3 = __builtin_fma(double(u.w), bs[4 * p + 3], s3);
+  }
+  double t = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if (l == 0) x[i] = t;
+}
+
+__global__ __launch_bounds__(kB) void k_inverse_to_f32(int n, int ld, const double *__restrict__ a,
+                                                       float *__restrict__ af) {
+  const long long tot = (long long)n * ld;
+  for (long long q = blockIdx.x * (long long)kB + threadIdx.x; q < tot;
+       q += (long long)gridDim.x * kB) {
+    const int i = int(q / ld), j = int(q % ld);
+    af[q] = j < n ? float(a[size_t(i) * n + j]) : 0.0f;
+  }
+}
+
+hipError_t launch_amg_inverse_to_f32(int n, int ld, const double *a, float *af, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const long long g = std::min<long long>(((long long)n * ld + kB - 1) / kB, 8192);
+  hipLaunchKernelGGL(k_inverse_to_f32, dim3(unsigned(g)), dim3(kB), 0, s, n, ld, a, af);
+  return hipGetLastError();
+}
+
+hipError_t launch_amg_coarse_apply_f32(int n, int ld, const float *ainv, const double *b,
+                                       double *x, hipStream_t s) {
+  if (n > kAmgMaxDense || ld % 4 || ld < n || ld > kAmgMaxDense + 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_coarse_apply_f32, dim3((n + kCaWaves - 1) / kCaWaves), dim3(64 * kCaWaves),
+                     0, s, n, ld, ainv, b, x);
+  return hipGetLastError();
+}
+
 hipError_t launch_amg_coarse_apply(int n, const double *ainv, const double *b, double *x,
                                    hipStream_t s) {
   if (n > kAmgMaxDense) return hipErrorInvalidValue;

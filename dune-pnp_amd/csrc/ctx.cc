@@ -296,8 +296,9 @@ struct pnp_ctx {
     DBuf<float> vf;  // single-precision values for the V-cycle's sweeps (amg_f32; null: fp64)
   };
   // PNP_AMG_F32 (default 1): the coarse levels' sweeps and residuals read single-precision block
-  // values (the arithmetic, the Galerkin products, the diagonal inverses and the coarsest solve
-  // stay fp64), as the ILU(0) factors do; 0 keeps fp64 (A/B)
+  // values, and the coarsest solve a single-precision copy of its inverse (the arithmetic, the
+  // Galerkin products, the diagonal inverses and the LU / inverse themselves stay fp64), as the
+  // ILU(0) factors do; 0 keeps fp64 (A/B)
   static bool amg_f32() {
     static const bool v = [] {
       const char *e = std::getenv("PNP_AMG_F32");
@@ -310,6 +311,8 @@ struct pnp_ctx {
   int amg_nf = 0;
   double amg_setup_ms = 0;
   DBuf<double> amg_ainv, amg_x0, amg_t, amg_y, amg_r, amg_z;
+  DBuf<float> amg_ainv_f;  // amg_f32(): the inverse in single precision, rows padded to amg_ld
+  int amg_ld = 0;
   DBuf<int> amg_ipiv, amg_info;
   rocblas_handle blas = nullptr;  // rocSOLVER getrf/getri of the AMG's coarsest level
 
@@ -1740,7 +1743,9 @@ struct pnp_ctx {
       }
       const size_t nc = size_t(amg_d[K - 1]->nb) * nf, nl = size_t(L.n_owned + L.n_ghost) * nf;
       hipError_t e;
-      if ((e = amg_ainv.alloc(nc * nc)) != hipSuccess || (e = amg_ipiv.alloc(nc)) != hipSuccess ||
+      amg_ld = int((nc + 3) & ~size_t(3));
+      if ((amg_f32() && (e = amg_ainv_f.alloc(nc * size_t(amg_ld))) != hipSuccess) ||
+          (e = amg_ainv.alloc(nc * nc)) != hipSuccess || (e = amg_ipiv.alloc(nc)) != hipSuccess ||
           (e = amg_info.alloc(1)) != hipSuccess ||
           (e = amg_x0.alloc(nl)) != hipSuccess || (e = amg_t.alloc(nl)) != hipSuccess ||
           (e = amg_y.alloc(nl)) != hipSuccess || (e = amg_r.alloc(nl)) != hipSuccess ||
@@ -1794,6 +1799,10 @@ struct pnp_ctx {
       if (info != 0)
         return fail(PNP_E_STATE, "AMG: coarsest matrix singular (getrf info " +
                                      std::to_string(info) + ")");
+      if (amg_ainv_f.p &&
+          (e = pnp::launch_amg_inverse_to_f32(nc, amg_ld, amg_ainv.p, amg_ainv_f.p, stream)) !=
+              hipSuccess)
+        return hipfail(e, "amg setup");
     }
     te(T_FACT, t0);
     amg_setup_ms = (now_s() - ts) * 1e3;  // host-side issue time (device time: T_FACT timers)
@@ -1841,7 +1850,10 @@ struct pnp_ctx {
                                      N.dinv.p, om, k + 2 < K ? N.x.p : nullptr, stream);
     }
     if (e == hipSuccess)
-      e = pnp::launch_amg_coarse_apply(amg_d[K - 1]->nb * nf, amg_ainv.p, amg_d[K - 1]->b.p,
+      e = amg_ainv_f.p
+              ? pnp::launch_amg_coarse_apply_f32(amg_d[K - 1]->nb * nf, amg_ld, amg_ainv_f.p,
+                                                 amg_d[K - 1]->b.p, amg_d[K - 1]->x.p, stream)
+              : pnp::launch_amg_coarse_apply(amg_d[K - 1]->nb * nf, amg_ainv.p, amg_d[K - 1]->b.p,
                                        amg_d[K - 1]->x.p, stream);
     const double *res = amg_d[K - 1]->x.p;  // the solution of the level just finished
     for (int k = K - 2; k >= 0 && e == hipSuccess; k--) {

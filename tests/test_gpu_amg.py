@@ -38,8 +38,8 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True, f32=True):
     """The V-cycle of amg.hip restated: Jacobi (pointwise) smoothing on level 0, `sweeps` damped
     block-Jacobi sweeps before and after the correction on the coarse levels, exact solve on the
     coarsest.  f32 (PNP_AMG_F32, the default): the coarse levels' sweeps and residuals multiply by
-    the block values rounded to single precision; the Galerkin products, the diagonal inverses and
-    the coarsest solve use the fp64 values."""
+    the block values rounded to single precision, the coarsest solve by the inverse rounded to
+    single precision; the Galerkin products and the diagonal inverses use the fp64 values."""
     As, Ps = [A0], []
     for agg in aggs:
         n = As[-1].shape[0] // nf
@@ -78,7 +78,10 @@ def numpy_vcycle(A0, nf, aggs, omega, d, sweeps=2, pre0=True, f32=True):
         b[k + 1] = Ps[k].T @ (b[k] - As[k] @ x[k])
         if k + 1 < K:
             x[k + 1] = omega * bj(As[k + 1], Dis[k + 1], b[k + 1])
-    e = np.linalg.solve(Ad[K].toarray(), b[K])
+    if f32:
+        e = np.linalg.inv(Ad[K].toarray()).astype(np.float32).astype(np.float64) @ b[K]
+    else:
+        e = np.linalg.solve(Ad[K].toarray(), b[K])
     for k in range(K - 1, 0, -1):
         xc = x[k] + Ps[k] @ e
         e = xc + omega * bj(As[k], Dis[k], b[k] - As[k] @ xc)
@@ -130,7 +133,10 @@ def test_amg_vcycle_matches_numpy_restatement(kind, sweeps, pre0):
     vn = np.empty_like(d)
     f32 = os.environ.get("PNP_AMG_F32", "1") != "0"
     vn[perm] = numpy_vcycle(Ji, nf, aggs, 0.8, d[perm], sweeps, bool(pre0), f32)
-    assert np.max(np.abs(v - vn)) <= 1e-10 * np.max(np.abs(vn))
+    # f32: the coarsest solve multiplies by the inverse rounded to single precision (the GPU's
+    # rocSOLVER inverse and numpy's differ in the last fp64 bits, so a few entries round to the
+    # neighbouring float): ~1e-8 of the correction, against the 1e-10 of the fp64 cycle
+    assert np.max(np.abs(v - vn)) <= (1e-7 if f32 else 1e-10) * np.max(np.abs(vn))
 
 
 def test_amg_cg_solves_pb_system():
