@@ -91,9 +91,36 @@ int main(int argc, char **argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     return 1e3 * ms / reps;
   };
+  // the same launches captured once into a hipGraph and replayed (per launch inside the replay)
+  auto run_graph = [&](int mode) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < reps; i++) {
+      if (mode == 0)
+        hipLaunchKernelGGL(k_shape<0>, dim3(wgs), dim3(256), 0, st, n, idx, a, b);
+      else
+        hipLaunchKernelGGL(k_shape<2>, dim3(wgs), dim3(256), 0, st, n, idx, a, b);
+    }
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipStreamSynchronize(st));
+    CK(hipEventRecord(e0, st));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    return 1e3 * ms / reps;
+  };
   const char *names[4] = {"empty", "own load+store", "+ dependent gather", "+ barrier + LDS"};
   std::printf("{\"workgroups\": %d, \"threads\": %d, \"reps\": %d", wgs, n, reps);
   for (int m = 0; m < 4; m++) std::printf(", \"%s_us\": %.3f", names[m], run(m));
+  std::printf(", \"graph empty_us\": %.3f, \"graph + dependent gather_us\": %.3f", run_graph(0),
+              run_graph(2));
   std::printf("}\n");
   CK(hipFree(idx));
   CK(hipFree(a));
