@@ -95,6 +95,26 @@ def profile_bicg(config):
     return None
 
 
+ILU_MODEL = os.path.join(ROOT, "profiles", "r05", "ilu", "launch_model.json")
+
+
+def ilu_launch_model():
+    """The committed per-launch model of the ILU(0) application (tools/ilu_launch_model.py: each
+    colour launch's PMC bytes against its trace time, fitted as fixed + bytes / marginal rate,
+    beside the measured floor of a launch of the same shape), or None."""
+    try:
+        with open(ILU_MODEL) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {"fixed_us_per_launch": d["fixed_us_per_launch"], "marginal_gbs": d["marginal_gbs"],
+            "launches_per_apply": len(d["launches"]),
+            "launch_floor_us_800wg": d["launch_floor_us_800wg"],
+            "note": "time = fixed + bytes / marginal over the colour launches; the fixed part is "
+                    "within ~0.8 us of an 800-workgroup kernel's floor with one dependent gather",
+            "source": os.path.relpath(ILU_MODEL, ROOT)}
+
+
 def profile_regime(name):
     """The committed rocprofv3 trace's average for one assembly regime (tools/asm_regimes.py:
     warm / in_situ / cold launches of the config-3 assembly), or None."""
@@ -1009,6 +1029,8 @@ def main():
                                        "blas_per_iter": M["blas"]}, stream_gbs),
                                   "kernels_profile": (profile_bicg(3) if args.scaling == "weak"
                                                       and world == 1 else None),
+                                  "ilu0_launch_model": (ilu_launch_model() if world == 1
+                                                        else None),
                                   "kernels_timing": "event pairs around each unit's launches "
                                                     "(launch gaps included); kernels_profile: "
                                                     "the same pass's device time per unit from "
