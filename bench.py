@@ -204,6 +204,16 @@ def tile_mesh(mesh, n):
     return P.Mesh(xy_all, np.concatenate(tri_out), np.concatenate(bs), np.concatenate(bgs))
 
 
+_T0 = time.perf_counter()
+
+
+def progress(rank, msg):
+    """One line per leg on rank 0's stderr (the JSON line stays alone on stdout), so a long run
+    shows where it is."""
+    if rank == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def barrier_sync(dist, world):
     import torch
     if torch.cuda.is_available():
@@ -802,7 +812,9 @@ def main():
         dist.init_process_group("gloo")
     prec = P.PREC_BY_NAME[args.prec]
 
+    progress(rank, f"N = {world}: stream ceilings")
     stream_gbs = measured_stream_gbs(local)
+    progress(rank, "primary system: mesh, PB Newton, timed assembly and BiCGSTAB")
     cfg, mesh = primary_mesh(args, world)
     ctx, x0, pb_res, t_setup = make_context(mesh, cfg, rank, world, local, dist)
     M = measure(ctx, mesh, args, prec, dist, world)
@@ -810,6 +822,7 @@ def main():
 
     # ---- time to solution (reported beside the metric): PNP Newton from the Boltzmann state ----
     newton = None
+    progress(rank, "time to solution: PNP Newton (ILU(0) f32 / f64, AMG)")
     nt_red = args.newton_reduction or cfg.system["newtonReduction"]
     nt_linred = args.min_linear_reduction or cfg.system["newtonMinLinearReduction"]
     if not args.no_solve:
@@ -865,19 +878,23 @@ def main():
                       "amg_rows": ctx.amg_info()["rows"]}
     ssork = None
     if not args.no_ssork:
+        progress(rank, "BCGS_SSORk (natural-order SSOR)")
         ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters, dist, world)
     ctx.close()
     per_config = None
     if world == 1 and not args.no_per_config:
+        progress(rank, "per-config legs (configs 1, 2, 4)")
         per_config = per_config_legs(prec)
 
     # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
     strong = parity = None
     if args.scaling == "weak" and not args.no_strong:
+        progress(rank, "config 5 (strong scaling)")
         scfg, smesh = strong_mesh(args.strong_refine)
         sctx, sx0, spb, s_setup = make_context(smesh, scfg, rank, world, local, dist)
         S = measure(sctx, smesh, args, prec, dist, world)
         if not args.no_parity:
+            progress(rank, "rccl_parity (partitioned vs one-rank Newton on config 5)")
             parity = rccl_parity(sctx, smesh, scfg, sx0, rank, world, local, dist)
         sctx.close()
         strong = {"workload": f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
@@ -900,6 +917,7 @@ def main():
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the contract: rank 0 at N=1 only
+        progress(rank, "CPU baseline (oracle, 1 and 16 threads)")
         hostcpu = host_cpu_info()
         cb = cpu_baseline(cfg if args.scaling == "weak" else P.read_config(args.cfg),
                           args.cpu_refine, args.cpu_seconds)
