@@ -236,3 +236,19 @@ def test_config4_steps_with_amg_need_no_fallback():
         u, res = ctx.newton(u, reduction=1e-8, abs_limit=1e-9, prec=P.PREC_AMG)
         assert res["converged"] == 1 and res["status"] == 0, (i, res)
         assert res["linear_fallbacks"] == 0
+
+
+def test_amg_fp64_values_vcycle_child():
+    """PNP_AMG_F32=0 (read once per process, so in a child process): the V-cycle with fp64
+    coarse-level values and fp64 coarsest inverse matches the fp64 restatement to 1e-10, for a
+    PNP and a PB cycle."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import conftest; import test_gpu_amg as T; "
+            "T.test_amg_vcycle_matches_numpy_restatement('pnp', 2, 0); "
+            "T.test_amg_vcycle_matches_numpy_restatement('pb', 2, 1); print('CHILD OK')" % here)
+    env = dict(os.environ, PNP_AMG_F32="0")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=here)
+    assert p.returncode == 0 and "CHILD OK" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
