@@ -238,7 +238,11 @@ __device__ __forceinline__ void store_block(double *__restrict__ vc, int lane, i
   // non-temporal: the blocks are read back only by later kernels (SpMV, split), which stream
   // them non-temporally too; plain stores allocate the 207 MB in the caches and evict the
   // gathered x / xy / column indices.  94 -> 77 us at config 3 (profiles/r01/ab_asm_nt_stores.log)
+#ifdef ASM_STORE_PLAIN  // A/B build flag: plain (allocating) block stores
+  store_vals<NK>(vc + size_t(s) * NK * kRows, lane, Kc);
+#else
   store_vals_nt<NK>(vc + size_t(s) * NK * kRows, lane, Kc);
+#endif
 }
 
 // One thread per owned vertex row.  JAC = 0: residual only (Newton line search).
