@@ -1810,6 +1810,16 @@ struct pnp_ctx {
     return PNP_OK;
   }
 
+  // block-Jacobi sweeps on coarse level k + 1 (amg_d[k]): the configured count; PNP_AMG_DEEP_SWEEPS
+  // (A/B, environment) overrides it below level 1, where the kernels sit at the launch floor
+  int amg_sweeps(int k) const {
+    static const int deep = [] {
+      const char *e = std::getenv("PNP_AMG_DEEP_SWEEPS");
+      return e ? std::atoi(e) : 0;
+    }();
+    return (k >= 1 && deep >= 1) ? deep : amg_opts.coarse_sweeps;
+  }
+
   // one V-cycle: vout = B d (owned rows); see amg.hip for the kernels
   int amg_apply(const double *d, double *vout) {
     const int K = int(amg_d.size()), sm = amg_opts.smoother, n = L.n_owned;
@@ -1836,7 +1846,7 @@ struct pnp_ctx {
                                    om, K > 1 ? amg_d[0]->x.p : nullptr, stream);
     for (int k = 0; k + 1 < K && e == hipSuccess; k++) {
       AmgDev &C = *amg_d[k], &N = *amg_d[k + 1];
-      for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more pre-smoothing
+      for (int sw = 1; sw < amg_sweeps(k) && e == hipSuccess; sw++) {  // more pre-smoothing
         e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, nullptr, C.x.p,
                                  nullptr, C.b.p, C.dinv.p, om, C.x2.p, stream);
         std::swap(C.x.p, C.x2.p);
@@ -1861,7 +1871,7 @@ struct pnp_ctx {
       e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, amg_d[k + 1]->agg.p,
                                C.x.p, res, C.b.p, C.dinv.p, om, C.x2.p, stream);
       res = C.x2.p;
-      for (int sw = 1; sw < amg_opts.coarse_sweeps && e == hipSuccess; sw++) {  // more post-smoothing
+      for (int sw = 1; sw < amg_sweeps(k) && e == hipSuccess; sw++) {  // more post-smoothing
         double *out = res == C.x2.p ? C.x.p : C.x2.p;
         e = pnp::launch_amg_post(nf, C.nb, C.rp.p, C.col.p, C.v.p, C.vf.p, nullptr, res,
                                  nullptr, C.b.p, C.dinv.p, om, out, stream);
