@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 5, final: the whole GPU suite and smoke at HEAD
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
+O=gpurun_out/r5fin; mkdir -p $O
+export TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > $O/tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -5 $O/tests.log
+fatal $rc && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -2 $O/smoke.log
+exit $rc
