@@ -358,10 +358,13 @@ def byte_models(info, nf, N_local, T_local, prec):
     spmv = info["nslots"] * (8 * info["nks"] + 4) + 8 * n_loc + 16 * N_local
     # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
     # written, re-read by the backward sweep (gathers counted once), v written
-    vb = 4 * info["nvb"] if info["ilu_f32"] else \
-        8 * info["nvb"]  # bytes per block of the stored factors (float: quads + the remainder)
+    # bytes per block of the stored factors: float (quads + the remainder), bfloat16 (NV rounded
+    # up to 8 shorts: one 16-B record), or double
+    nvb = info["nvb"]
+    vb = {1: 4 * nvb, 2: 2 * (nvb if nvb == 1 else (nvb + 7) // 8 * 8)}.get(info["ilu_f32"],
+                                                                          8 * nvb)
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
-    if info["ilu_f32"] and info["nvb"] == 7:
+    if info["ilu_f32"] == 1 and nvb == 7:
         ilu -= 16 * V  # the forward steps read only the 12-B lower tail of each diagonal block
     pb = pmc_blas_bytes(N_local)
     # the update kernels' counted bytes (PMC); ~24 vector passes (the contract's 192 N) only when
@@ -457,6 +460,7 @@ def measure(ctx, mesh, args, prec, dist, world):
     asm_batch_s = ctx.assemble_state_timed(args.steps) / args.steps
     # BiCGSTAB with fp64 ILU(0) factors (the default stores them in single precision)
     t_bicg64 = None
+    f_default = ctx.get_option(P.OPT_ILU_F32)
     if prec == P.PREC_ILU0:
         ctx.set_option(P.OPT_ILU_F32, 0)
         ctx.bicgstab_iterations(2, prec)
@@ -466,7 +470,7 @@ def measure(ctx, mesh, args, prec, dist, world):
             ctx.bicgstab_iterations(args.bicg_iters, prec)
         barrier_sync(dist, world)
         t_bicg64 = max_over_ranks(dist, world, time.perf_counter() - t0)
-        ctx.set_option(P.OPT_ILU_F32, 1)
+        ctx.set_option(P.OPT_ILU_F32, f_default)
     t_asm, t_bicg = max_over_ranks(dist, world, t_asm), max_over_ranks(dist, world, t_bicg)
 
     nf = 3
@@ -839,11 +843,14 @@ def main():
                   "first_defect": nres["first_defect"], "defect": nres["defect"],
                   "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                   "reduction": nt_red, "min_linear_reduction": nt_linred,
-                  "preconditioner": args.prec + (", f32 factors" if prec == P.PREC_ILU0 else "")}
+                  "preconditioner": args.prec + (
+                      ", " + {1: "f32", 2: "bf16"}.get(ctx.get_option(P.OPT_ILU_F32), "f64") +
+                      " factors" if prec == P.PREC_ILU0 else "")}
     # the same with fp64 ILU(0) factors (the default stores them in single precision): the f32
     # choice's effect on time to solution, linear iterations and seconds side by side
     newton_f64 = None
     if not args.no_solve and prec == P.PREC_ILU0:
+        f_default = ctx.get_option(P.OPT_ILU_F32)
         ctx.set_option(P.OPT_ILU_F32, 0)
         barrier_sync(dist, world)
         t0 = time.perf_counter()
@@ -855,7 +862,7 @@ def main():
                       "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
                       "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                       "preconditioner": "ilu0, fp64 factors"}
-        ctx.set_option(P.OPT_ILU_F32, 1)
+        ctx.set_option(P.OPT_ILU_F32, f_default)
     # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB
     newton_amg = None
     if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
@@ -1032,7 +1039,8 @@ def main():
                                   "frac": M["it_stored"]["frac"],
                                   "byte_model": "stored formats (k-form SELL + 4-B index per "
                                                 "slot, split ILU(0) factors, vectors)",
-                                  "ilu_factor_precision": "f32" if info["ilu_f32"] else "f64",
+                                  "ilu_factor_precision": {0: "f64", 1: "f32", 2: "bf16"}.get(
+                                      info["ilu_f32"], "f32"),
                                   "contract_bytes_per_iter": M["it_contract"]["bytes"],
                                   "contract_model_gbs": M["it_contract"]["achieved"],
                                   "contract_model_ratio": M["it_contract"]["frac"],

@@ -151,11 +151,18 @@ struct pnp_ctx {
   // sweeps compute in fp64, the matrix, SpMV, SSOR and every vector stay fp64).  Measured at
   // config 3: ILU(0) apply 119 -> 95 us, BiCGSTAB 428 -> 389 us/it, Newton 9,295 -> 9,177
   // iterations (profiles/r02/ab_ilu_f32.log)
+  // 2 (the default since round 5): bfloat16 factors for block systems (linalg.hip bf16s: 16 B per
+  // PNP block instead of 28; ILU(0) apply 66.3 -> 58.6 us, BiCGSTAB 0.285 -> 0.270 ms per
+  // iteration at config 3, Newton counts inside their last-bit spread); scalar
+  // systems (PB, Poisson, diffusion: one value per block, 2 B saved per slot) keep f32, where the
+  // PB Newton at config 1 took 13 % more iterations with bf16
   int ilu_f32 = [] {
     const char *e = std::getenv("PNP_ILU_F32");
-    return (e && std::atoi(e) == 0) ? 0 : 1;
+    const int v = e ? std::atoi(e) : 2;
+    return (v == 0 || v == 1) ? v : 2;
   }();
-  int f32_now() const { return split_of == 2 ? ilu_f32 : 0; }
+  int ilu_eff() const { return (ilu_f32 == 2 && nf == 1) ? 1 : ilu_f32; }
+  int f32_now() const { return split_of == 2 ? ilu_eff() : 0; }
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
   int amg_fallback = 0;  // PNP_OPT_AMG_FALLBACK
   int twored_opt = [] {  // PNP_OPT_BICG_TWORED: -1 auto (on with more than one rank), 0, 1
@@ -1663,7 +1670,7 @@ struct pnp_ctx {
     hipError_t e;
     if (ilu_fused) {
       e = pnp::launch_ilu0_factor_fused(dl, L.color_ptr.data(), nf, pat, vals.p, d_rowoff.p,
-                                        d_rowcol.p, lu.p, lvals.p, uvals.p, ilu_f32, stream);
+                                        d_rowcol.p, lu.p, lvals.p, uvals.p, ilu_eff(), stream);
     } else {
       e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
       if (e == hipSuccess)
@@ -1686,7 +1693,7 @@ struct pnp_ctx {
     hipEvent_t t0 = tb(T_FACT);
     hipError_t e = pnp::launch_split(dl, nf, pat, which == 1 ? 1 : 0, which == 2 ? lu.p : vals.p,
                                      d_lsrc.p, (long long)d_lsrc.n, d_usrc.p, (long long)d_usrc.n,
-                                     lvals.p, uvals.p, stream, which == 2 ? ilu_f32 : 0);
+                                     lvals.p, uvals.p, stream, which == 2 ? ilu_eff() : 0);
     if (e != hipSuccess) return hipfail(e, "split");
     te(T_FACT, t0);
     split_of = which;
@@ -3761,7 +3768,7 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     return PNP_OK;
   }
   if (option == PNP_OPT_ILU_F32) {
-    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0 or 1");
+    if (value < 0 || value > 2) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0, 1 or 2");
     if (c->ilu_f32 != int(value)) {
       c->ilu_f32 = int(value);
       if (c->split_of == 2) c->split_of = 0;  // re-split the factors in the new precision

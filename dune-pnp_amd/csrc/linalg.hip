@@ -437,10 +437,48 @@ __device__ __forceinline__ void load_f32_slot(const float *__restrict__ sb, int 
       B[fperm(NV, 4 * NQ + i)] = T(NT ? __builtin_nontemporal_load(pr + i) : pr[i]);
   }
 }
+// bfloat16 factor storage (PNP_OPT_ILU_F32 = 2): the f32 factors rounded to 8 significant bits
+// (nearest even), fp64 arithmetic as before.  Slots of NV > 1 values hold NV rounded up to 8
+// shorts per lane, so one dwordx4 per lane moves a PNP block (16 B instead of 28): value q of
+// lane l at (q >> 3) * 8 * kRows + 8 l + (q & 7); NV == 1 is row-contiguous (2 B per row).
+// Measured first with f32 storage rounded to 8 / 11 bits (ILU_ROUND_BITS): the config-3 PNP
+// Newton's BiCGSTAB count stays inside its last-bit spread.
+typedef unsigned short bf16s;
+__host__ __device__ constexpr int nvp_b(int nv) { return nv == 1 ? 1 : ((nv + 7) & ~7); }
+__host__ __device__ constexpr int vinb(int nv, int q, int lane) {
+  return nv == 1 ? lane : (q >> 3) * 8 * kRows + 8 * lane + (q & 7);
+}
+__device__ __forceinline__ bf16s to_bf16(float x) {
+  unsigned u = __float_as_uint(x);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return bf16s(u >> 16);
+}
+__device__ __forceinline__ float from_bf16(unsigned h) { return __uint_as_float(h << 16); }
+template <int NV, int NT, typename T = double>
+__device__ __forceinline__ void load_bf16_slot(const bf16s *__restrict__ sb, int lane, T *B) {
+  if constexpr (NV == 1) {
+    B[0] = T(from_bf16(NT ? __builtin_nontemporal_load(sb + lane) : sb[lane]));
+  } else {
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int k = 0; k < (NV + 7) / 8; k++) {
+      const u4v *pp = reinterpret_cast<const u4v *>(sb + k * 8 * kRows) + lane;
+      const u4v t = NT ? __builtin_nontemporal_load(pp) : *pp;
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (8 * k + i < NV) B[8 * k + i] = T(from_bf16((i & 1) ? (t[i >> 1] >> 16) : (t[i >> 1] & 0xFFFFu)));
+    }
+  }
+}
+
 template <int NV, typename VT>
 __host__ __device__ constexpr int slot_vals() {
-  return std::is_same<VT, float>::value ? nvp_f<NV>() : NV;
+  return std::is_same<VT, float>::value ? nvp_f<NV>()
+                                        : (std::is_same<VT, bf16s>::value ? nvp_b(NV) : NV);
 }
+// the value type a slot's values are kept in between their load and their use
+template <typename VT>
+using slot_keep_t = typename std::conditional<std::is_same<VT, bf16s>::value, float, VT>::type;
 
 template <int NV, int NT, typename VT, int LOWER = 0>
 __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int lane, double *B) {
@@ -449,6 +487,8 @@ __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int l
       load_vals_nt<NV>(sb, lane, B);
     else
       load_vals<NV>(sb, lane, B);
+  } else if constexpr (std::is_same<VT, bf16s>::value) {
+    load_bf16_slot<NV, NT, double>(sb, lane, B);
   } else if constexpr (NV == 1) {
     B[0] = NT ? __builtin_nontemporal_load(sb + lane) : sb[lane];
   } else {
@@ -724,6 +764,21 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(DevLayout L, int r0, int
 // KMAX > 0: the row's own blocks live in LDS during the elimination (KMAX >= the fan length +
 // 1 of every row) and reach the scratch once, when they are final: the per-row working set of a
 // wave does not fit the L2 otherwise, and every update of an own block was a write-back.
+// A/B build flag ILU_ROUND_BITS = b: the single-precision factors rounded to b significant bits
+// (11: half precision, 8: bfloat16) in f32 storage and range -- what a 16-bit factor format would
+// cost in preconditioner quality, measured before building one
+__device__ __forceinline__ float ilu_round(float x) {
+#ifdef ILU_ROUND_BITS
+  constexpr int drop = 24 - ILU_ROUND_BITS;
+  unsigned u = __float_as_uint(x);
+  u += (1u << (drop - 1)) - 1u + ((u >> drop) & 1u);
+  u &= ~((1u << drop) - 1u);
+  return __uint_as_float(u);
+#else
+  return x;
+#endif
+}
+
 template <int NF, int PAT, typename VT, int KMAX, int TB>
 __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, int r1,
                                                           const double *__restrict__ kvals,
@@ -878,9 +933,12 @@ __global__ __launch_bounds__(TB) void k_ilu0_factor_fused(DevLayout L, int r0, i
     if constexpr (std::is_same<VT, double>::value) {
 #pragma unroll
       for (int q = 0; q < NV; q++) sb[vin(NV, q, ln)] = B[q];
+    } else if constexpr (std::is_same<VT, bf16s>::value) {
+#pragma unroll
+      for (int q = 0; q < NS; q++) sb[vinb(NV, q, ln)] = q < NV ? to_bf16(float(B[q])) : bf16s(0);
     } else {
 #pragma unroll
-      for (int q = 0; q < NS; q++) sb[vinf(NV, q, ln)] = q < NV ? float(B[q]) : 0.0f;
+      for (int q = 0; q < NS; q++) sb[vinf(NV, q, ln)] = q < NV ? ilu_round(float(B[q])) : 0.0f;
     }
   };
   const int loff = L.lchunk_off[ci], uoff = L.uchunk_off[ci];
@@ -1014,7 +1072,8 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   // a batch's list positions and factor values (kept as stored, float or double, until used) do
   // not depend on the staging: the first batch is in flight with it
   int li[B];
-  VT ar[B][NS];
+  using KT = slot_keep_t<VT>;
+  KT ar[B][NS];
   auto fetch = [&](int sb) {
 #pragma unroll
     for (int b = 0; b < B; b++) {
@@ -1023,9 +1082,11 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
       const VT *sbp = R.vc + size_t(s) * NS * kRows;
       if (s >= R.len) {
 #pragma unroll
-        for (int qq = 0; qq < NS; qq++) ar[b][qq] = VT(0);
+        for (int qq = 0; qq < NS; qq++) ar[b][qq] = KT(0);
       } else if constexpr (std::is_same<VT, double>::value) {
         load_split_vals<NV, NT>(sbp, R.lane, ar[b]);
+      } else if constexpr (std::is_same<VT, bf16s>::value) {
+        load_bf16_slot<NV, NT, float>(sbp, R.lane, ar[b]);
       } else if constexpr (NV == 1) {
         ar[b][0] = NT ? __builtin_nontemporal_load(sbp + R.lane) : sbp[R.lane];
       } else {
@@ -1219,7 +1280,8 @@ __device__ __forceinline__ void ilu_flow_unit(const DevLayout &L, const IluFlow 
       (FWD ? L.lsx_idx + L.lchunk_off[chunk] : L.usx_idx + L.uchunk_off[chunk]) + R.lane;
   const int s0 = FWD ? 0 : 1;
   int li[B];
-  VT ar[B][NS];
+  using KT = slot_keep_t<VT>;
+  KT ar[B][NS];
   auto fetch = [&](int sb) {
 #pragma unroll
     for (int b = 0; b < B; b++) {
@@ -1228,9 +1290,11 @@ __device__ __forceinline__ void ilu_flow_unit(const DevLayout &L, const IluFlow 
       const VT *sbp = R.vc + size_t(s) * NS * kRows;
       if (s >= R.len) {
 #pragma unroll
-        for (int qq = 0; qq < NS; qq++) ar[b][qq] = VT(0);
+        for (int qq = 0; qq < NS; qq++) ar[b][qq] = KT(0);
       } else if constexpr (std::is_same<VT, double>::value) {
         load_split_vals<NV, 0>(sbp, R.lane, ar[b]);
+      } else if constexpr (std::is_same<VT, bf16s>::value) {
+        load_bf16_slot<NV, 0, float>(sbp, R.lane, ar[b]);
       } else if constexpr (NV == 1) {
         ar[b][0] = sbp[R.lane];
       } else {
@@ -1391,6 +1455,9 @@ __global__ __launch_bounds__(kBlock) void k_split(DevLayout L, const double *__r
   if constexpr (std::is_same<VT, double>::value) {
 #pragma unroll
     for (int q = 0; q < NV; q++) sb[vin(NV, q, lane)] = B[q];
+  } else if constexpr (std::is_same<VT, bf16s>::value) {
+#pragma unroll
+    for (int q = 0; q < NS; q++) sb[vinb(NV, q, lane)] = q < NV ? to_bf16(float(B[q])) : bf16s(0);
   } else {
 #pragma unroll
     for (int q = 0; q < NS; q++) sb[vinf(NV, q, lane)] = q < NV ? float(B[q]) : 0.0f;
@@ -2073,7 +2140,7 @@ hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *cp, int nf, i
     });
     return hipGetLastError();
   };
-  return f32 ? run(float()) : run(double());
+  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
 }
 
 // LDS-staged sweeps when the layout carries their lists and the sweep shape is the default one
@@ -2154,7 +2221,7 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
       });
       return hipGetLastError();
     };
-    return f32 ? run(float()) : run(double());
+    return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
   }
   auto run = [&](auto vt) -> hipError_t {
     using VT = decltype(vt);
@@ -2180,7 +2247,7 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     }));
     return hipGetLastError();
   };
-  return f32 ? run(float()) : run(double());
+  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
 }
 
 // every workgroup of a grid resident at once: CUs x the occupancy at this LDS size (capped by n)
@@ -2217,7 +2284,7 @@ hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pa
     });
     return hipGetLastError();
   };
-  return f32 ? run(float()) : run(double());
+  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
 }
 
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
@@ -2242,7 +2309,7 @@ hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, c
     });
     return hipGetLastError();
   };
-  return f32 ? run(float()) : run(double());
+  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
 }
 
 hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,
@@ -2255,6 +2322,9 @@ hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const d
     if (from_k)
       hipLaunchKernelGGL((k_split<NFc, PATc, 1>), g, dim3(kBlock), 0, s, L, src, lsrc, ln, usrc,
                          un, static_cast<double *>(lv), static_cast<double *>(uv));
+    else if (f32 == 2)
+      hipLaunchKernelGGL((k_split<NFc, PATc, 0, bf16s>), g, dim3(kBlock), 0, s, L, src, lsrc, ln,
+                         usrc, un, static_cast<bf16s *>(lv), static_cast<bf16s *>(uv));
     else if (f32)
       hipLaunchKernelGGL((k_split<NFc, PATc, 0, float>), g, dim3(kBlock), 0, s, L, src, lsrc, ln,
                          usrc, un, static_cast<float *>(lv), static_cast<float *>(uv));

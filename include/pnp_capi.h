@@ -354,12 +354,14 @@ int pnp_amg_aggregates(pnp_ctx *ctx, int32_t level, int32_t *agg);
 
 /* ---- context options ------------------------------------------------------------------------ */
 enum {
-  /* 1 (default): the ILU(0) factors (PNP_PREC_ILU0 and the AMG's ILU(0) smoother) are stored in
-   * single precision; the sweeps read them as float and compute in fp64.  The matrix, the SpMV,
-   * SSOR/Jacobi and every vector stay fp64, so the operator and the converged solutions are those
-   * of the fp64 path; only the preconditioner is a rounded ILU(0) (config 3: apply 119 -> 95 us,
-   * Newton BiCGSTAB iterations 9,295 -> 9,177).  0: fp64 factors (the environment variable
-   * PNP_ILU_F32=0 sets the default to 0). */
+  /* Storage precision of the ILU(0) factors (PNP_PREC_ILU0 and the AMG's ILU(0) smoother); the
+   * sweeps compute in fp64 whatever it is.  The matrix, the SpMV, SSOR/Jacobi and every vector stay
+   * fp64, so the operator and the converged solutions are those of the fp64 path; only the
+   * preconditioner is a rounded ILU(0).  2 (default): bfloat16 factors for block systems (8
+   * significant bits, 16 B per PNP block instead of 28; config 3: apply 66 -> 59 us, Newton counts
+   * within their last-bit spread), single precision for scalar ones (PB, Poisson, diffusion);
+   * 1: single precision (apply 119 -> 95 us against fp64 in round 2, Newton 9,295 -> 9,177
+   * iterations); 0: fp64.  The environment variable PNP_ILU_F32 = 0 / 1 / 2 sets the default. */
   PNP_OPT_ILU_F32 = 1,
   /* 1 (default): ILU(0) factorisation in one launch per colour with the k-form expansion and the
    * split into L / U storage folded in; 0: the three-pass path (expand, factor, split).  Both
