@@ -110,8 +110,9 @@ def ilu_launch_model():
     return {"fixed_us_per_launch": d["fixed_us_per_launch"], "marginal_gbs": d["marginal_gbs"],
             "launches_per_apply": len(d["launches"]),
             "launch_floor_us_800wg": d["launch_floor_us_800wg"],
-            "note": "time = fixed + bytes / marginal over the colour launches; the fixed part is "
-                    "within ~0.8 us of an 800-workgroup kernel's floor with one dependent gather",
+            "note": "time = fixed + bytes / marginal over the colour launches (PMC bytes against "
+                    "trace times); launch_floor: an 800-workgroup kernel of the same shape, empty "
+                    "/ with its own load and store / plus one dependent gather",
             "source": os.path.relpath(ILU_MODEL, ROOT)}
 
 
