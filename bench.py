@@ -360,12 +360,14 @@ def byte_models(info, nf, N_local, T_local, prec):
     # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
     # written, re-read by the backward sweep (gathers counted once), v written
     # bytes per block of the stored factors: float (quads + the remainder), bfloat16 (NV rounded
-    # up to 8 shorts: one 16-B record), or double
+    # up to 8 shorts: one 16-B record), or double; mode 3: bfloat16 factors and a 4-B forward
+    # intermediate (scalar systems run 2 and 3 as 1)
     nvb = info["nvb"]
-    vb = {1: 4 * nvb, 2: 2 * (nvb if nvb == 1 else (nvb + 7) // 8 * 8)}.get(info["ilu_f32"],
-                                                                          8 * nvb)
-    ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * (N_local + 3 * n_loc)
-    if info["ilu_f32"] == 1 and nvb == 7:
+    mode = info["ilu_f32"] if nvb > 1 or info["ilu_f32"] < 2 else 1
+    vb = {1: 4 * nvb, 2: 2 * (nvb if nvb == 1 else (nvb + 7) // 8 * 8)}.get(min(mode, 2), 8 * nvb)
+    yb = 4 if mode == 3 else 8
+    ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * N_local + (2 * yb + 8) * n_loc
+    if mode == 1 and nvb == 7:
         ilu -= 16 * V  # the forward steps read only the 12-B lower tail of each diagonal block
     pb = pmc_blas_bytes(N_local)
     # the update kernels' counted bytes (PMC); ~24 vector passes (the contract's 192 N) only when
@@ -845,8 +847,10 @@ def main():
                   "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
                   "reduction": nt_red, "min_linear_reduction": nt_linred,
                   "preconditioner": args.prec + (
-                      ", " + {1: "f32", 2: "bf16"}.get(ctx.get_option(P.OPT_ILU_F32), "f64") +
-                      " factors" if prec == P.PREC_ILU0 else "")}
+                      ", " + {1: "f32 factors", 2: "bf16 factors",
+                              3: "bf16 factors, f32 intermediate"}.get(
+                          ctx.get_option(P.OPT_ILU_F32), "f64 factors")
+                      if prec == P.PREC_ILU0 else "")}
     # the same with fp64 ILU(0) factors (the default stores them in single precision): the f32
     # choice's effect on time to solution, linear iterations and seconds side by side
     newton_f64 = None
@@ -1040,8 +1044,10 @@ def main():
                                   "frac": M["it_stored"]["frac"],
                                   "byte_model": "stored formats (k-form SELL + 4-B index per "
                                                 "slot, split ILU(0) factors, vectors)",
-                                  "ilu_factor_precision": {0: "f64", 1: "f32", 2: "bf16"}.get(
-                                      info["ilu_f32"], "f32"),
+                                  "ilu_factor_precision": {0: "f64", 1: "f32", 2: "bf16",
+                                                           3: "bf16"}.get(info["ilu_f32"], "f32"),
+                                  "ilu_intermediate_precision": "f32" if info["ilu_f32"] == 3
+                                                                else "f64",
                                   "contract_bytes_per_iter": M["it_contract"]["bytes"],
                                   "contract_model_gbs": M["it_contract"]["achieved"],
                                   "contract_model_ratio": M["it_contract"]["frac"],

@@ -156,13 +156,24 @@ struct pnp_ctx {
   // iteration at config 3, Newton counts inside their last-bit spread); scalar
   // systems (PB, Poisson, diffusion: one value per block, 2 B saved per slot) keep f32, where the
   // PB Newton at config 1 took 13 % more iterations with bf16
+  // 3 (the default): the bf16 factors of 2, and the forward sweep's intermediate y = L^-1 d kept in
+  // single precision (ilu_y32: 12 B per PNP row written, re-read by the backward sweep and gathered
+  // by the forward one, instead of 24).  The dataflow form (PNP_OPT_ILU_FLOW)
+  // keeps y in fp64, so with it on 3 runs as 2
   int ilu_f32 = [] {
     const char *e = std::getenv("PNP_ILU_F32");
-    const int v = e ? std::atoi(e) : 2;
-    return (v == 0 || v == 1) ? v : 2;
+    const int v = e ? std::atoi(e) : 3;
+    return (v >= 0 && v <= 2) ? v : 3;
   }();
-  int ilu_eff() const { return (ilu_f32 == 2 && nf == 1) ? 1 : ilu_f32; }
-  int f32_now() const { return split_of == 2 ? ilu_eff() : 0; }
+  int ilu_eff() const { return (ilu_f32 >= 2 && nf == 1) ? 1 : ilu_f32; }
+  // the factors' storage: 0 fp64, 1 f32, 2 bf16 (the kernels' f32 argument)
+  int ilu_fac() const { return ilu_eff() == 3 ? 2 : ilu_eff(); }
+  int f32_now() const { return split_of == 2 ? ilu_fac() : 0; }
+  // the single-precision forward intermediate of the colour launches, or null
+  DBuf<float> ilu_y32buf;
+  float *ilu_y32() const {
+    return (split_of == 2 && ilu_eff() == 3 && !ilu_flow_opt) ? ilu_y32buf.p : nullptr;
+  }
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
   int amg_fallback = 0;  // PNP_OPT_AMG_FALLBACK
   int twored_opt = [] {  // PNP_OPT_BICG_TWORED: -1 auto (on with more than one rank), 0, 1
@@ -1350,7 +1361,8 @@ struct pnp_ctx {
       }
     }
     hipError_t e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d,
-                                          vout, stream, c_first, nullptr, nullptr, f32_now());
+                                          vout, stream, c_first, nullptr, nullptr, f32_now(),
+                                          ilu_y32());
     return e == hipSuccess ? PNP_OK : hipfail(e, what);
   }
   // a dataflow application that timed out (never expected) leaves void results and a sticky word
@@ -1670,7 +1682,7 @@ struct pnp_ctx {
     hipError_t e;
     if (ilu_fused) {
       e = pnp::launch_ilu0_factor_fused(dl, L.color_ptr.data(), nf, pat, vals.p, d_rowoff.p,
-                                        d_rowcol.p, lu.p, lvals.p, uvals.p, ilu_eff(), stream);
+                                        d_rowcol.p, lu.p, lvals.p, uvals.p, ilu_fac(), stream);
     } else {
       e = pnp::launch_expand(dl, nf, pat, vals.p, lu.p, stream);
       if (e == hipSuccess)
@@ -1693,7 +1705,7 @@ struct pnp_ctx {
     hipEvent_t t0 = tb(T_FACT);
     hipError_t e = pnp::launch_split(dl, nf, pat, which == 1 ? 1 : 0, which == 2 ? lu.p : vals.p,
                                      d_lsrc.p, (long long)d_lsrc.n, d_usrc.p, (long long)d_usrc.n,
-                                     lvals.p, uvals.p, stream, which == 2 ? ilu_eff() : 0);
+                                     lvals.p, uvals.p, stream, which == 2 ? ilu_fac() : 0);
     if (e != hipSuccess) return hipfail(e, "split");
     te(T_FACT, t0);
     split_of = which;
@@ -1894,7 +1906,7 @@ struct pnp_ctx {
     if (e != hipSuccess) return hipfail(e, "amg v-cycle");
     if (sm == PNP_PREC_ILU0) {  // vout = y + M^-1 r, written by the backward sweep
       e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, amg_r.p,
-                                 amg_z.p, stream, 0, amg_y.p, vout, f32_now());
+                                 amg_z.p, stream, 0, amg_y.p, vout, f32_now(), ilu_y32());
       return e == hipSuccess ? PNP_OK : hipfail(e, "amg v-cycle");
     }
     if ((rc = smoother(sm, amg_r.p, amg_z.p))) return rc;
@@ -2021,7 +2033,7 @@ struct pnp_ctx {
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 0, k == 0 ? 1 : 0, nullptr, nullptr,
                                     rs.p, v.p, p.p, uvals.p, y.p, nullptr, nullptr, stream,
-                                    f32_now());
+                                    f32_now(), nullptr, ilu_y32());
       else
         e = pnp::launch_update_p(n, S.p, rs.p, v.p, p.p, k == 0 ? 1 : 0, stream);
       if (e != hipSuccess) return hipfail(e, "update_p");
@@ -2049,7 +2061,7 @@ struct pnp_ctx {
       if (fuse)
         e = pnp::launch_update_fwd0(dl, nf, pat, c0_end, S.p, 1, 0, xdefer ? nullptr : zout, yin,
                                     rs.p, v.p, nullptr, uvals.p, y2p, partials2.p, &npu, stream,
-                                    f32_now(), twored ? rt.p : nullptr);
+                                    f32_now(), twored ? rt.p : nullptr, ilu_y32());
       else
         e = pnp::launch_update_xr(n, S.p, 0, zout, yin, rs.p, v.p, twored ? rt.p : nullptr,
                                   partials2.p, stream);
@@ -2111,7 +2123,7 @@ struct pnp_ctx {
       // failure turns graphs off for the rest of the solve (eager launches, same results)
       const int glen = std::min(check, 16);
       while (graphs && glen > 1 && kend - k >= glen) {
-        const GraphKey key{glen, prec, fuse ? 1 : 0, nf, pat, f32_now(),
+        const GraphKey key{glen, prec, fuse ? 1 : 0, nf, pat, f32_now() + (ilu_y32() ? 4 : 0),
                            ilu_flow_opt * 4 + (nat_flow_opt + 1), zout, dl.dmask, graph_epoch};
         bool captured = true;
         rc = graph_run(key, [&]() -> int {
@@ -3198,7 +3210,8 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
       (rc = al(c->fluxred, 2 * 256, "flux reduce")) || (rc = al(c->x, nv3, "x")) ||
       (rc = al(c->r, nv3, "r")) || (rc = al(c->rs, nv3, "rs")) || (rc = al(c->z, nv3, "z")) || (rc = al(c->rt, nv3, "rt")) ||
       (rc = al(c->p, nv3, "p")) || (rc = al(c->v, nv3, "v")) || (rc = al(c->t, nv3, "t")) ||
-      (rc = al(c->y, nv3, "y")) || (rc = al(c->y2, nv3, "y2")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
+      (rc = al(c->y, nv3, "y")) || (rc = al(c->y2, nv3, "y2")) ||
+      (rc = al(c->ilu_y32buf, nv3, "ILU(0) intermediate")) || (rc = al(c->b, nv3, "b")) || (rc = al(c->prevu, nv3, "prevu")) ||
       (rc = al(c->ext, 3 * size_t(c->mesh.nv), "ext")) ||
       (rc = al(c->sendbuf, 3 * std::max<size_t>(1, L.send_idx.size()), "sendbuf")) ||
       // up to 3 partials per workgroup (SpMV mode 4) / 2 (updates with <rt, s>)
@@ -3340,7 +3353,7 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->ilu_flow_applies = c->ilu_flow_n;
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
-                        c->y2.n + c->b.n + c->prevu.n + c->ext.n) * 8;
+                        c->y2.n + c->b.n + c->prevu.n + c->ext.n) * 8 + c->ilu_y32buf.n * 4;
   b += c->d_colidx.n * 4 + c->d_rowmeta.n * 8 + c->d_xy.n * 8;
   info->device_bytes = int64_t(b);
   return PNP_OK;
@@ -3768,7 +3781,7 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     return PNP_OK;
   }
   if (option == PNP_OPT_ILU_F32) {
-    if (value < 0 || value > 2) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0, 1 or 2");
+    if (value < 0 || value > 3) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_F32 takes 0 .. 3");
     if (c->ilu_f32 != int(value)) {
       c->ilu_f32 = int(value);
       if (c->split_of == 2) c->split_of = 0;  // re-split the factors in the new precision

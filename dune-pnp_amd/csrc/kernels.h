@@ -60,6 +60,20 @@ __device__ __forceinline__ void store_nf(double *__restrict__ x, size_t j, const
   }
   if (f < NF) b[f] = v[f];
 }
+// the ILU(0) forward sweep's single-precision intermediate (PNP_OPT_ILU_F32 = 3): rounded to
+// nearest on the store, widened exactly on the load
+template <int NF>
+__device__ __forceinline__ void load_nf(const float *__restrict__ x, size_t j, double (&o)[NF]) {
+  const float *b = x + size_t(NF) * j;
+#pragma unroll
+  for (int f = 0; f < NF; f++) o[f] = double(b[f]);
+}
+template <int NF>
+__device__ __forceinline__ void store_nf(float *__restrict__ x, size_t j, const double (&v)[NF]) {
+  float *b = x + size_t(NF) * j;
+#pragma unroll
+  for (int f = 0; f < NF; f++) b[f] = float(v[f]);
+}
 
 // ---- SELL value layout --------------------------------------------------------------------------
 // Slot s of chunk c holds NV values for each of the chunk's 64 rows, at doubles
@@ -341,11 +355,14 @@ hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *color_ptr_hos
                                     const double *kvals, const int *rowoff, const int *rowcol,
                                     double *aos, void *lv, void *uv, int f32, hipStream_t s);
 // c_first = 1: colour 0's forward step was already applied (launch_update_fwd0); add != null:
-// also out = add + v (written row by row as the backward sweep finishes them)
+// also out = add + v (written row by row as the backward sweep finishes them).  yf != null (bf16
+// factors only, f32 = 2): the forward sweep's intermediate y = L^-1 d is stored in single precision
+// there (colour 0's by launch_update_fwd0 when c_first = 1) instead of in v, and the forward
+// gathers and the backward sweep's own rows read it from there
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                              const void *lv, const void *uv, const double *d, double *v,
                              hipStream_t s, int c_first = 0, const double *add = nullptr,
-                             double *out = nullptr, int f32 = 0);
+                             double *out = nullptr, int f32 = 0, float *yf = nullptr);
 // The same application as ONE dataflow launch (k_ilu0_flow, PNP_ILU_FLOW): the colour launches'
 // 256-row blocks become units in the launches' order (forward colours c_first .. nc-2, the last
 // colour, backward colours nc-2 .. 0); a workgroup takes the next unit by an atomic ticket, waits
@@ -372,12 +389,13 @@ hipError_t launch_ilu0_flow(const DevLayout &L, const IluFlow &F, int nf, int pa
 // BiCGSTAB update fused with colour 0 of the ILU(0) forward sweep (rows [0, c0_end)): which 0:
 // p = r + beta (p - omega v) (first: p = r), yout = Ld^-1 p on colour 0; which 1: x += alpha yin,
 // r -= alpha v, partials ||r||^2 (one per workgroup, *nparts), yout = Ld^-1 r on colour 0.
-// which 1 with x = null: x += alpha yin is left to launch_update_xr(.., y1 = yin) (S->xpend)
+// which 1 with x = null: x += alpha yin is left to launch_update_xr(.., y1 = yin) (S->xpend).
+// youtf != null (bf16 factors, launch_ilu0_apply's yf): colour 0's y goes there, not to yout
 hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, const Scalars *S,
                               int which, int first, double *x, const double *yin, double *r,
                               const double *v, double *p, const void *uv, double *yout,
                               double *partials, int *nparts, hipStream_t s, int f32 = 0,
-                              const double *rt = nullptr);
+                              const double *rt = nullptr, float *youtf = nullptr);
 
 // BLAS-1 over n = n_owned*nf entries
 int blas_nparts(long long n);

@@ -534,9 +534,9 @@ __device__ __forceinline__ SplitRow<VT> split_row(const DevLayout &L, const VT *
 // lanes, slots interleaved), partial sums combined across the row's lanes.  A colour holds ~1/6
 // of the rows (~2 waves per SIMD at config 3), so latency is hidden inside the thread: the
 // column indices of B slots are loaded together, then their gathers and values together.
-template <int NF, int PAT, int LPR, int B, int NT = 0, typename VT = double>
+template <int NF, int PAT, int LPR, int B, int NT = 0, typename VT = double, typename XT = double>
 __device__ __forceinline__ void split_row_dot(const SplitRow<VT> &R, int s0, int q, int row,
-                                              const double *__restrict__ v, double (&acc)[NF]) {
+                                              const XT *__restrict__ v, double (&acc)[NF]) {
   constexpr int NV = popc9(PAT), NS = slot_vals<NV, VT>();
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] = 0.0;
@@ -993,17 +993,22 @@ __device__ __forceinline__ void diag_upper_solve(const double (&Dg)[NV], double 
 enum { kIluFwd = 0, kIluBwd = 1, kIluLast = 2 };
 
 // ADD = 1 (backward / last-colour launches): also out_i = add_i + v_i for the finished rows (the
-// AMG's post-smoothing update y + M^-1 r without a separate pass)
-template <int NF, int PAT, int KIND, int LPR, int B, int NT, int ADD = 0, typename VT = double>
+// AMG's post-smoothing update y + M^-1 r without a separate pass).  YT = float (bf16 factors,
+// launch_ilu0_apply's yf): the forward colours store y = L^-1 d in yv, rounded to single precision,
+// the forward gathers and the backward sweep's own rows read it there; YT = double: y lives in v
+template <int NF, int PAT, int KIND, int LPR, int B, int NT, int ADD = 0, typename VT = double,
+          typename YT = double>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int r1,
                                                        const VT *__restrict__ lv,
                                                        const VT *__restrict__ uv,
                                                        const double *__restrict__ d,
                                                        double *__restrict__ v,
                                                        const double *__restrict__ add = nullptr,
-                                                       double *__restrict__ out = nullptr) {
+                                                       double *__restrict__ out = nullptr,
+                                                       YT *__restrict__ yv = nullptr) {
   constexpr int NV = popc9(PAT);
   constexpr bool FWD = KIND != kIluBwd;
+  constexpr bool YF = !std::is_same<YT, double>::value;
   const int gt = xcd_block(blockIdx.x, gridDim.x, 1) * kBlock + threadIdx.x;
   const int k = gt / LPR, q = gt % LPR;
   const bool live = r0 + k < r1;
@@ -1011,16 +1016,25 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
   const int row = R.row;
   // own data and diagonal block first: they share the neighbour loop's round trips
   double own[NF], Dg[NV];
-  load_nf<NF>(FWD ? d : v, size_t(row), own);
+  if constexpr (YF && !FWD)
+    load_nf<NF>(yv, size_t(row), own);
+  else
+    load_nf<NF>(FWD ? d : v, size_t(row), own);
   load_split_vals<NV, 0, VT, KIND == kIluFwd>(R.dg, R.dlane, Dg);
   double acc[NF];
-  split_row_dot<NF, PAT, LPR, B, NT, VT>(R, FWD ? 0 : 1, q, row, v, acc);
+  if constexpr (YF && FWD)
+    split_row_dot<NF, PAT, LPR, B, NT, VT>(R, 0, q, row, static_cast<const YT *>(yv), acc);
+  else
+    split_row_dot<NF, PAT, LPR, B, NT, VT>(R, FWD ? 0 : 1, q, row, v, acc);
   if (!live || q != 0) return;
 #pragma unroll
   for (int f = 0; f < NF; f++) acc[f] += own[f];
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
   if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
-  store_nf<NF>(v, size_t(row), acc);
+  if constexpr (YF && KIND == kIluFwd)
+    store_nf<NF>(yv, size_t(row), acc);
+  else
+    store_nf<NF>(v, size_t(row), acc);
   if constexpr (ADD && KIND != kIluFwd) {
     double ad[NF];
     load_nf<NF>(add, size_t(row), ad);
@@ -1041,16 +1055,19 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve(DevLayout L, int r0, int 
 #ifndef ILU_SU
 #define ILU_SU 4  // staged list entries per thread issued together (build-flag A/B knob)
 #endif
-template <int NF, int PAT, int KIND, int B, int NT, int ADD = 0, typename VT = double>
+template <int NF, int PAT, int KIND, int B, int NT, int ADD = 0, typename VT = double,
+          typename YT = double>
 __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, int r1, int blk0,
                                                            const VT *__restrict__ lv,
                                                            const VT *__restrict__ uv,
                                                            const double *__restrict__ d,
                                                            double *__restrict__ v,
                                                            const double *__restrict__ add = nullptr,
-                                                           double *__restrict__ out = nullptr) {
+                                                           double *__restrict__ out = nullptr,
+                                                           YT *__restrict__ yv = nullptr) {
   constexpr int NV = popc9(PAT), NS = slot_vals<NV, VT>();
   constexpr bool FWD = KIND != kIluBwd;
+  constexpr bool YF = !std::is_same<YT, double>::value;  // k_ilu0_solve's YT
   extern __shared__ double sx[];  // [cnt][NF]
   const int bl = xcd_block(blockIdx.x, gridDim.x, 1);
   const bool live = r0 + bl * kBlock + int(threadIdx.x) < r1;
@@ -1063,7 +1080,10 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   const SplitRow<VT> R = split_row<NV, FWD, VT>(L, lv, uv, pos, live);
   const int row = R.row;
   double own[NF], Dg[NV];
-  load_nf<NF>(FWD ? d : v, size_t(row), own);
+  if constexpr (YF && !FWD)
+    load_nf<NF>(yv, size_t(row), own);
+  else
+    load_nf<NF>(FWD ? d : v, size_t(row), own);
   load_split_vals<NV, 0, VT, KIND == kIluFwd>(R.dg, R.dlane, Dg);
   const int chunk = pos / kRows;
   const uint16_t *__restrict__ lix =
@@ -1109,7 +1129,12 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
     double t[kSU][NF];
 #pragma unroll
     for (int u = 0; u < kSU; u++)
-      if (jj[u] >= 0) load_nf<NF>(v, size_t(jj[u]), t[u]);
+      if (jj[u] >= 0) {
+        if constexpr (YF && FWD)
+          load_nf<NF>(yv, size_t(jj[u]), t[u]);
+        else
+          load_nf<NF>(v, size_t(jj[u]), t[u]);
+      }
 #pragma unroll
     for (int u = 0; u < kSU; u++) {
       const int k = int(threadIdx.x) + u * kBlock;
@@ -1120,7 +1145,10 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   }
   for (int k = int(threadIdx.x) + ILU_SU * kBlock; k < cnt; k += kBlock) {  // longer lists
     double t[NF];
-    load_nf<NF>(v, size_t(lst[u0 + k]), t);
+    if constexpr (YF && FWD)
+      load_nf<NF>(yv, size_t(lst[u0 + k]), t);
+    else
+      load_nf<NF>(v, size_t(lst[u0 + k]), t);
 #pragma unroll
     for (int f = 0; f < NF; f++) sx[k * NF + f] = t[f];
   }
@@ -1154,7 +1182,10 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_solve_lds(DevLayout L, int r0, 
   for (int f = 0; f < NF; f++) acc[f] += own[f];
   if (FWD) diag_lower_solve<NF, PAT>(Dg, acc);
   if (KIND != kIluFwd) diag_upper_solve<NF, PAT>(Dg, acc);
-  store_nf<NF>(v, size_t(row), acc);
+  if constexpr (YF && KIND == kIluFwd)
+    store_nf<NF>(yv, size_t(row), acc);
+  else
+    store_nf<NF>(v, size_t(row), acc);
   if constexpr (ADD && KIND != kIluFwd) {
     double ad[NF];
     load_nf<NF>(add, size_t(row), ad);
@@ -1554,8 +1585,9 @@ __global__ __launch_bounds__(kBlock) void k_update_xr(long long n, const Scalars
 // beta (p - omega v); WHICH 1: x += alpha y, s = r - alpha v with the ||s||^2 partials) applies it
 // in the same pass, one row per thread, and the sweep starts at colour 1: one launch and one
 // re-read of d fewer per preconditioner application.  yin may alias yout (x += alpha y reads a
-// row's y before the row's new y is written, by the same thread).
-template <int NF, int PAT, int WHICH, typename VT = double>
+// row's y before the row's new y is written, by the same thread).  YT = float: yout is the ILU(0)
+// application's single-precision intermediate (launch_ilu0_apply's yf).
+template <int NF, int PAT, int WHICH, typename VT = double, typename YT = double>
 __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
                                                         Scalars *S, int first,
                                                         double *__restrict__ x, const double *yin,
@@ -1563,7 +1595,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fwd0(DevLayout L, int c0_end,
                                                         const double *__restrict__ v,
                                                         double *__restrict__ p,
                                                         const VT *__restrict__ uv,
-                                                        double *yout,
+                                                        YT *yout,
                                                         double *__restrict__ partials,
                                                         const double *__restrict__ rt) {
   constexpr int NV = popc9(PAT);
@@ -2165,8 +2197,9 @@ static int ilu_lds_bsel() {
 
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const void *lvp,
                              const void *uvp, const double *d, double *v, hipStream_t s,
-                             int c_first, const double *add, double *out, int f32) {
+                             int c_first, const double *add, double *out, int f32, float *yf) {
   if (L.n_owned == 0) return hipSuccess;
+  if (yf && f32 != 2) return hipErrorInvalidValue;  // the bf16-factor mode only
   const int nc = L.ncolors;
   if (ilu_lds() && L.lsx_ptr && sweep_cfg() == 20) {
     // block numbering of the lists: colour by colour, 256-row blocks
@@ -2175,8 +2208,9 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     blk0[0] = 0;
     for (int c = 0; c < nc; c++) blk0[c + 1] = blk0[c] + (cp[c + 1] - cp[c] + kBlock - 1) / kBlock;
     const size_t lds = size_t(L.sx_max) * nf * sizeof(double);
-    auto run = [&](auto vt) -> hipError_t {
+    auto run = [&](auto vt, auto *yv) -> hipError_t {
       using VT = decltype(vt);
+      using YT = std::remove_pointer_t<decltype(yv)>;
       const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
       // slot batch (the sums run over the slots in order whatever the batch, so bitwise alike):
       // 2 below 1.5 M rows, 3 above -- config 3 apply 69.5 -> 66.8 us with 2, config 5 215 ->
@@ -2192,13 +2226,13 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
             constexpr int NT = decltype(ntc)::value;
             constexpr int BB = decltype(bc)::value;
             if (add && K != kIluFwd)
-              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 1, VT>), rows_grid(n),
+              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 1, VT, YT>), rows_grid(n),
                                  dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
-                                 add, out);
+                                 add, out, yv);
             else
-              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 0, VT>), rows_grid(n),
+              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 0, VT, YT>), rows_grid(n),
                                  dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
-                                 nullptr, nullptr);
+                                 nullptr, nullptr, yv);
           };
           auto batch = [&](auto ntc) {
             if (kBsel == 8)
@@ -2221,23 +2255,26 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
       });
       return hipGetLastError();
     };
-    return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
+    if (yf) return run(bf16s(), yf);
+    return f32 == 2 ? run(bf16s(), v) : f32 ? run(float(), v) : run(double(), v);
   }
-  auto run = [&](auto vt) -> hipError_t {
+  auto run = [&](auto vt, auto *yv) -> hipError_t {
     using VT = decltype(vt);
+    using YT = std::remove_pointer_t<decltype(yv)>;
     const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
     PNP_PAT_DISPATCH(nf, pat, PNP_LPR_DISPATCH({
       auto go = [&](auto kind, int c) {
         const int n = cp[c + 1] - cp[c];
         if (n <= 0) return;
-        if (add && decltype(kind)::value != kIluFwd)
-          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 1, VT>),
+        constexpr int K = decltype(kind)::value;
+        if (add && K != kIluFwd)
+          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, K, LPRc, Bc, NTc, 1, VT, YT>),
                              rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
-                             d, v, add, out);
+                             d, v, add, out, yv);
         else
-          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, decltype(kind)::value, LPRc, Bc, NTc, 0, VT>),
+          hipLaunchKernelGGL((k_ilu0_solve<NFc, PATc, K, LPRc, Bc, NTc, 0, VT, YT>),
                              rows_grid(n * LPRc), dim3(kBlock), 0, s, L, cp[c], cp[c + 1], lv, uv,
-                             d, v, nullptr, nullptr);
+                             d, v, nullptr, nullptr, yv);
       };
       // the last colour's backward step runs in its forward launch (kIluLast); c_first = 1:
       // colour 0's forward step was done by launch_update_fwd0
@@ -2247,7 +2284,8 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     }));
     return hipGetLastError();
   };
-  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
+  if (yf) return run(bf16s(), yf);
+  return f32 == 2 ? run(bf16s(), v) : f32 ? run(float(), v) : run(double(), v);
 }
 
 // every workgroup of a grid resident at once: CUs x the occupancy at this LDS size (capped by n)
@@ -2291,25 +2329,28 @@ hipError_t launch_update_fwd0(const DevLayout &L, int nf, int pat, int c0_end, c
                               int which, int first, double *x, const double *yin, double *r,
                               const double *v, double *p, const void *uvp, double *yout,
                               double *partials, int *nparts, hipStream_t s, int f32,
-                              const double *rt) {
+                              const double *rt, float *youtf) {
   const dim3 g = rows_grid(L.n_owned);
   Scalars *Sw = const_cast<Scalars *>(S);  // which 1 with x = null sets S->xpend
   if (nparts) *nparts = int(g.x);
   if (L.n_owned == 0) return hipSuccess;
-  auto run = [&](auto vt) -> hipError_t {
+  if (youtf && f32 != 2) return hipErrorInvalidValue;  // the bf16-factor mode only
+  auto run = [&](auto vt, auto *yo) -> hipError_t {
     using VT = decltype(vt);
+    using YT = std::remove_pointer_t<decltype(yo)>;
     const VT *uv = static_cast<const VT *>(uvp);
     PNP_PAT_DISPATCH(nf, pat, {
       if (which == 0)
-        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT>), g, dim3(kBlock), 0, s, L, c0_end, Sw,
-                           first, x, yin, r, v, p, uv, yout, partials, nullptr);
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 0, VT, YT>), g, dim3(kBlock), 0, s, L, c0_end,
+                           Sw, first, x, yin, r, v, p, uv, yo, partials, nullptr);
       else
-        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT>), g, dim3(kBlock), 0, s, L, c0_end, Sw,
-                           first, x, yin, r, v, p, uv, yout, partials, rt);
+        hipLaunchKernelGGL((k_update_fwd0<NFc, PATc, 1, VT, YT>), g, dim3(kBlock), 0, s, L, c0_end,
+                           Sw, first, x, yin, r, v, p, uv, yo, partials, rt);
     });
     return hipGetLastError();
   };
-  return f32 == 2 ? run(bf16s()) : f32 ? run(float()) : run(double());
+  if (youtf) return run(bf16s(), youtf);
+  return f32 == 2 ? run(bf16s(), yout) : f32 ? run(float(), yout) : run(double(), yout);
 }
 
 hipError_t launch_split(const DevLayout &L, int nf, int pat, int from_k, const double *src,

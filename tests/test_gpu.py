@@ -406,7 +406,7 @@ def _ilu0_dense(A, M):
     return A
 
 
-@pytest.mark.parametrize("f32", [0, 1, 2])
+@pytest.mark.parametrize("f32", [0, 1, 2, 3])
 @pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
                                        ("pore_small_k0", "pb"), ("cylinder_k0", "pnp")])
 def test_ilu0_application_matches_textbook_ilu0(name, kind, f32):
@@ -414,8 +414,9 @@ def test_ilu0_application_matches_textbook_ilu0(name, kind, f32):
     stored block pattern, ordered colour-major by vertex with fields ascending.
     f32 = 0: fp64 factors, to rounding (1e-10); f32 = 1: the factors stored in single precision,
     fp64 sweeps -- the same operator to float rounding of the factors (2e-5 of max|v| on these
-    well-conditioned small systems); f32 = 2 (PNP_OPT_ILU_F32's default): bfloat16 factors for
-    block systems (8 significant bits: 2e-2 of max|v|), single precision for scalar ones."""
+    well-conditioned small systems); f32 = 2: bfloat16 factors for block systems (8 significant
+    bits: 2e-2 of max|v|), single precision for scalar ones; f32 = 3 (PNP_OPT_ILU_F32's default):
+    2 with the forward intermediate in single precision (the same bound)."""
     import scipy.linalg as sla
     z, mesh, par, orc = golden(name)
     ctx = P.Context(mesh, par)
@@ -446,7 +447,7 @@ def test_ilu0_application_matches_textbook_ilu0(name, kind, f32):
     y = sla.solve_triangular(np.tril(F, -1) + np.eye(len(F)), d[perm], lower=True)
     v_ref = sla.solve_triangular(np.triu(F), y, lower=False)
     v = ctx.prec_apply(d, P.PREC_ILU0)[perm]
-    tol = 1e-10 if f32 == 0 else (2e-2 if f32 == 2 and nf > 1 else 2e-5)
+    tol = 1e-10 if f32 == 0 else (2e-2 if f32 >= 2 and nf > 1 else 2e-5)
     assert np.max(np.abs(v - v_ref)) <= tol * np.max(np.abs(v_ref))
 
 
@@ -643,6 +644,37 @@ def test_cg_matches_oracle_cg(prec):
     assert ro.converged
     assert abs(res["iterations"] - ro.iterations) <= 1
     assert np.max(np.abs(sol - xo)) <= 1e-8 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
+                                       ("pore_small_k0", "pb"), ("cylinder_k0", "pnp")])
+def test_ilu0_single_precision_intermediate(name, kind):
+    """PNP_OPT_ILU_F32 = 3 (the default) against 2: the same bfloat16 factors, the forward sweep's
+    intermediate L^-1 d rounded to single precision between the colour launches.  Block systems:
+    the application differs from 2's (so the single-precision path ran) by float rounding only
+    (1e-6 of max|v|), and BiCGSTAB converges with either; scalar systems keep f32 factors and fp64
+    intermediates under both, bit for bit."""
+    z, mesh, par, orc = golden(name)
+    ctx = P.Context(mesh, par)
+    set_ops(z, ctx, orc, kind)
+    nf = 3 if kind.startswith("pnp") else 1
+    x = z[kind + "_x"]
+    ctx.jacobian(x, export=False)
+    d = np.random.default_rng(11).standard_normal(nf * mesh.nv)
+    rhs = ctx.residual(x)
+    out = {}
+    for f32 in (2, 3):
+        ctx.set_option(P.OPT_ILU_F32, f32)
+        v = ctx.prec_apply(d, P.PREC_ILU0)
+        sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=1e-12, maxit=20000)
+        assert res["converged"]
+        out[f32] = (v, sol)
+    (v2, s2), (v3, s3) = out[2], out[3]
+    if nf == 1:
+        assert np.array_equal(v2, v3) and np.array_equal(s2, s3)
+        return
+    assert not np.array_equal(v2, v3)
+    assert np.max(np.abs(v3 - v2)) <= 1e-6 * np.max(np.abs(v2))
 
 
 @pytest.mark.parametrize("f32", [0, 1])

@@ -75,6 +75,7 @@ def test_flow_partitioned_ranks_bitwise():
 
     def fn(c, r):
         c.set_operator(P.OP_PNP)
+        c.set_option(P.OPT_ILU_F32, 2)  # as in test_flow_config3_bitwise
         c.jacobian(x, export=False)
         b = c.sync_vector(c.residual(x))
         out = []
@@ -104,6 +105,9 @@ def test_flow_config3_bitwise():
                         0.06 * rng.uniform(0.5, 1.5, nv)])
     ctx = P.Context(mesh, par)
     ctx.set_operator(P.OP_PNP)
+    # bfloat16 factors; 2, not the default 3, whose single-precision forward intermediate lives
+    # in the colour launches only (the dataflow form keeps it in fp64 and runs 3 as 2)
+    ctx.set_option(P.OPT_ILU_F32, 2)
     ctx.jacobian(x, export=False)
     rhs = ctx.residual(x)
 

@@ -3,7 +3,8 @@ the default) against the direct-gather sweeps (PNP_ILU_LDS=0), and the longest-f
 the split L / U storage (the default) against the identity order (PNP_SPLIT_SORT=0).  The knobs
 are read once per process, so each variant runs in a child process.  Every variant keeps each
 row's slot order and arithmetic, so preconditioner applications (ILU(0) with fp32 and fp64
-factors, the multicolour SSOR), BiCGSTAB iterates and counts, the AMG's ILU(0)-smoothed cycle and
+factors, fp32 and fp64, and bf16 factors with the single-precision intermediate, the
+multicolour SSOR), BiCGSTAB iterates and counts, the AMG's ILU(0)-smoothed cycle and
 a PB -> PNP Newton must be bitwise the same, on one rank and on 3 partitioned ranks."""
 import json
 import os
@@ -36,7 +37,7 @@ for name in ("pore_small_k0", "cylinder_k0"):
     out[f"{name}ssor"] = h(ctx.prec_apply(rhs, P.PREC_SSOR))
     sol, res = ctx.linear_solve(rhs, prec=P.PREC_SSOR, reduction=1e-10, maxit=20000)
     out[f"{name}ssor_solve"] = [h(sol), res["iterations"]]
-    for f32 in (1, 0):
+    for f32 in (3, 1, 0):
         ctx.set_option(P.OPT_ILU_F32, f32)
         out[f"{name}apply{f32}"] = h(ctx.prec_apply(rhs, P.PREC_ILU0))
         sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=1e-10, maxit=20000)

@@ -32,7 +32,7 @@ for name in ("pore_small_k0", "cylinder_k0"):
     ctx.set_operator(P.OP_PNP)
     ctx.jacobian(x, export=False)
     rhs = ctx.residual(x)
-    for f32 in (1, 0):
+    for f32 in (3, 1, 0):
         ctx.set_option(P.OPT_ILU_F32, f32)
         for red in (1e-10, 1e-2, 1e-3, 1e-4, 1e-6):
             sol, res = ctx.linear_solve(rhs, prec=P.PREC_ILU0, reduction=red, maxit=20000)

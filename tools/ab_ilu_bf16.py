@@ -1,7 +1,8 @@
-"""ILU(0) factors in bfloat16 (PNP_OPT_ILU_F32 = 2) against single precision (1) at config 3,
-interleaved: the ILU(0) application's event time per apply and the BiCGSTAB wall time per
-iteration, 200 iterations (no convergence stop) on the Jacobian at a random admissible state.
-usage: python tools/ab_ilu_bf16.py [reps=3]"""
+"""PNP_OPT_ILU_F32 modes against each other at config 3, interleaved (default: bfloat16 factors, 2,
+against single precision, 1; 3 = bfloat16 factors with the single-precision forward intermediate):
+the ILU(0) application's event time per apply and the BiCGSTAB wall time per iteration, 200
+iterations (no convergence stop) on the Jacobian at a random admissible state.
+usage: python tools/ab_ilu_bf16.py [reps=3] [modes=1,2]"""
 import json
 import os
 import sys
@@ -16,6 +17,8 @@ import pnp_amd as P  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    modes = [int(m) for m in (sys.argv[2] if len(sys.argv) > 2 else "1,2").split(",")]
+    names = {0: "f64", 1: "f32", 2: "bf16", 3: "bf16_y32"}
     cfg = P.read_config(os.path.join(ROOT, "data", "pore_pnp", "pore.cfg"))
     mesh = P.Mesh.read_gmsh(cfg.meshfile).refine(4)
     ctx = P.Context(mesh, P.Params.from_config(cfg))
@@ -27,9 +30,9 @@ def main():
     ctx.state_set(x)
     ctx.assemble_state(1)
     n = 200
-    out = {1: {"apply_us": [], "iter_ms": []}, 2: {"apply_us": [], "iter_ms": []}}
+    out = {m: {"apply_us": [], "iter_ms": []} for m in modes}
     for _ in range(reps):
-        for f in (1, 2):
+        for f in modes:
             ctx.set_option(P.OPT_ILU_F32, f)
             ctx.bicgstab_iterations(8, P.PREC_ILU0)  # factorisation in this precision, warm
             ctx.timers(enable=True, reset=True)
@@ -39,7 +42,7 @@ def main():
             t0 = time.perf_counter()
             ctx.bicgstab_iterations(n, P.PREC_ILU0)
             out[f]["iter_ms"].append(1e3 * (time.perf_counter() - t0) / n)
-    res = {("f32" if f == 1 else "bf16"): {"apply_us_median": float(np.median(v["apply_us"])),
+    res = {names[f]: {"apply_us_median": float(np.median(v["apply_us"])),
                                            "iter_ms_median": float(np.median(v["iter_ms"])),
                                            **v} for f, v in out.items()}
     print(json.dumps(res), flush=True)
