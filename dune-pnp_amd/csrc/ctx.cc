@@ -156,14 +156,17 @@ struct pnp_ctx {
   // iteration at config 3, Newton counts inside their last-bit spread); scalar
   // systems (PB, Poisson, diffusion: one value per block, 2 B saved per slot) keep f32, where the
   // PB Newton at config 1 took 13 % more iterations with bf16
-  // 3 (the default): the bf16 factors of 2, and the forward sweep's intermediate y = L^-1 d kept in
+  // 3 (opt-in): the bf16 factors of 2, and the forward sweep's intermediate y = L^-1 d kept in
   // single precision (ilu_y32: 12 B per PNP row written, re-read by the backward sweep and gathered
-  // by the forward one, instead of 24).  The dataflow form (PNP_OPT_ILU_FLOW)
-  // keeps y in fp64, so with it on 3 runs as 2
+  // by the forward one, instead of 24): apply 56.3 -> 54.5 us at config 3, but the backward
+  // sweep's cancellation on the drift blocks turns y's rounding into a nonlinear preconditioner
+  // error that stalls BiCGSTAB on the config-5 Newton and the config-4 AMG steps (DESIGN.md
+  // §0.13), so not the default.  The dataflow form (PNP_OPT_ILU_FLOW) keeps y in fp64 and runs
+  // 3 as 2
   int ilu_f32 = [] {
     const char *e = std::getenv("PNP_ILU_F32");
-    const int v = e ? std::atoi(e) : 3;
-    return (v >= 0 && v <= 2) ? v : 3;
+    const int v = e ? std::atoi(e) : 2;
+    return (v >= 0 && v <= 3) ? v : 2;
   }();
   int ilu_eff() const { return (ilu_f32 >= 2 && nf == 1) ? 1 : ilu_f32; }
   // the factors' storage: 0 fp64, 1 f32, 2 bf16 (the kernels' f32 argument)

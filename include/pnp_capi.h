@@ -357,11 +357,12 @@ enum {
   /* Storage precision of the ILU(0) factors (PNP_PREC_ILU0 and the AMG's ILU(0) smoother); the
    * sweeps compute in fp64 whatever it is.  The matrix, the SpMV, SSOR/Jacobi and every vector stay
    * fp64, so the operator and the converged solutions are those of the fp64 path; only the
-   * preconditioner is a rounded ILU(0).  3 (default): the factors of 2, and the forward sweep's
+   * preconditioner is a rounded ILU(0).  2 (default): bfloat16 factors for block systems (8
+   * significant bits, 16 B per PNP block instead of 28; config 3: apply 66 -> 59 us, Newton counts
+   * within their last-bit spread).  3 (opt-in): the factors of 2, and the forward sweep's
    * intermediate L^-1 d kept in single precision between the colour launches (12 B per PNP row
-   * instead of 24; the result and every other vector stay fp64; with PNP_OPT_ILU_FLOW on, 3 runs
-   * as 2).  2: bfloat16 factors for block systems (8 significant bits, 16 B per PNP block instead
-   * of 28; config 3: apply 66 -> 59 us, Newton counts within their last-bit spread); 2 and 3 keep
+   * instead of 24; apply -1.8 us at config 3), which stalls BiCGSTAB on some drift-dominated
+   * systems; with PNP_OPT_ILU_FLOW on, 3 runs as 2.  2 and 3 keep
    * single-precision factors for scalar systems (PB, Poisson, diffusion); 1: single precision
    * (apply 119 -> 95 us against fp64 in round 2, Newton 9,295 -> 9,177 iterations); 0: fp64.
    * The environment variable PNP_ILU_F32 = 0 .. 3 sets the default. */

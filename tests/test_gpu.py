@@ -414,8 +414,8 @@ def test_ilu0_application_matches_textbook_ilu0(name, kind, f32):
     stored block pattern, ordered colour-major by vertex with fields ascending.
     f32 = 0: fp64 factors, to rounding (1e-10); f32 = 1: the factors stored in single precision,
     fp64 sweeps -- the same operator to float rounding of the factors (2e-5 of max|v| on these
-    well-conditioned small systems); f32 = 2: bfloat16 factors for block systems (8 significant
-    bits: 2e-2 of max|v|), single precision for scalar ones; f32 = 3 (PNP_OPT_ILU_F32's default):
+    well-conditioned small systems); f32 = 2 (PNP_OPT_ILU_F32's default): bfloat16 factors for
+    block systems (8 significant bits: 2e-2 of max|v|), single precision for scalar ones; f32 = 3:
     2 with the forward intermediate in single precision (the same bound)."""
     import scipy.linalg as sla
     z, mesh, par, orc = golden(name)
@@ -649,7 +649,7 @@ def test_cg_matches_oracle_cg(prec):
 @pytest.mark.parametrize("name,kind", [("pore_small_k0", "pnp"), ("pore_small_k0", "pnp_ie"),
                                        ("pore_small_k0", "pb"), ("cylinder_k0", "pnp")])
 def test_ilu0_single_precision_intermediate(name, kind):
-    """PNP_OPT_ILU_F32 = 3 (the default) against 2: the same bfloat16 factors, the forward sweep's
+    """PNP_OPT_ILU_F32 = 3 (opt-in) against 2: the same bfloat16 factors, the forward sweep's
     intermediate L^-1 d rounded to single precision between the colour launches.  Block systems:
     the application differs from 2's (so the single-precision path ran) by float rounding only
     (1e-6 of max|v|), and BiCGSTAB converges with either; scalar systems keep f32 factors and fp64

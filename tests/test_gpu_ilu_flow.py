@@ -105,8 +105,8 @@ def test_flow_config3_bitwise():
                         0.06 * rng.uniform(0.5, 1.5, nv)])
     ctx = P.Context(mesh, par)
     ctx.set_operator(P.OP_PNP)
-    # bfloat16 factors; 2, not the default 3, whose single-precision forward intermediate lives
-    # in the colour launches only (the dataflow form keeps it in fp64 and runs 3 as 2)
+    # bfloat16 factors (2, the default; 3's single-precision forward intermediate lives in the
+    # colour launches only: the dataflow form keeps it in fp64 and runs 3 as 2)
     ctx.set_option(P.OPT_ILU_F32, 2)
     ctx.jacobian(x, export=False)
     rhs = ctx.residual(x)
