@@ -158,10 +158,10 @@ struct pnp_ctx {
   // PB Newton at config 1 took 13 % more iterations with bf16
   // 3 (opt-in): the bf16 factors of 2, and the forward sweep's intermediate y = L^-1 d kept in
   // single precision (ilu_y32: 12 B per PNP row written, re-read by the backward sweep and gathered
-  // by the forward one, instead of 24): apply 56.3 -> 54.5 us at config 3, but the backward
-  // sweep's cancellation on the drift blocks turns y's rounding into a nonlinear preconditioner
-  // error that stalls BiCGSTAB on the config-5 Newton and the config-4 AMG steps (DESIGN.md
-  // §0.13), so not the default.  The dataflow form (PNP_OPT_ILU_FLOW) keeps y in fp64 and runs
+  // by the forward one, instead of 24): apply 56.3 -> 54.5 us at config 3, but the rounding makes
+  // the preconditioner nonlinear (2-5e-8 relative per application), which BiCGSTAB's short
+  // recurrences do not tolerate: 408 -> 710 iterations on a config-5 solve, the config-5 Newton
+  // and the config-4 AMG steps stall, so not the default.  The dataflow form (PNP_OPT_ILU_FLOW) keeps y in fp64 and runs
   // 3 as 2
   int ilu_f32 = [] {
     const char *e = std::getenv("PNP_ILU_F32");
