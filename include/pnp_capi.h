@@ -361,8 +361,9 @@ enum {
    * significant bits, 16 B per PNP block instead of 28; config 3: apply 66 -> 59 us, Newton counts
    * within their last-bit spread).  3 (opt-in): the factors of 2, and the forward sweep's
    * intermediate L^-1 d kept in single precision between the colour launches (12 B per PNP row
-   * instead of 24; apply -1.8 us at config 3), which stalls BiCGSTAB on some drift-dominated
-   * systems; with PNP_OPT_ILU_FLOW on, 3 runs as 2.  2 and 3 keep
+   * instead of 24; apply -1.8 us at config 3); the rounding makes the preconditioner nonlinear,
+   * and BiCGSTAB then needs up to 2.6x the iterations on config 5; with
+   * PNP_OPT_ILU_FLOW on, 3 runs as 2.  2 and 3 keep
    * single-precision factors for scalar systems (PB, Poisson, diffusion); 1: single precision
    * (apply 119 -> 95 us against fp64 in round 2, Newton 9,295 -> 9,177 iterations); 0: fp64.
    * The environment variable PNP_ILU_F32 = 0 .. 3 sets the default. */
