@@ -46,13 +46,13 @@ import pnp_amd as P  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured stream ceilings
 #                       are in the line (`measured_stream_gbs`, tools/micro/stream.hip)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05", "pmc_summary.json")
 SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
 
 
 def pmc_summary():
     """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py), or None."""
-    for path in (PMC_SUMMARY, PMC_SUMMARY.replace("r04", "r03"), PMC_SUMMARY.replace("r04", "r02")):
+    for path in (PMC_SUMMARY, PMC_SUMMARY.replace("r05", "r04"), PMC_SUMMARY.replace("r05", "r03")):
         try:
             with open(path) as f:
                 d = json.load(f)
