@@ -179,6 +179,7 @@ struct pnp_ctx {
   }
   int ilu_fused = 1;  // PNP_OPT_ILU_FUSED_FACTOR
   int amg_fallback = 0;  // PNP_OPT_AMG_FALLBACK
+  int ilu_retry = 1;     // PNP_OPT_ILU_RETRY
   int twored_opt = [] {  // PNP_OPT_BICG_TWORED: -1 auto (on with more than one rank), 0, 1
     const char *ev = std::getenv("PNP_BICG_TWORED");
     return ev ? (std::atoi(ev) != 0 ? 1 : 0) : -1;
@@ -340,6 +341,7 @@ struct pnp_ctx {
 
   // vectors (sized n_local * 3)
   DBuf<double> x, r, rs, z, rt, p, v, t, y, y2, b, prevu, ext, sendbuf, partials, partials2;
+  DBuf<double> redmw;  // the multi-workgroup reduction's ticket and slice sums (main stream only)
   std::vector<int> newton_its;        // pnp_newton_history: linear iterations per Newton step
   std::vector<double> newton_defects; // and the defect after each step
   DBuf<pnp::Scalars> S;
@@ -708,10 +710,10 @@ struct pnp_ctx {
     hipError_t e;
     const double *src = from2 ? partials2.p : partials.p;
     if (!dist) {
-      e = pnp::launch_reduce(src, np, k, S.p, stream, stage);
+      e = pnp::launch_reduce(src, np, k, S.p, stream, stage, redmw.p);
       return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
     }
-    e = pnp::launch_reduce(src, np, k, S.p, stream);
+    e = pnp::launch_reduce(src, np, k, S.p, stream, -1, redmw.p);
     if (e != hipSuccess) return hipfail(e, "reduce");
     int rc = allreduce_red(k);
     if (rc) return rc;
@@ -723,10 +725,11 @@ struct pnp_ctx {
   int reduce_derive2(int npa, int ka, int npb, int kb, int stage) {
     hipError_t e;
     if (!dist) {
-      e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream, stage);
+      e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream, stage,
+                              redmw.p);
       return e == hipSuccess ? PNP_OK : hipfail(e, "reduce");
     }
-    e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream);
+    e = pnp::launch_reduce2(partials.p, npa, ka, partials2.p, npb, kb, S.p, stream, -1, redmw.p);
     if (e != hipSuccess) return hipfail(e, "reduce");
     int rc = allreduce_red(ka + kb);
     if (rc) return rc;
@@ -900,6 +903,13 @@ struct pnp_ctx {
     // input needs no scatter into an external copy (PNP config 3: 20 us per application,
     // profiles/r05/nat_split_r5d.txt); the result is gathered out of vb afterwards
     auto P = [&](int R) { return L.g2l[R % nv] * nf + R / nv; };
+    // NatSweep::info packs a row's entry count and its diagonal's offset into one int as
+    // len | offset << 8 (the kernels decode len & 255): at most 255 entries per row (P1 PNP rows
+    // have <= 3 * 21); a wider pattern would corrupt both, so refuse it here
+    for (int R = 0; R < n; R++)
+      if (cnt[R + 1] - cnt[R] > 255)
+        return fail(PNP_E_STATE, "natural SSOR: a row has more than 255 CSR entries (row " +
+                                     std::to_string(R) + ")");
     auto schedule = [&](bool fwd, NatDir &W) -> int {
       std::vector<int> &lptr = W.lptr;
       std::vector<int> lev(n, -1), push(n, 0);
@@ -1118,6 +1128,7 @@ struct pnp_ctx {
     };
     nat_units.clear();
     nat_units_ok = true;
+    nat_resident = -1;
     nat_max_width = 0;
     if ((rc = schedule(true, nat_f)) || (rc = schedule(false, nat_b))) return rc;
     if (nat_units_ok && (rc = upv(d_nat_units, nat_units, "natural SSOR units"))) return rc;
@@ -1138,12 +1149,12 @@ struct pnp_ctx {
   int csr_values() {
     int rc;
     if ((rc = csr_structure())) return rc;
-    if (csr_vals_valid) return PNP_OK;
+    if (csr_vals_valid) return nat_probe_run();
     hipError_t e = pnp::launch_csr_fill(dl, nf, pat, vals.p, csr_nnz, csr_src.p, csr_vidx.p,
                                         csr_val.p, stream);
     if (e != hipSuccess) return hipfail(e, "csr fill");
     csr_vals_valid = true;
-    return PNP_OK;
+    return nat_probe_run();
   }
 
   // v = SSOR_natural^{-1} d on internal-layout owned rows (ssor_natural.hip); csr_values() first
@@ -1161,11 +1172,26 @@ struct pnp_ctx {
       const char *ev = std::getenv("PNP_NAT_FLOW");
       return !(ev && std::atoi(ev) == 0);
     }();
-    return nat_flow_opt == 0 ? false
-           : nat_flow_opt == 1 ? nat_units_ok
-                               : env_on && !lg && !host_tr() && nat_units_ok;
+    return nat_resident != 0 &&
+           (nat_flow_opt == 0   ? false
+            : nat_flow_opt == 1 ? nat_units_ok
+                                : env_on && !lg && !host_tr() && nat_units_ok);
   }
   int nat_flow_opt = -1;  // PNP_OPT_NAT_FLOW: -1 auto (above), 0 level launches, 1 dataflow
+  // the dataflow's progress needs its whole grid resident: checked once per schedule on the device
+  // (pnp::ssor_natural_flow_resident) before the first dataflow application; 0 keeps the level
+  // launches (the same results bit for bit).  -1 not yet checked
+  int nat_resident = -1;
+  DBuf<unsigned> nat_probe;
+  int nat_probe_run() {
+    if (nat_resident >= 0 || !use_nat_flow()) return PNP_OK;
+    hipError_t e = nat_probe.p ? hipSuccess : nat_probe.alloc(2);
+    if (e != hipSuccess) return hipfail(e, "natural SSOR probe");
+    const int r = pnp::ssor_natural_flow_resident(nat_flow_view(), nat_probe.p, stream);
+    if (r < 0) return fail(PNP_E_HIP, "natural SSOR: co-residency probe failed");
+    nat_resident = r;
+    return PNP_OK;
+  }
   long long nat_flow_n = 0, nat_level_n = 0;  // applications per schedule (pnp_info)
   hipError_t nat_sweep(const double *d, double *vout) {
     if (use_nat_flow()) {
@@ -1175,7 +1201,7 @@ struct pnp_ctx {
     nat_level_n++;
     return ssor_natural_levels(d, vout);
   }
-  hipError_t ssor_natural_flow(const double *d, double *vout) {
+  pnp::NatFlow nat_flow_view() const {
     pnp::NatFlow F;
     F.units = d_nat_units.p;
     F.nunits = int(nat_units.size());
@@ -1188,6 +1214,10 @@ struct pnp_ctx {
     F.fwd = nat_f.view();
     F.bwd = nat_b.view();
     F.abort_word = nat_abort.p;
+    return F;
+  }
+  hipError_t ssor_natural_flow(const double *d, double *vout) {
+    const pnp::NatFlow F = nat_flow_view();
     hipError_t e = pnp::launch_ssor_natural_flow(F, nf * mesh.nv, csr_val.p, d, nat_vf.p, nat_v.p,
                                                  stream);
     // the result out of the external-layout vb (storing it at internal positions from the
@@ -3226,7 +3256,7 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
                2 * std::max<size_t>(size_t(pnp::blas_nparts(3LL * nloc)),
                                     size_t(pnp::spmv_parts(L.n_owned))) + 64,
                "partials2")) ||
-      (rc = al(c->S, 2, "scalars")) ||
+      (rc = al(c->S, 2, "scalars")) || (rc = al(c->redmw, pnp::kRedMwDoubles, "reduce ticket")) ||
       (rc = al(c->dmask, 3 * size_t(L.n_owned), "dmask")) ||
       (rc = al(c->cvec, 3 * size_t(L.n_owned), "cvec")) || (rc = al(c->aux0, nloc, "aux0")) ||
       (rc = al(c->aux1, nloc, "aux1"))) {
@@ -3806,6 +3836,11 @@ extern "C" int pnp_set_option(pnp_ctx *c, int32_t option, int64_t value) {
     c->amg_fallback = int(value);
     return PNP_OK;
   }
+  if (option == PNP_OPT_ILU_RETRY) {
+    if (value != 0 && value != 1) return c->fail(PNP_E_ARG, "PNP_OPT_ILU_RETRY takes 0 or 1");
+    c->ilu_retry = int(value);
+    return PNP_OK;
+  }
   if (option == PNP_OPT_BICG_TWORED) {
     if (value < -1 || value > 1) return c->fail(PNP_E_ARG, "PNP_OPT_BICG_TWORED takes -1, 0 or 1");
     c->twored_opt = int(value);
@@ -3888,6 +3923,10 @@ extern "C" int pnp_get_option(pnp_ctx *c, int32_t option, int64_t *value) {
   }
   if (option == PNP_OPT_AMG_FALLBACK) {
     *value = c->amg_fallback;
+    return PNP_OK;
+  }
+  if (option == PNP_OPT_ILU_RETRY) {
+    *value = c->ilu_retry;
     return PNP_OK;
   }
   if (option == PNP_OPT_SEQ_ORDER) {
@@ -4108,6 +4147,18 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
   double t_start = now_s();
   int rc;
   long long n = c->nown();
+  // PNP_OPT_ILU_RETRY: the factor precision a retry switched from, restored when this call ends
+  int ilu_saved = -1;
+  struct IluRestore {
+    pnp_ctx *c;
+    int &saved;
+    ~IluRestore() {
+      if (saved < 0) return;
+      c->ilu_f32 = saved;
+      if (c->split_of == 2) c->split_of = 0;
+      c->lu_valid = false;
+    }
+  } ilu_restore{c, ilu_saved};
   if ((rc = c->upload_ext(u, c->nf, c->x.p, true))) return rc;
   double ta = now_s();
   if ((rc = c->assemble(c->x.p, 0))) return rc;
@@ -4156,6 +4207,22 @@ extern "C" int pnp_newton(pnp_ctx *c, double *u, const pnp_newton_opts *o, pnp_n
       res->linear_iterations += sr.iterations;
       step_its += sr.iterations;
       res->linear_fallbacks++;
+    }
+    const bool uses_ilu = lo.prec == PNP_PREC_ILU0 ||
+                          (lo.prec == PNP_PREC_AMG && c->amg_opts.smoother == PNP_PREC_ILU0);
+    if (c->ilu_retry && uses_ilu && c->ilu_f32 != 0 && (sr.breakdown || !sr.converged)) {
+      // reduced-precision ILU(0) factors stalled this solve: re-solve with fp64 factors (ISTL's
+      // SeqILU0) and keep them for the rest of this call
+      if (ilu_saved < 0) ilu_saved = c->ilu_f32;
+      c->ilu_f32 = 0;
+      if (c->split_of == 2) c->split_of = 0;
+      c->lu_valid = false;
+      CK(hipMemcpyAsync(c->b.p, c->r.p, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream),
+         "rhs");
+      if ((rc = c->krylov(c->b.p, c->z.p, lo, sr))) return rc;
+      res->linear_iterations += sr.iterations;
+      step_its += sr.iterations;
+      res->precision_retries++;
     }
     res->solve_seconds += now_s() - ts;
     if (sr.breakdown) {

@@ -417,14 +417,17 @@ hipError_t launch_update_xr(long long n, const Scalars *S, int which, double *x,
 hipError_t launch_dot(long long n, const double *a, const double *b, int two, double *partials,
                       hipStream_t s);
 // sum partials[nparts][k] -> S->red[0..k) (deterministic order); derive_stage >= 0 also runs
-// the derive step in the same launch (single GPU: no allreduce in between)
+// the derive step in the same launch (single GPU: no allreduce in between).  mw (kRedMwDoubles
+// doubles, zeroed once, one per stream): with it, long partial arrays (>= 8,192) are summed by a
+// multi-workgroup launch whose last workgroup finishes the sum (linalg.hip k_reduce_mw)
+constexpr int kRedMwDoubles = 1 + 64 * 5;
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
-                         int derive_stage = -1);
+                         int derive_stage = -1, double *mw = nullptr);
 // partial-sum count of launch_spmv over nrows rows (allocation bound)
 int spmv_parts(int nrows);
 // sum partials pa[npa][ka] -> S->red[0..ka) and pb[npb][kb] -> S->red[ka..ka+kb), ka+kb <= 5
 hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
-                          Scalars *S, hipStream_t s, int derive_stage = -1);
+                          Scalars *S, hipStream_t s, int derive_stage = -1, double *mw = nullptr);
 // derive scalars after a reduction; stage: 0 init (red: <r,r>), 1 after h, 2 after first half
 // norm, 3 after <t,r>,<t,t>, 4 after second half (red: <r,r>, <rt,r>); 23 = 2 then 3 from one
 // reduction (red: <t,r>, <t,t>, ||s||^2), the first half step's test deferred to the second's;
@@ -459,7 +462,8 @@ hipError_t launch_csr_fill(const DevLayout &L, int nf, int pat, const double *va
 // ISTL SeqSSOR (k = 1, omega = 1) in the lexicographic DOF order (ssor_natural.hip): v = 0, then
 // the forward levels and the backward levels, one launch per level.  Per sweep direction
 // (NatSweep): sweep positions t of level l are lptr[l] .. lptr[l+1] (host array); info[t] = {row
-// (external index), entry count | the diagonal's offset in the row << 8, index of the row's first
+// (external index), entry count | the diagonal's offset in the row << 8 (so at most 255 entries
+// per row: csr_values() refuses a wider pattern with PNP_E_STATE), index of the row's first
 // entry in the external-layout CSR values val (its entries are contiguous there), the row's
 // internal position}; the operand codes of the row's entries (ecol, CSR order) as an ELL of the
 // level stored unit-major: with tl = t - lptr[l], entry k at eoff[l] + (tl / U * w_l + k) * U +
@@ -508,6 +512,11 @@ struct NatFlow {
   NatSweep fwd, bwd;
   unsigned *abort_word = nullptr;
 };
+// 1 if the dataflow launch's head grid and its chain grid are each resident at once on this
+// device (each kernel launched once in probe mode with its full grid: workgroups check in and
+// wait for the whole grid, bounded), 0 if not, -1 on a HIP error; probe: 2 unsigned of scratch.
+// Synchronous (not inside a stream capture)
+int ssor_natural_flow_resident(const NatFlow &F, unsigned *probe, hipStream_t s);
 hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
                                     double *vf, double *vb, hipStream_t s);
 // ---- reference-order mode (PNP_OPT_SEQ_ORDER, seq_order.hip) ----------------------------------

@@ -1741,6 +1741,83 @@ __global__ __launch_bounds__(kRedBlock) void k_reduce(const double *__restrict__
   }
 }
 
+// Multi-workgroup form for long partial arrays (the SpMV's two partials per 256-row workgroup at
+// config 5: ~23,000, which one workgroup summed in two dependent passes, 12.3 us for
+// k_reduce<2,1>, profiles/r05/final/bicg_split.txt).  G workgroups each sum a contiguous slice
+// of the partial indices (every thread its kRedMwPer loads back to back, then the block tree),
+// publish the slice sums with agent-scope stores and take a ticket; the workgroup that draws the
+// last ticket sums the G slice sums in slice order, derives and re-arms the ticket.  The sums are
+// deterministic for a given (np, G): fixed slices, fixed trees, fixed final order.
+// mw = [ticket word (8 B) | slice sums, G * (KA + KB) doubles], zeroed once by the context.
+constexpr int kRedMwBlock = 256;
+constexpr int kRedMwPer = 6;    // partials per thread and slice
+constexpr int kRedMwMax = 64;   // workgroups at most (mw holds 1 + 64 * 5 doubles)
+constexpr int kRedMwMin = 8192; // below this many partials the one-workgroup k_reduce
+
+template <int KA, int KB>
+__global__ __launch_bounds__(kRedMwBlock) void k_reduce_mw(const double *__restrict__ pa, int npa,
+                                                           const double *__restrict__ pb, int npb,
+                                                           Scalars *__restrict__ S, int stage,
+                                                           double *mw) {
+  constexpr int K = KA + KB;
+  if (S->done && stage != 0 && stage != 10) {  // uniform: S changes only after the last ticket
+    if (stage == 4 && blockIdx.x == 0 && threadIdx.x == 0) S->xpend = 0;
+    return;
+  }
+  const int np = npa > npb ? npa : npb;
+  const int per = (np + int(gridDim.x) - 1) / int(gridDim.x);
+  const int lo = int(blockIdx.x) * per, hi = min(np, lo + per);
+  double acc[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) acc[j] = 0;
+  for (int i0 = lo + int(threadIdx.x); i0 < hi; i0 += kRedMwPer * kRedMwBlock) {
+    double va[kRedMwPer][K];
+#pragma unroll
+    for (int u = 0; u < kRedMwPer; u++) {
+      const int i = i0 + u * kRedMwBlock;
+#pragma unroll
+      for (int j = 0; j < KA; j++) va[u][j] = (i < hi && i < npa) ? pa[size_t(i) * KA + j] : 0.0;
+#pragma unroll
+      for (int j = 0; j < KB; j++)
+        va[u][KA + j] = (i < hi && i < npb) ? pb[size_t(i) * KB + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kRedMwPer; u++)
+#pragma unroll
+      for (int j = 0; j < K; j++) acc[j] += va[u][j];
+  }
+  double out[K];
+  block_sum<K, kRedMwBlock>(acc, out);
+  unsigned *ticket = reinterpret_cast<unsigned *>(mw);
+  double *slices = mw + 1;
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < K; j++)
+      __hip_atomic_store(slices + size_t(blockIdx.x) * K + j, out[j], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double v[K];
+#pragma unroll
+  for (int j = 0; j < K; j++)
+    v[j] = int(threadIdx.x) < int(gridDim.x)
+               ? __hip_atomic_load(slices + size_t(threadIdx.x) * K + j, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT)
+               : 0.0;
+  block_sum<K, kRedMwBlock>(v, out);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < K; j++) S->red[j] = out[j];
+    if (stage >= 0) derive(S, stage);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void k_derive(Scalars *S, int stage) {
   if (threadIdx.x == 0) derive(S, stage);
 }
@@ -2419,8 +2496,26 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
   return hipGetLastError();
 }
 
+// the multi-workgroup grid for np partials, or 0 for the one-workgroup k_reduce
+static int reduce_mw_grid(int np, const double *mw) {
+  if (!mw || np < kRedMwMin) return 0;
+  const int g = (np + kRedMwPer * kRedMwBlock - 1) / (kRedMwPer * kRedMwBlock);
+  return g < 2 ? 0 : (g > kRedMwMax ? kRedMwMax : g);
+}
+
 hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, hipStream_t s,
-                         int derive_stage) {
+                         int derive_stage, double *mw) {
+  if (const int G = reduce_mw_grid(nparts, mw)) {
+    const dim3 g(G), b(kRedMwBlock);
+    switch (k) {
+      case 1: hipLaunchKernelGGL((k_reduce_mw<1, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage, mw); break;
+      case 2: hipLaunchKernelGGL((k_reduce_mw<2, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage, mw); break;
+      case 3: hipLaunchKernelGGL((k_reduce_mw<3, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage, mw); break;
+      case 4: hipLaunchKernelGGL((k_reduce_mw<4, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage, mw); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   const dim3 g(1), b(kRedBlock);
   switch (k) {
     case 1: hipLaunchKernelGGL((k_reduce<1, 0>), g, b, 0, s, partials, nparts, nullptr, 0, S, derive_stage); break;
@@ -2433,7 +2528,21 @@ hipError_t launch_reduce(const double *partials, int nparts, int k, Scalars *S, 
 }
 
 hipError_t launch_reduce2(const double *pa, int npa, int ka, const double *pb, int npb, int kb,
-                          Scalars *S, hipStream_t s, int derive_stage) {
+                          Scalars *S, hipStream_t s, int derive_stage, double *mw) {
+  if (const int G = reduce_mw_grid(npa > npb ? npa : npb, mw)) {
+    const dim3 g(G), b(kRedMwBlock);
+    if (ka == 2 && kb == 1)
+      hipLaunchKernelGGL((k_reduce_mw<2, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage, mw);
+    else if (ka == 1 && kb == 1)
+      hipLaunchKernelGGL((k_reduce_mw<1, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage, mw);
+    else if (ka == 2 && kb == 2)
+      hipLaunchKernelGGL((k_reduce_mw<2, 2>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage, mw);
+    else if (ka == 3 && kb == 2)
+      hipLaunchKernelGGL((k_reduce_mw<3, 2>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage, mw);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   const dim3 g(1), b(kRedBlock);
   if (ka == 2 && kb == 1)
     hipLaunchKernelGGL((k_reduce<2, 1>), g, b, 0, s, pa, npa, pb, npb, S, derive_stage);

@@ -141,6 +141,26 @@ __device__ __forceinline__ unsigned long long nat_ld(const unsigned long long *p
   return __hip_atomic_load(p, __ATOMIC_RELAXED, SCOPE);
 }
 
+// Co-residency probe (ssor_natural_flow_resident): the head and chain kernels launched with their
+// full grid and a negative u0 / bwd only check in -- thread 0 of every workgroup adds one to w[0]
+// and waits until the whole grid has arrived.  A grid that is not resident at once cannot arrive
+// in full: its waiting workgroups give up after kNatProbeTimeout and set w[1], so the probe always
+// drains.  The same kernel, so the same registers and LDS: the probe measures the residency the
+// dataflow launch relies on (the occupancy query can over-report by a block per CU, §0.4).
+constexpr unsigned long long kNatProbeTimeout = 2000000ull;  // wall_clock64 ticks: 20 ms
+__device__ __forceinline__ void nat_probe(unsigned *w) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+    if (wall_clock64() - t0 > kNatProbeTimeout) {
+      __hip_atomic_store(w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 // PAD > 0: the workgroup reserves PAD bytes of LDS it never uses, so that at most one workgroup
 // runs per CU (the sparse tail grid, below).  KS: entries per lane and pass (KS * kL per row and
 // pass); rows longer than that take several passes, each a full load -> poll round trip.  KS = 4
@@ -156,7 +176,11 @@ __global__ void __launch_bounds__(BLK)
                     int spec = 0) {
   if constexpr (PAD > 0) {
     __shared__ char pad[PAD];
-    if (u0 < 0) reinterpret_cast<volatile char *>(pad)[threadIdx.x] = 1;  // never: u0 >= 0
+    if (u0 < -1) reinterpret_cast<volatile char *>(pad)[threadIdx.x] = 1;  // never: u0 >= -1
+  }
+  if (u0 < 0) {  // co-residency probe
+    nat_probe(abort_word);
+    return;
   }
   const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
   const int G = gridDim.x * (BLK / 64);
@@ -293,6 +317,10 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4)))
                     const int4 *__restrict__ info_b, const int *__restrict__ ecol_b,
                     const double *__restrict__ val, const double *__restrict__ d,
                     unsigned long long *vf, unsigned long long *vb, unsigned *abort_word) {
+  if (u0 < 0) {  // co-residency probe
+    nat_probe(abort_word);
+    return;
+  }
   const int lane = threadIdx.x % 64, t = lane / kL, j = lane % kL, base = lane - j;
   const int G = gridDim.x * (BLK / 64);
   // wave-uniform (readfirstlane): the unit records become scalar loads, off the vector counter
@@ -497,6 +525,10 @@ __global__ void __launch_bounds__(64)
                      unsigned long long *vf, unsigned long long *vb, int bwd,
                      unsigned *abort_word) {
   constexpr int D = kChainD, A = kChainA;
+  if (bwd < 0) {  // co-residency probe
+    nat_probe(abort_word);
+    return;
+  }
   const int lane = threadIdx.x;
   const int p0 = gptr[blockIdx.x], len = gptr[blockIdx.x + 1] - p0;
   if (len <= 0) return;
@@ -602,9 +634,14 @@ int ssor_natural_chain_capacity() {
   return cus * std::max(1, per);
 }
 
-hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
-                                    double *vf, double *vb, hipStream_t s) {
-  static int grid = [] {
+// the dataflow launch's configuration (process-wide: grid from the occupancy query, A/B knobs)
+struct NatFlowCfg {
+  int grid, cus, tail_wpc, spec;
+  bool pipe, ks4;
+};
+static const NatFlowCfg &nat_flow_cfg() {
+  static const NatFlowCfg c = [] {
+    NatFlowCfg k{};
     int dev = 0, cus = 0, per = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -620,37 +657,68 @@ hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, 
     // 4 workgroups per CU (16 waves): fewer pollers than the occupancy allows and enough for
     // the wide levels (PNP config 3: 2.25 ms per application against 2.36 at the occupancy, 2.94
     // at 1; profiles/r04/nat_wg*_r4d.log).  PNP_NAT_FLOW_WG_PER_CU overrides (capped at the
-    // occupancy)
+    // occupancy).  ssor_natural_flow_resident() checks the result on the device.
     const char *ev = std::getenv("PNP_NAT_FLOW_WG_PER_CU");
     per = std::min(per, (ev && std::atoi(ev) > 0) ? std::atoi(ev) : 4);
-    return std::max(1, cus * std::max(1, per));
+    k.grid = std::max(1, cus * std::max(1, per));
+    k.cus = std::max(1, cus);
+    // PNP_NAT_PIPE=0: the head as the unpipelined flow kernel (A/B)
+    ev = std::getenv("PNP_NAT_PIPE");
+    k.pipe = !(ev && std::atoi(ev) == 0);
+    // PNP_NAT_FLOW_KS4=1: rows of 25-32 entries in one pass of 32 instead of two of 24 (A/B knob,
+    // off: PNP config 3 1.584 against 1.553 ms per application, profiles/r05/nat_ks4_r5h.log)
+    ev = std::getenv("PNP_NAT_FLOW_KS4");
+    k.ks4 = ev && std::atoi(ev) == 1;
+    // PNP_NAT_SPEC=1: forward head units try plain loads first (A/B knob, default off)
+    ev = std::getenv("PNP_NAT_SPEC");
+    k.spec = (ev && std::atoi(ev) != 0) ? 1 : 0;
+    ev = std::getenv("PNP_NAT_TAIL_WPC");
+    k.tail_wpc = ev ? std::max(0, std::atoi(ev)) : 0;
+    return k;
   }();
-  static const int cus = [] {
-    int dev = 0, c = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max(1, c);
-  }();
-  // PNP_NAT_PIPE=0: the head as the unpipelined flow kernel (A/B)
-  static const bool pipe = [] {
-    const char *ev = std::getenv("PNP_NAT_PIPE");
-    return !(ev && std::atoi(ev) == 0);
-  }();
-  // PNP_NAT_FLOW_KS4=1: rows of 25-32 entries in one pass of 32 instead of two of 24 (A/B knob,
-  // off: PNP config 3 1.584 against 1.553 ms per application, profiles/r05/nat_ks4_r5h.log)
-  static const bool ks4 = [] {
-    const char *ev = std::getenv("PNP_NAT_FLOW_KS4");
-    return ev && std::atoi(ev) == 1;
-  }();
-  // PNP_NAT_SPEC=1: forward head units try plain loads first (A/B knob, default off)
-  static const int spec = [] {
-    const char *ev = std::getenv("PNP_NAT_SPEC");
-    return (ev && std::atoi(ev) != 0) ? 1 : 0;
-  }();
-  static const int tail_wpc = [] {
-    const char *ev = std::getenv("PNP_NAT_TAIL_WPC");
-    return ev ? std::max(0, std::atoi(ev)) : 0;
-  }();
+  return c;
+}
+
+int ssor_natural_flow_resident(const NatFlow &F, unsigned *probe, hipStream_t s) {
+  const NatFlowCfg &C = nat_flow_cfg();
+  unsigned h[2] = {0, 0};
+  auto run = [&](auto launch) -> int {
+    if (hipMemsetAsync(probe, 0, 2 * sizeof(unsigned), s) != hipSuccess) return -1;
+    launch();
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (hipMemcpyAsync(h, probe, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return -1;
+    return h[1] == 0 && h[0] >= 1 ? 1 : 0;
+  };
+  int ok = run([&] {
+    if (F.max_width <= kC && C.pipe)
+      hipLaunchKernelGGL(k_ssor_nat_pipe<kB>, dim3(C.grid), dim3(kB), 0, s, F.units, -1, 0, 0,
+                         F.fwd.info, F.fwd.ecol, F.bwd.info, F.bwd.ecol, nullptr, nullptr, nullptr,
+                         nullptr, probe);
+    else if (F.max_width <= 4 * kL && C.ks4)
+      hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT, 0, 4>), dim3(C.grid),
+                         dim3(kB), 0, s, F.units, -1, 0, 0, F.fwd.info, F.fwd.ecol, F.bwd.info,
+                         F.bwd.ecol, nullptr, nullptr, nullptr, nullptr, probe, 0);
+    else
+      hipLaunchKernelGGL((k_ssor_nat_flow<kB, __HIP_MEMORY_SCOPE_AGENT>), dim3(C.grid), dim3(kB), 0,
+                         s, F.units, -1, 0, 0, F.fwd.info, F.fwd.ecol, F.bwd.info, F.bwd.ecol,
+                         nullptr, nullptr, nullptr, nullptr, probe, 0);
+  });
+  const int ng = std::max(F.chain_f.ngroups, F.chain_b.ngroups);
+  if (ok == 1 && ng > 0)
+    ok = run([&] {
+      hipLaunchKernelGGL(k_ssor_nat_chain, dim3(ng), dim3(64), 0, s, F.chain_f.gptr, F.chain_f.rec,
+                         F.chain_f.ecode, 0, nullptr, nullptr, nullptr, nullptr, -1, probe);
+    });
+  return ok;
+}
+
+hipError_t launch_ssor_natural_flow(const NatFlow &F, int n, const double *val, const double *d,
+                                    double *vf, double *vb, hipStream_t s) {
+  const NatFlowCfg &C = nat_flow_cfg();
+  const int grid = C.grid, cus = C.cus, tail_wpc = C.tail_wpc, spec = C.spec;
+  const bool pipe = C.pipe, ks4 = C.ks4;
   // both result vectors to the pending pattern in one launch (two memsets cost four fill launches,
   // ~23 us at config 3, profiles/r05/nat_split_r5d.txt)
   if (n > 0)

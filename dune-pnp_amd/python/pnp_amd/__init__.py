@@ -34,7 +34,7 @@ OP_PNP, OP_PNP_IMPLICIT_EULER, OP_PB, OP_DIFF, OP_DIFF_IMPLICIT_EULER, OP_POISSO
 PREC_NONE, PREC_SSOR, PREC_ILU0, PREC_JACOBI, PREC_AMG, PREC_SSOR_NATURAL = range(6)
 METHOD_BICGSTAB, METHOD_CG = 0, 1
 (OPT_ILU_F32, OPT_ILU_FUSED_FACTOR, OPT_JAC_FD, OPT_BICG_TWORED, OPT_AMG_FALLBACK,
- OPT_GRAPH, OPT_SEQ_ORDER, OPT_ILU_FLOW, OPT_NAT_FLOW) = 1, 2, 3, 4, 5, 6, 7, 8, 9
+ OPT_GRAPH, OPT_SEQ_ORDER, OPT_ILU_FLOW, OPT_NAT_FLOW, OPT_ILU_RETRY) = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
 DEVICE_PTRS, JAC_FD = 1, 2
 CREATE_ABSORB_THIN_COLOR = 1
 PREC_BY_NAME = {"none": PREC_NONE, "nonprec": PREC_NONE, "ssor": PREC_SSOR, "ilu0": PREC_ILU0,
@@ -225,7 +225,7 @@ class _NewtonResult(C.Structure):
                 ("linear_iterations", C.c_int32), ("status", C.c_int32),
                 ("first_defect", C.c_double), ("defect", C.c_double), ("elapsed", C.c_double),
                 ("assemble_seconds", C.c_double), ("solve_seconds", C.c_double),
-                ("linear_fallbacks", C.c_int32)]
+                ("linear_fallbacks", C.c_int32), ("precision_retries", C.c_int32)]
 
 
 class _Timers(C.Structure):

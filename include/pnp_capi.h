@@ -424,7 +424,14 @@ enum {
    * concurrently (the dataflow needs every workgroup of its grid resident).  Both schedules give
    * the same results bit for bit; pnp_info.nat_flow_applies / nat_level_applies count them.  The
    * environment variable PNP_NAT_FLOW=0 turns the automatic choice off. */
-  PNP_OPT_NAT_FLOW = 9
+  PNP_OPT_NAT_FLOW = 9,
+  /* 1 (default): pnp_newton re-solves a Newton step whose BiCGSTAB with reduced-precision ILU(0)
+   * factors (PNP_OPT_ILU_F32 = 1, 2 or 3; PNP_PREC_ILU0, or the AMG's ILU(0) smoother) broke down
+   * or stopped unconverged, with the factors in fp64 -- ISTL's own SeqILU0 precision -- and keeps
+   * fp64 for the rest of that call (pnp_newton_result.precision_retries).  A rounded
+   * preconditioner is a different M; the retry makes the fp64 preconditioner the fallback
+   * whenever the cheaper one stalls.  0: a failed solve ends Newton as in ISTL. */
+  PNP_OPT_ILU_RETRY = 10
 };
 int pnp_set_option(pnp_ctx *ctx, int32_t option, int64_t value);
 
@@ -465,6 +472,10 @@ typedef struct {
       whose AMG-preconditioned solve failed (diverged: ||r|| > 1e10 ||r0||, breakdown or maxit)
       and were re-solved with the AMG's level-0 smoother alone; linear_iterations counts both
       solves.  Off by default: a failed AMG solve ends Newton like any linear-solver failure. */
+  int32_t precision_retries; /* PNP_OPT_ILU_RETRY: Newton steps whose linear solve with
+      reduced-precision ILU(0) factors (PNP_OPT_ILU_F32 1..3; PNP_PREC_ILU0, or PNP_PREC_AMG with
+      the ILU(0) smoother) broke down or did not converge and were re-solved with fp64 factors;
+      the rest of that pnp_newton call then keeps fp64 factors.  linear_iterations counts both. */
 } pnp_newton_result;
 int pnp_newton(pnp_ctx *ctx, double *u, const pnp_newton_opts *opts, pnp_newton_result *res);
 /* per-step record of the last pnp_newton on ctx (PDELab Newton's verbose per-step output,

@@ -918,6 +918,19 @@ int orc_num_threads(void) {
  * order, not ISTL's; the tests leave it off and keep the serial order) */
 static int g_par = 0;
 void orc_set_parallel(int on) { g_par = on; }
+static int g_bj = 0, g_bj_nf = 1; /* block-Jacobi SSOR / ILU(0): blocks, fields per vertex */
+void orc_set_block_jacobi(int nblocks, int nfields) {
+  g_bj = nblocks > 1 ? nblocks : 0;
+  g_bj_nf = nfields > 0 ? nfields : 1;
+}
+
+static double wtime(void) {
+#ifdef _OPENMP
+  return omp_get_wtime();
+#else
+  return 0.0;
+#endif
+}
 
 void orc_spmv(const orc_csr *A, const double *x, double *y) {
 #pragma omp parallel for schedule(static) if (g_par)
@@ -944,12 +957,43 @@ typedef struct {
   const orc_csr *A;
   orc_csr LU; /* ILU0 factors (diag stored inverted) */
   int *diag;
+  int nb, nv;  /* block-Jacobi: blocks (0: sequential) and vertices per field */
+  orc_csr B;   /* block-Jacobi: A without the couplings between blocks */
 } prec_t;
+
+static int bj_block(int nb, int nv, int i) { return (int)((long long)(i % nv) * nb / nv); }
 
 static void prec_init(prec_t *P, const orc_csr *A, int kind) {
   P->kind = kind;
   P->A = A;
+  P->nb = 0;
   memset(&P->LU, 0, sizeof P->LU);
+  memset(&P->B, 0, sizeof P->B);
+  if (g_bj > 1 && (kind == ORC_PREC_SSOR || kind == ORC_PREC_ILU0) && A->n % g_bj_nf == 0 &&
+      A->n / g_bj_nf >= g_bj) {
+    /* the rank-local matrices of a NOVLP backend: keep only couplings inside a row's block */
+    int nb = g_bj, nv = A->n / g_bj_nf;
+    orc_csr *B = &P->B;
+    B->n = A->n;
+    B->rowptr = (int *)malloc(sizeof(int) * (A->n + 1));
+    B->col = (int *)malloc(sizeof(int) * A->nnz);
+    B->val = (double *)malloc(sizeof(double) * A->nnz);
+    int k2 = 0;
+    B->rowptr[0] = 0;
+    for (int i = 0; i < A->n; i++) {
+      int bi = bj_block(nb, nv, i);
+      for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++)
+        if (bj_block(nb, nv, A->col[k]) == bi) {
+          B->col[k2] = A->col[k];
+          B->val[k2++] = A->val[k];
+        }
+      B->rowptr[i + 1] = k2;
+    }
+    B->nnz = k2;
+    P->A = A = B;
+    P->nb = nb;
+    P->nv = nv;
+  }
   P->diag = (int *)malloc(sizeof(int) * A->n);
   for (int i = 0; i < A->n; i++) {
     P->diag[i] = -1;
@@ -989,7 +1033,24 @@ static void prec_init(prec_t *P, const orc_csr *A, int kind) {
 static void prec_free(prec_t *P) {
   free(P->diag);
   if (P->LU.val) free(P->LU.val);
+  if (P->B.rowptr) orc_csr_free(&P->B);
 }
+
+/* rows of block b in increasing order: field-major, each field's vertex range of the block */
+#define BJ_ROWS(P, b, i, BODY)                                                               \
+  do {                                                                                       \
+    int v0_ = (int)(((long long)(b) * (P)->nv + (P)->nb - 1) / (P)->nb);                    \
+    int v1_ = (int)(((long long)((b) + 1) * (P)->nv + (P)->nb - 1) / (P)->nb);              \
+    for (int f_ = 0; f_ < (P)->A->n / (P)->nv; f_++)                                         \
+      for (int i = f_ * (P)->nv + v0_; i < f_ * (P)->nv + v1_; i++) BODY                    \
+  } while (0)
+#define BJ_ROWS_REV(P, b, i, BODY)                                                           \
+  do {                                                                                       \
+    int v0_ = (int)(((long long)(b) * (P)->nv + (P)->nb - 1) / (P)->nb);                    \
+    int v1_ = (int)(((long long)((b) + 1) * (P)->nv + (P)->nb - 1) / (P)->nb);              \
+    for (int f_ = (P)->A->n / (P)->nv - 1; f_ >= 0; f_--)                                    \
+      for (int i = f_ * (P)->nv + v1_ - 1; i >= f_ * (P)->nv + v0_; i--) BODY               \
+  } while (0)
 
 /* v = W^{-1} d, v is zero on entry (BiCGSTAB sets y = 0 before _prec.apply) */
 static void prec_apply(const prec_t *P, double *v, const double *d) {
@@ -999,6 +1060,35 @@ static void prec_apply(const prec_t *P, double *v, const double *d) {
     for (int i = 0; i < n; i++) v[i] += 1.0 * d[i];
   } else if (P->kind == ORC_PREC_JACOBI) {
     for (int i = 0; i < n; i++) v[i] = d[i] / A->val[P->diag[i]];
+  } else if (P->nb > 1 && P->kind == ORC_PREC_SSOR) { /* each block's SeqSSOR, in parallel */
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int b = 0; b < P->nb; b++) {
+      BJ_ROWS(P, b, i, {
+        double rhs = d[i];
+        for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++) rhs -= A->val[k] * v[A->col[k]];
+        v[i] += 1.0 * (rhs / A->val[P->diag[i]]);
+      });
+      BJ_ROWS_REV(P, b, i, {
+        double rhs = d[i];
+        for (int k = A->rowptr[i]; k < A->rowptr[i + 1]; k++) rhs -= A->val[k] * v[A->col[k]];
+        v[i] += 1.0 * (rhs / A->val[P->diag[i]]);
+      });
+    }
+  } else if (P->nb > 1) { /* each block's ILU(0) solve, in parallel */
+    const orc_csr *L = &P->LU;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int b = 0; b < P->nb; b++) {
+      BJ_ROWS(P, b, i, {
+        double s = d[i];
+        for (int k = L->rowptr[i]; k < P->diag[i]; k++) s -= L->val[k] * v[L->col[k]];
+        v[i] = s;
+      });
+      BJ_ROWS_REV(P, b, i, {
+        double s = v[i];
+        for (int k = P->diag[i] + 1; k < L->rowptr[i + 1]; k++) s -= L->val[k] * v[L->col[k]];
+        v[i] = s * L->val[P->diag[i]];
+      });
+    }
   } else if (P->kind == ORC_PREC_SSOR) { /* SeqSSOR(A, 1, 1.0): bsorf then bsorb */
     for (int i = 0; i < n; i++) {
       double rhs = d[i];
@@ -1045,8 +1135,11 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
   double *y = (double *)calloc(n, sizeof(double));
   double *rt = (double *)malloc(sizeof(double) * n);
   prec_t P;
-  prec_init(&P, A, prec);
   memset(res, 0, sizeof *res);
+  double t_setup = wtime();
+  prec_init(&P, A, prec);
+  res->setup_seconds = wtime() - t_setup;
+  double t_iter = wtime();
   /* r = b - A x */
   orc_spmv(A, x, t);
   for (int i = 0; i < n; i++) r[i] -= t[i];
@@ -1100,6 +1193,7 @@ void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, doubl
     norm = sqrt(dot(n, r, r));
     if (norm < reduction * norm_0 || norm < 1e-30) { res->converged = 1; break; }
   }
+  res->iter_seconds = wtime() - t_iter;
   if (it > maxit) it = maxit;
   res->it_half = it;
   res->iterations = (int)ceil(it);

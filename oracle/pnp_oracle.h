@@ -154,12 +154,20 @@ typedef struct {
   double reduction;
   double defect0, defect;
   int breakdown; /* 1 rho, 2 omega, 3 h */
+  double setup_seconds; /* preconditioner construction (ILU(0) factorisation, block split) */
+  double iter_seconds;  /* the iteration loop (wall clock, omp_get_wtime) */
 } orc_solve_result;
 
 void orc_spmv(const orc_csr *A, const double *x, double *y);
 /* ISTL BiCGSTABSolver::apply(x, b, res): x overwritten (start value = x), b overwritten. */
 /* 1: OpenMP row-parallel SpMV / dots / updates in orc_bicgstab (all-core CPU baseline) */
 void orc_set_parallel(int on);
+/* nblocks > 1: SSOR and ILU(0) act block-Jacobi on nblocks vertex ranges (row f*nv + v is in
+ * block v*nblocks/nv; couplings between blocks dropped), the blocks swept in parallel -- what the
+ * reference's ISTLBackend_NOVLP_* applies with nblocks MPI ranks, each rank's SeqSSOR / SeqILU0
+ * on its own rows (src/stationary_pnp_from_pb.hh:168-169), here with contiguous vertex ranges
+ * instead of the reference's load-balanced partition.  0 or 1: the sequential preconditioner. */
+void orc_set_block_jacobi(int nblocks, int nfields);
 void orc_bicgstab(const orc_csr *A, int prec, double reduction, int maxit, double *x, double *b,
                   orc_solve_result *res);
 /* v = W^{-1} d, one application of preconditioner prec from v = 0 (ISTL SeqSSOR / SeqILU0 /

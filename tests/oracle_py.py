@@ -53,7 +53,8 @@ class OrcPk(C.Structure):
 class OrcSolveResult(C.Structure):
     _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("it_half", C.c_double),
                 ("reduction", C.c_double), ("defect0", C.c_double), ("defect", C.c_double),
-                ("breakdown", C.c_int)]
+                ("breakdown", C.c_int), ("setup_seconds", C.c_double),
+                ("iter_seconds", C.c_double)]
 
 
 class OrcNewtonOpts(C.Structure):

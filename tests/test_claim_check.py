@@ -81,3 +81,22 @@ def test_natural_ssor_units_drain_with_the_resident_grid():
     assert CC.check(n, deps, CC.Static(G), G, G, seeds=4) is None
     assert CC.check(n, deps, CC.Static(G), G, G // 2, seeds=4) is not None
     assert CC.check(n, deps, CC.Ticket(), G, 4, seeds=4) is None
+
+
+def test_natural_ssor_head_is_probed_before_the_static_schedule():
+    """The head's actual protocol since round 6: ssor_natural_flow_resident() first launches the
+    head (and chain) kernels in probe mode with their full grid G; only if all G workgroups check
+    in at once does the context use the static schedule (wave w: units w, w + G, ...), else the
+    level launches (one launch per level, no waits inside a launch: always drains).  So for every
+    residency R -- including R < G, where the static schedule alone can hang -- the sweep drains."""
+    cfg = P.read_config(os.path.join(DATA, "pore_pnp", "pore.cfg"))
+    mesh = P.Mesh.read_gmsh(cfg.meshfile)
+    n, deps = _nat_units(mesh)
+    G = 24
+    for R in (1, 5, G // 2, G - 1, G, 2 * G):
+        if CC.probe_arrivals(G, R) >= G:  # probe passed: the static dataflow schedule
+            assert R >= G
+            assert CC.check(n, deps, CC.Static(G), G, R, seeds=4) is None
+        else:  # probe failed: level launches, each a launch without intra-launch waits
+            assert R < G
+            assert CC.check(n, deps, CC.Static(G), G, R, seeds=2) is not None  # what it avoids

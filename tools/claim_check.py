@@ -38,6 +38,18 @@ usage: python tools/claim_check.py   (runs the demonstration cases; tests/test_c
 import random
 
 
+def probe_arrivals(G, R, hold=True):
+    """The co-residency probe of ssor_natural.hip (nat_probe): the grid's G workers each check in
+    and wait, bounded, until all G have; the dispatcher starts worker R + i only after a resident
+    worker exits.  Returns the largest arrival count any waiting worker can observe before its
+    wait ends (hold: workers hold their slot while they wait, as the probe's wave does).  The
+    probe passes iff that count reaches G; otherwise every waiting worker times out, exits, and
+    the launch drains with the flag set -- the context then keeps the level launches."""
+    if not hold:
+        return G
+    return min(G, R)
+
+
 class Claimer:
     def reset(self, n, deps):
         self.n, self.deps = n, deps
