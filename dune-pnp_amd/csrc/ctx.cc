@@ -292,7 +292,7 @@ struct pnp_ctx {
   DBuf<unsigned char> seq_mask;
   DBuf<int> seq_bptr;
   DBuf<double> seq_bval, seq_phi, seq_cp, seq_cm, seq_xold;
-  DBuf<double> seq_rl, seq_rlo, seq_jl, seq_vec, seq_dotv;
+  DBuf<double> seq_rl, seq_rlt, seq_rlo, seq_jl, seq_jlt, seq_vec, seq_dotv;
   int nat_pat = -1, nat_nf = 0;
   // ion-current observable (pnp_ion_flux): boundary segments handled by this rank (the owner of
   // the segment's lower global vertex), {a, c, opposite vertex, group} in local indices, in
@@ -1480,7 +1480,8 @@ struct pnp_ctx {
     split_of = 0;
     amg_valid = false;
     if (on && degree == 1) {
-      const size_t need = size_t(fd_ne) * 9 * nf * nf;
+      // one-step operators keep two matrices per element (spatial, temporal: fd_jacobian.hip)
+      const size_t need = size_t(fd_ne) * 9 * nf * nf * 2;
       if (fd_jel.n < need) {
         hipError_t e = fd_jel.alloc(need);
         if (e != hipSuccess) return hipfail(e, "fd element matrices");
@@ -2288,53 +2289,69 @@ struct pnp_ctx {
     if ((e = seq_vec.alloc(size_t(SQ_N) * 3 * nv)) != hipSuccess ||
         (e = seq_dotv.alloc(2)) != hipSuccess || (e = seq_rl.alloc(size_t(9) * nt)) != hipSuccess ||
         (e = seq_rlo.alloc(size_t(9) * nt)) != hipSuccess ||
-        (e = seq_jl.alloc(size_t(81) * nt)) != hipSuccess)
+        (e = seq_rlt.alloc(size_t(9) * nt)) != hipSuccess ||
+        (e = seq_jl.alloc(size_t(81) * nt)) != hipSuccess ||
+        (e = seq_jlt.alloc(size_t(81) * nt)) != hipSuccess)
       return hipfail(e, "seq buffers");
     seq_built = true;
     return PNP_OK;
   }
 
-  // per operator: constrained rows, alpha_boundary's terms per row in the order the reference adds
-  // them (boundary intersections in segment order, 2-point Gauss, fields in order; the oracle's
-  // boundary_flux statements: r += scale * (j * psi * factor)), frozen fields
+  // per operator: constrained rows, alpha_boundary's terms per (element, local index) in the order
+  // PDELab adds them into the element's local vector (the oracle's boundary_face statements: the
+  // element's faces in DUNE's order (0,1), (0,2), (1,2), each a boundary intersection when its edge
+  // is a boundary segment, run from its lower to its higher local vertex; 2-point Gauss; fields in
+  // order; every basis function of the element at the face point; rl += scale * (j * phi * factor)),
+  // frozen fields
   int seq_prepare() {
     int rc;
     if ((rc = seq_build())) return rc;
     if (seq_op_valid) return PNP_OK;
     if (seq_cextra) return fail(PNP_E_ARG, "PNP_OPT_SEQ_ORDER: pnp_op_args.c_extra is not supported");
-    const int nv = mesh.nv, n = nseq();
-    std::vector<std::vector<double>> terms(n);
+    const int nt = mesh.nt, nl = 3 * nf;
+    std::vector<std::vector<double>> terms(size_t(nt) * nl);
     const bool bnd = kind == PNP_OP_PNP || kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_PB ||
                      kind == PNP_OP_POISSON;
     if (bnd) {
+      std::unordered_map<long long, int> seg;  // edge -> its (first) boundary segment
+      auto key = [](int a, int b) { return (long long)std::min(a, b) << 32 | unsigned(std::max(a, b)); };
+      for (int b = 0; b < mesh.nb; b++) seg.emplace(key(mesh.bseg[2 * b], mesh.bseg[2 * b + 1]), b);
+      static const int kFaceV[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+      static const double corner[3][2] = {{0.0, 0.0}, {1.0, 0.0}, {0.0, 1.0}};
       const double PI = params.pi;
       const double scale = kind == PNP_OP_PNP_IMPLICIT_EULER ? seq_dt : 1.0;
       const double gt[2] = {0.5 - 0.5 / std::sqrt(3.0), 0.5 + 0.5 / std::sqrt(3.0)};
-      for (int b = 0; b < mesh.nb; b++) {
-        const int v0 = mesh.bseg[2 * b], v1 = mesh.bseg[2 * b + 1];
-        const pnp::Surface &S = params.surf[mesh.bgroup[b]];
-        const double dx = mesh.xy[2 * v1] - mesh.xy[2 * v0],
-                     dy = mesh.xy[2 * v1 + 1] - mesh.xy[2 * v0 + 1];
-        const double len = std::sqrt(dx * dx + dy * dy);
-        for (int q = 0; q < 2; q++) {
-          double factor = 0.5 * len;
-          const double y = mesh.xy[2 * v0 + 1] + gt[q] * dy;
-          if (params.cylindrical) factor *= y * 2 * PI;
-          const double psi[2] = {1.0 - gt[q], gt[q]};
-          for (int f = 0; f < nf; f++) {
-            if (S.btype(f) == 0) continue;  // isDirichlet
-            const double j = S.flux(f);
-            terms[size_t(f) * nv + v0].push_back(scale * (j * psi[0] * factor));
-            terms[size_t(f) * nv + v1].push_back(scale * (j * psi[1] * factor));
+      for (int e = 0; e < nt && !seg.empty(); e++)
+        for (int k = 0; k < 3; k++) {
+          const int ia = kFaceV[k][0], ib = kFaceV[k][1];
+          const int va = mesh.tri[3 * e + ia], vb = mesh.tri[3 * e + ib];
+          const auto it = seg.find(key(va, vb));
+          if (it == seg.end()) continue;
+          const pnp::Surface &S = params.surf[mesh.bgroup[it->second]];
+          const double dx = mesh.xy[2 * vb] - mesh.xy[2 * va],
+                       dy = mesh.xy[2 * vb + 1] - mesh.xy[2 * va + 1];
+          const double len = std::sqrt(dx * dx + dy * dy);
+          for (int q = 0; q < 2; q++) {
+            double factor = 0.5 * len;
+            const double y = mesh.xy[2 * va + 1] + gt[q] * dy;
+            if (params.cylindrical) factor *= y * 2 * PI;
+            const double lx = corner[ia][0] + (corner[ib][0] - corner[ia][0]) * gt[q];
+            const double ly = corner[ia][1] + (corner[ib][1] - corner[ia][1]) * gt[q];
+            const double phi[3] = {1.0 - lx - ly, lx, ly};
+            for (int f = 0; f < nf; f++) {
+              if (S.btype(f) == 0) continue;  // isDirichlet
+              const double j = S.flux(f);
+              for (int i = 0; i < 3; i++)
+                terms[size_t(e) * nl + 3 * f + i].push_back(scale * (j * phi[i] * factor));
+            }
           }
         }
-      }
     }
-    std::vector<int> bptr(n + 1, 0);
+    std::vector<int> bptr(size_t(nt) * nl + 1, 0);
     std::vector<double> bval;
-    for (int R = 0; R < n; R++) {
-      bptr[R + 1] = bptr[R] + int(terms[R].size());
-      bval.insert(bval.end(), terms[R].begin(), terms[R].end());
+    for (size_t q = 0; q < terms.size(); q++) {
+      bptr[q + 1] = bptr[q] + int(terms[q].size());
+      bval.insert(bval.end(), terms[q].begin(), terms[q].end());
     }
     if ((rc = upv(seq_bptr, bptr, "seq boundary")) || (rc = upv(seq_bval, bval, "seq boundary")))
       return rc;
@@ -2378,11 +2395,12 @@ struct pnp_ctx {
     int rc;
     if ((rc = seq_prepare())) return rc;
     const bool old = kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_DIFF_IMPLICIT_EULER;
-    hipError_t e = pnp::launch_seq_element(seq_mesh(), seq_op(), x, 0, seq_rl.p, seq_rlo.p,
-                                           seq_jl.p, stream);
+    hipError_t e = pnp::launch_seq_element(seq_mesh(), seq_op(), x, 0, seq_rl.p, seq_rlt.p,
+                                           seq_rlo.p, seq_jl.p, seq_jlt.p, seq_bptr.p, seq_bval.p,
+                                           stream);
     if (e == hipSuccess)
-      e = pnp::launch_seq_residual_gather(seq_mesh(), nf, old ? 1 : 0, seq_rl.p, seq_rlo.p,
-                                          seq_bptr.p, seq_bval.p, seq_mask.p, r, stream);
+      e = pnp::launch_seq_residual_gather(seq_mesh(), nf, old ? 1 : 0, seq_rl.p, seq_rlt.p,
+                                          seq_rlo.p, seq_mask.p, r, stream);
     return e == hipSuccess ? PNP_OK : hipfail(e, "seq residual");
   }
   // the CSR view = J(x) (GridOperator::jacobian + constrained rows to identity); fd: PDELab's
@@ -2390,10 +2408,13 @@ struct pnp_ctx {
   int seq_jacobian(const double *x, bool fd) {
     int rc;
     if ((rc = seq_prepare()) || (rc = csr_structure())) return rc;
+    const bool onestep = kind == PNP_OP_PNP_IMPLICIT_EULER || kind == PNP_OP_DIFF_IMPLICIT_EULER;
     hipError_t e = pnp::launch_seq_element(seq_mesh(), seq_op(), x, fd ? 2 : 1, seq_rl.p,
-                                           seq_rlo.p, seq_jl.p, stream);
+                                           seq_rlt.p, seq_rlo.p, seq_jl.p, seq_jlt.p, seq_bptr.p,
+                                           seq_bval.p, stream);
     if (e == hipSuccess)
-      e = pnp::launch_seq_jacobian_gather(seq_mesh(), nf, seq_jl.p, csr_rowptr.p, csr_col.p,
+      e = pnp::launch_seq_jacobian_gather(seq_mesh(), nf, seq_jl.p, onestep ? seq_jlt.p : nullptr,
+                                          csr_rowptr.p, csr_col.p,
                                           seq_mask.p, csr_val.p, stream);
     if (e != hipSuccess) return hipfail(e, "seq jacobian");
     assembled = true;
@@ -3019,6 +3040,10 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     std::vector<uint16_t> li, ui;
     const bool ok = lists(lcl, lco, lcol, 0, rowL, lp, ll, li) &&
                     lists(ucl, uco, ucol, 1, rowU, up2, ul, ui);
+    // padding past the last chunk: the sweeps' branch-free prefetch (linalg.hip ILU_PF) reads slot
+    // 0 of a chunk whose rows have no slots at all
+    li.resize(li.size() + 64 * 16, 0xFFFF);
+    ui.resize(ui.size() + 64 * 16, 0xFFFF);
     int mx = 0;
     for (size_t k = 0; ok && k + 1 < lp.size(); k++) mx = std::max(mx, lp[k + 1] - lp[k]);
     for (size_t k = 0; ok && k + 1 < up2.size(); k++) mx = std::max(mx, up2[k + 1] - up2[k]);

@@ -17,6 +17,12 @@
 //                 element matrices that touch it in ascending element order (BCRSMatrix
 //                 accumulation order), the block pattern's values stored as they are (kPat*FD).
 //
+// One-step operators (implicit Euler: PnpOperator + PnpTOperator, DiffusionOperator +
+// DiffusionTOperator under OneStepGridOperator, src/instationary_pnp_from_pb.hh:324): each local
+// operator has its own NumericalJacobianVolume, so per element the spatial operator's matrix
+// (weight dt: dt ((r_s(u + delta e_j) - r_s(u)) / delta)) and the temporal operator's are two
+// matrices, added into the BCRS matrix one after the other (the oracle's orc_op_jacobian).
+//
 // The analytic Jacobian (assemble.hip) stays the default; this mode exists for bit-level parity
 // with the reference's FD Jacobian.  Polynomial operators (PNP, PnpT, Poisson, Diffusion) give
 // the oracle's FD matrix to the last bits; PB goes through sinh, whose device and host libm results
@@ -252,8 +258,43 @@ __device__ void op_volume(const ElGeo &G, const FdArgs &a, const double *f0, con
   }
 }
 
-// NumericalJacobianVolume::jacobian_volume, epsilon 1e-7, for one element per thread:
-// jel[e][i][j] = (r(u + delta_j e_j) - r(u))_i / delta_j
+// the one-step operators' spatial and temporal element residuals, apart
+template <int NF>
+__device__ void op_spatial(const ElGeo &G, const FdArgs &a, const double *f0, const double *xl,
+                           double *rl) {
+  for (int i = 0; i < 3 * NF; i++) rl[i] = 0.0;
+  if constexpr (NF == 3)
+    lop_pnp(G, a, xl, rl);
+  else
+    lop_diff(G, a, f0, xl, rl);
+}
+template <int NF>
+__device__ void op_temporal(const ElGeo &G, const FdArgs &a, const double *xl, double *rl) {
+  for (int i = 0; i < 3 * NF; i++) rl[i] = 0.0;
+  if constexpr (NF == 3)
+    lop_pnpt(G, a, xl, rl);
+  else
+    lop_difft(G, xl, rl);
+}
+
+// NumericalJacobianVolume::jacobian_volume, epsilon 1e-7, of the element residual ev, with the
+// weight w of the operator's accumulation view: J[i][j] = w ((r(u + delta_j e_j) - r(u))_i / delta_j)
+template <int NF, typename F>
+__device__ void fd_columns(const double *xl, double w, F &&ev, double *J) {
+  constexpr int NL = 3 * NF;
+  double u[NL], down[NL], up[NL];
+  for (int i = 0; i < NL; i++) u[i] = xl[i];
+  ev(u, down);
+  for (int j = 0; j < NL; j++) {
+    const double delta = 1e-7 * (1.0 + fabs(u[j]));
+    u[j] += delta;
+    ev(u, up);
+    for (int i = 0; i < NL; i++) J[i * NL + j] = w * ((up[i] - down[i]) / delta);
+    u[j] = xl[j];
+  }
+}
+
+// one element per thread: jel[e] (stationary), or jel[2e] (spatial) and jel[2e + 1] (temporal)
 template <int NF>
 __global__ __launch_bounds__(kB) void k_fd_element(int ne, const int *__restrict__ etri,
                                                    const double *__restrict__ xy,
@@ -267,29 +308,29 @@ __global__ __launch_bounds__(kB) void k_fd_element(int ne, const int *__restrict
   const int t[3] = {etri[3 * e], etri[3 * e + 1], etri[3 * e + 2]};
   const ElGeo G = element_geometry(xy + 2 * size_t(t[0]), xy + 2 * size_t(t[1]),
                                    xy + 2 * size_t(t[2]));
-  double xl[NL], u[NL], down[NL], up[NL], f0[3] = {0, 0, 0}, f1[3] = {0, 0, 0};
+  double xl[NL], f0[3] = {0, 0, 0}, f1[3] = {0, 0, 0};
   for (int f = 0; f < NF; f++)
     for (int k = 0; k < 3; k++) xl[3 * f + k] = x[size_t(t[k]) * NF + f];
   if (aux0)
     for (int k = 0; k < 3; k++) f0[k] = aux0[t[k]];
   if (aux1)
     for (int k = 0; k < 3; k++) f1[k] = aux1[t[k]];
-  for (int i = 0; i < NL; i++) u[i] = xl[i];
-  op_volume<NF>(G, a, f0, f1, u, down);
-  double *J = jel + size_t(e) * NL * NL;
-  for (int j = 0; j < NL; j++) {
-    const double delta = 1e-7 * (1.0 + fabs(u[j]));
-    u[j] += delta;
-    op_volume<NF>(G, a, f0, f1, u, up);
-    for (int i = 0; i < NL; i++) J[i * NL + j] = (up[i] - down[i]) / delta;
-    u[j] = xl[j];
+  if (a.kind == OP_PNP_IE || a.kind == OP_DIFF_IE) {
+    double *J = jel + size_t(2 * e) * NL * NL;
+    fd_columns<NF>(xl, a.dt, [&](const double *u, double *r) { op_spatial<NF>(G, a, f0, u, r); },
+                   J);
+    fd_columns<NF>(xl, 1.0, [&](const double *u, double *r) { op_temporal<NF>(G, a, u, r); },
+                   J + NL * NL);
+    return;
   }
+  fd_columns<NF>(xl, 1.0, [&](const double *u, double *r) { op_volume<NF>(G, a, f0, f1, u, r); },
+                 jel + size_t(e) * NL * NL);
 }
 
 // block (row, slot) = sum over its element contributions in ascending element order; cdata per
 // row: for each slot, the count then codes e * 9 + a * 3 + b (row = local vertex a of element e,
 // column = vertex b)
-template <int NF, int PAT>
+template <int NF, int PAT, int TWO = 0>
 __global__ __launch_bounds__(kB) void k_fd_gather(DevLayout L, const long long *__restrict__ rptr,
                                                   const int *__restrict__ cdata,
                                                   const double *__restrict__ jel,
@@ -308,14 +349,17 @@ __global__ __launch_bounds__(kB) void k_fd_gather(DevLayout L, const long long *
     for (int k = 0; k < n; k++) {
       const int code = cdata[p++];
       const int e = code / 9, ab = code % 9, ea = ab / 3, eb = ab % 3;
-      const double *J = jel + size_t(e) * NL * NL;
 #pragma unroll
-      for (int f = 0; f < NF; f++)
+      for (int m = 0; m <= TWO; m++) {  // one-step: the spatial matrix, then the temporal one
+        const double *J = jel + size_t((TWO + 1) * e + m) * NL * NL;
 #pragma unroll
-        for (int g = 0; g < NF; g++) {
-          const int v = pat_index(PAT, f, g);
-          if (v >= 0) acc[v] += J[(3 * f + ea) * NL + 3 * g + eb];
-        }
+        for (int f = 0; f < NF; f++)
+#pragma unroll
+          for (int g = 0; g < NF; g++) {
+            const int v = pat_index(PAT, f, g);
+            if (v >= 0) acc[v] += J[(3 * f + ea) * NL + 3 * g + eb];
+          }
+      }
     }
     double *sb = vals + (size_t(off) + size_t(s) * kRows) * NV;
 #pragma unroll
@@ -346,7 +390,10 @@ hipError_t launch_fd_jacobian(const DevLayout &L, const AsmArgs &aa, int nf, int
     hipLaunchKernelGGL((k_fd_gather<3, kPatPnpFD>), gr, dim3(kB), 0, s, L, rptr, cdata, jel,
                        aa.vals);
   else if (nf == 3 && pat == kPatPnpIEFD)
-    hipLaunchKernelGGL((k_fd_gather<3, kPatPnpIEFD>), gr, dim3(kB), 0, s, L, rptr, cdata, jel,
+    hipLaunchKernelGGL((k_fd_gather<3, kPatPnpIEFD, 1>), gr, dim3(kB), 0, s, L, rptr, cdata, jel,
+                       aa.vals);
+  else if (nf == 1 && aa.kind == OP_DIFF_IE)
+    hipLaunchKernelGGL((k_fd_gather<1, kPatScalar, 1>), gr, dim3(kB), 0, s, L, rptr, cdata, jel,
                        aa.vals);
   else if (nf == 1)
     hipLaunchKernelGGL((k_fd_gather<1, kPatScalar>), gr, dim3(kB), 0, s, L, rptr, cdata, jel,

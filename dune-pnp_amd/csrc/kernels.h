@@ -534,13 +534,16 @@ struct SeqOp {
   double pi = 3.1415, l_b = 1, c0 = 0, tau = 1, dt = 0, z = 0;
   const double *phi = nullptr, *cp = nullptr, *cm = nullptr, *x_old = nullptr;
 };
+// element pass (RLT / JLT: the one-step temporal operator's; bptr / bval: alpha_boundary's terms
+// per (element, local index), CSR over e * nl + i) and the row gathers of seq_order.hip
 hipError_t launch_seq_element(const SeqMesh &M, const SeqOp &P, const double *x, int mode,
-                              double *RL, double *RLO, double *JL, hipStream_t s);
+                              double *RL, double *RLT, double *RLO, double *JL, double *JLT,
+                              const int *bptr, const double *bval, hipStream_t s);
 hipError_t launch_seq_residual_gather(const SeqMesh &M, int nf, int has_old, const double *RL,
-                                      const double *RLO, const int *bptr, const double *bval,
+                                      const double *RLT, const double *RLO,
                                       const unsigned char *mask, double *r, hipStream_t s);
 hipError_t launch_seq_jacobian_gather(const SeqMesh &M, int nf, const double *JL,
-                                      const int *rowptr, const int *col,
+                                      const double *JLT, const int *rowptr, const int *col,
                                       const unsigned char *mask, double *val, hipStream_t s);
 hipError_t launch_seq_spmv(int n, const int *rowptr, const int *col, const double *val,
                            const double *x, double *y, hipStream_t s);

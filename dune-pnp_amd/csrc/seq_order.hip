@@ -3,11 +3,11 @@
 // BiCGSTAB run here takes the same iterates -- and the same iteration counts on chaotic systems --
 // as the oracle's single-rank run.  A parity mode, not a speed mode: the fast path (assemble.hip,
 // linalg.hip) sums in the GPU's orders and its iteration counts agree with the oracle's only as
-// distributions where BiCGSTAB is chaotic.  One known difference from the DUNE
-// program remains in the rounding order: PDELab's local assembler adds alpha_boundary's terms into
-// the element's local vector before it scatters, and its one-step operator weights every
-// accumulated term, while this file (as the oracle) adds all volume terms, then the boundary
-// terms, then scales; parity with the DUNE program itself is unpinned.
+// distributions where BiCGSTAB is chaotic.  Since round 6 the oracle, and this file,
+// restate PDELab's GridOperator accumulation: alpha_boundary's terms go into the element's local
+// vector before its one scatter, and a one-step operator's const residual, spatial and temporal
+// local vectors are separate passes / scatters.  Parity with the DUNE program itself stays
+// unpinned (its grid's vertex order and dune-geometry's tabulated points are not in the tree).
 //
 // What "the reference's order" is, per step (this file is compiled with -ffp-contract=off: no
 // fused multiply-add anywhere, as on the reference's x86-64 build):
@@ -20,11 +20,12 @@
 //    differences (delta = 1e-7 (1 + |x_j|), the mixins inherited at src/pnp_operator.hh:22-27) or
 //    the analytic element Jacobian;
 //  * GridOperator::residual / ::jacobian (PDELab, instantiated at src/stationary_pnp_from_pb.hh:165,
-//    315-321): the global vector / BCRS matrix starts at 0 and every element adds its local block in
-//    element order (k_seq_residual_gather / k_seq_jacobian_gather: one thread per row walks the
-//    row's incident elements in ascending element index, so every entry sees its terms in the
-//    reference's order), then alpha_boundary's terms in boundary-intersection order (host values,
-//    same expressions), then constrained rows become 0 / identity rows;
+//    315-321): the global vector / BCRS matrix starts at 0 (one-step: at the const residual) and
+//    every element adds its local block in element order (k_seq_residual_gather /
+//    k_seq_jacobian_gather: one thread per row walks the row's incident elements in ascending
+//    element index, so every entry sees its terms in the reference's order); an element's local
+//    residual holds alpha_volume and then alpha_boundary of its boundary faces (host values, the
+//    oracle's boundary_face statements); constrained rows become 0 / identity rows;
 //  * ISTL BiCGSTABSolver / CGSolver (dune-istl, src/stationary_pnp_from_pb.hh:168-169,329-331):
 //    BCRSMatrix::mv summed per row in ascending column order (k_seq_spmv), scalar products summed
 //    sequentially from entry 0 (k_seq_dot: one lane), the vector updates as their expressions
@@ -367,15 +368,51 @@ __device__ void jac_difft(const Geo &G, double *J) {
   }
 }
 
-// One thread per element, in the mesh's element order.  mode 0: RL[e] = the element residual of x
-// (and, implicit Euler, RLO[e] = -(the mass of x_old)); 1: JL[e] = the analytic element Jacobian;
-// 2: JL[e] = NumericalJacobianVolume's forward differences of the element residual.
+// One thread per element, in the mesh's element order.  mode 0: RL[e] = the element's local
+// residual -- alpha_volume, then alpha_boundary's terms of its boundary intersections (bval[bptr[e
+// nl + i] .. bptr[e nl + i + 1]), host values in face / quadrature order) added one by one; one-step
+// operators: RL[e] = the spatial operator's (weight dt), RLT[e] = the temporal operator's, RLO[e] =
+// -(the mass of x_old), the const residual; 1: JL[e] = the analytic element Jacobian; 2: JL[e] =
+// NumericalJacobianVolume's forward differences (w ((up - down) / delta)); one-step: JL[e] the
+// spatial operator's (w = dt), JLT[e] the temporal operator's (w = 1).
+__device__ void spatial(const Geo &G, const SeqOp &P, const double *aux, const double *xl,
+                        double *rl) {
+  for (int i = 0; i < 3 * P.nf; i++) rl[i] = 0.0;
+  if (P.nf == 3)
+    lop_pnp(G, P, xl, rl);
+  else
+    lop_diff(G, P, aux, xl, rl);
+}
+__device__ void temporal(const Geo &G, const SeqOp &P, const double *xl, double *rl) {
+  for (int i = 0; i < 3 * P.nf; i++) rl[i] = 0.0;
+  if (P.nf == 3)
+    lop_pnpt(G, P, xl, rl);
+  else
+    lop_difft(G, xl, rl);
+}
+template <typename F>
+__device__ void fd_element(const double *xl, int nl, double w, F &&ev, double *J) {
+  double u[9], down[9], up[9];
+  for (int i = 0; i < nl; i++) u[i] = xl[i];
+  ev(u, down);
+  for (int j = 0; j < nl; j++) {
+    const double delta = 1e-7 * (1.0 + fabs(u[j]));
+    u[j] += delta;
+    ev(u, up);
+    for (int i = 0; i < nl; i++) J[i * nl + j] += w * ((up[i] - down[i]) / delta);
+    u[j] = xl[j];
+  }
+}
+
 __global__ void __launch_bounds__(kB)
     k_seq_element(SeqMesh M, SeqOp P, const double *__restrict__ x, int mode,
-                  double *__restrict__ RL, double *__restrict__ RLO, double *__restrict__ JL) {
+                  double *__restrict__ RL, double *__restrict__ RLT, double *__restrict__ RLO,
+                  double *__restrict__ JL, double *__restrict__ JLT, const int *__restrict__ bptr,
+                  const double *__restrict__ bval) {
   const int e = blockIdx.x * kB + threadIdx.x;
   if (e >= M.nt) return;
   const int nf = P.nf, nl = 3 * nf, nv = M.nv;
+  const bool onestep = P.kind == OP_PNP_IE || P.kind == OP_DIFF_IE;
   const int t[3] = {M.tri[3 * e], M.tri[3 * e + 1], M.tri[3 * e + 2]};
   Geo G;
   geometry(M.xy, t, G);
@@ -392,42 +429,53 @@ __global__ void __launch_bounds__(kB)
     }
   if (mode == 0) {
     double rl[9];
-    volume(G, P, aux, xl, rl);
+    if (onestep) {
+      double rs[9];
+      spatial(G, P, aux, xl, rs);
+      for (int i = 0; i < nl; i++) rl[i] = P.dt * rs[i];
+    } else {
+      volume(G, P, aux, xl, rl);
+    }
+    for (int i = 0; i < nl; i++)
+      for (int k = bptr[size_t(e) * nl + i]; k < bptr[size_t(e) * nl + i + 1]; k++) rl[i] += bval[k];
     for (int i = 0; i < nl; i++) RL[size_t(e) * nl + i] = rl[i];
-    if (P.kind == OP_PNP_IE || P.kind == OP_DIFF_IE) {
-      double xo[9], ro[9];
+    if (onestep) {
+      temporal(G, P, xl, rl);
+      for (int i = 0; i < nl; i++) RLT[size_t(e) * nl + i] = rl[i];
+      double xo[9];
       for (int f = 0; f < nf; f++)
         for (int a = 0; a < 3; a++) xo[3 * f + a] = P.x_old[size_t(f) * nv + t[a]];
-      for (int i = 0; i < nl; i++) ro[i] = 0.0;
-      if (nf == 3)
-        lop_pnpt(G, P, xo, ro);
-      else
-        lop_difft(G, xo, ro);
-      for (int i = 0; i < nl; i++) RLO[size_t(e) * nl + i] = -ro[i];
+      temporal(G, P, xo, rl);
+      for (int i = 0; i < nl; i++) RLO[size_t(e) * nl + i] = -rl[i];
     }
     return;
   }
   double J[81];
   for (int i = 0; i < nl * nl; i++) J[i] = 0.0;
+  if (onestep) {
+    if (mode == 2)
+      fd_element(xl, nl, P.dt, [&](const double *u, double *r) { spatial(G, P, aux, u, r); }, J);
+    else if (nf == 3)
+      jac_pnp(G, P, xl, J, P.dt);
+    else
+      jac_scalar(G, P, xl, aux, J, P.dt);
+    for (int i = 0; i < nl * nl; i++) JL[size_t(e) * nl * nl + i] = J[i];
+    for (int i = 0; i < nl * nl; i++) J[i] = 0.0;
+    if (mode == 2)
+      fd_element(xl, nl, 1.0, [&](const double *u, double *r) { temporal(G, P, u, r); }, J);
+    else if (nf == 3)
+      jac_pnpt(G, P, J);
+    else
+      jac_difft(G, J);
+    for (int i = 0; i < nl * nl; i++) JLT[size_t(e) * nl * nl + i] = J[i];
+    return;
+  }
   if (mode == 2) {
-    double u[9], down[9], up[9];
-    for (int i = 0; i < nl; i++) u[i] = xl[i];
-    volume(G, P, aux, u, down);
-    for (int j = 0; j < nl; j++) {
-      const double delta = 1e-7 * (1.0 + fabs(u[j]));
-      u[j] += delta;
-      volume(G, P, aux, u, up);
-      for (int i = 0; i < nl; i++) J[i * nl + j] += (up[i] - down[i]) / delta;
-      u[j] = xl[j];
-    }
+    fd_element(xl, nl, 1.0, [&](const double *u, double *r) { volume(G, P, aux, u, r); }, J);
   } else {
     switch (P.kind) {
       case OP_PNP:
         jac_pnp(G, P, xl, J, 1.0);
-        break;
-      case OP_PNP_IE:
-        jac_pnp(G, P, xl, J, P.dt);
-        jac_pnpt(G, P, J);
         break;
       case OP_PB:
       case OP_POISSON:
@@ -436,48 +484,46 @@ __global__ void __launch_bounds__(kB)
       case OP_DIFF:
         jac_scalar(G, P, xl, aux, J, 1.0);
         break;
-      case OP_DIFF_IE:
-        jac_scalar(G, P, xl, aux, J, P.dt);
-        jac_difft(G, J);
-        break;
     }
   }
   for (int i = 0; i < nl * nl; i++) JL[size_t(e) * nl * nl + i] = J[i];
 }
 
-// r[R] for row R = f nv + v: 0, + the element terms (ascending element), + the old-time mass terms
-// (implicit Euler), + the boundary terms (boundary-intersection order), then 0 if constrained
+// r[R] for row R = f nv + v: 0, + (one-step) the const residual's element terms (ascending
+// element), + per incident element in ascending order its local residual's term (volume and
+// boundary) and (one-step) then its temporal term; then 0 if constrained
 __global__ void __launch_bounds__(kB)
     k_seq_residual_gather(SeqMesh M, int nf, int has_old, const double *__restrict__ RL,
-                          const double *__restrict__ RLO, const int *__restrict__ bptr,
-                          const double *__restrict__ bval, const unsigned char *__restrict__ mask,
-                          double *__restrict__ r) {
+                          const double *__restrict__ RLT, const double *__restrict__ RLO,
+                          const unsigned char *__restrict__ mask, double *__restrict__ r) {
   const int R = blockIdx.x * kB + threadIdx.x;
   if (R >= nf * M.nv) return;
   const int f = R / M.nv, v = R % M.nv, nl = 3 * nf;
   double s = 0.0;
-  for (int k = M.vptr[v]; k < M.vptr[v + 1]; k++) {
-    const int e = M.vinc[k] >> 2, a = M.vinc[k] & 3;
-    s += RL[size_t(e) * nl + 3 * f + a];
-  }
   if (has_old)
     for (int k = M.vptr[v]; k < M.vptr[v + 1]; k++) {
       const int e = M.vinc[k] >> 2, a = M.vinc[k] & 3;
       s += RLO[size_t(e) * nl + 3 * f + a];
     }
-  for (int k = bptr[R]; k < bptr[R + 1]; k++) s += bval[k];
+  for (int k = M.vptr[v]; k < M.vptr[v + 1]; k++) {
+    const int e = M.vinc[k] >> 2, a = M.vinc[k] & 3;
+    s += RL[size_t(e) * nl + 3 * f + a];
+    if (has_old) s += RLT[size_t(e) * nl + 3 * f + a];
+  }
   if (mask[R]) s = 0.0;
   r[R] = s;
 }
 
 // the CSR row R (ascending columns, the GPU's reduced pattern: every entry the operator can make
-// non-zero) = 0 + the element blocks' (R, C) terms in ascending element order; constrained rows:
-// identity.  An element term whose column is outside the pattern is an exact zero in the reference
-// (never written, or a forward difference of an unchanged value): skipped.
+// non-zero) = 0 + the element blocks' (R, C) terms in ascending element order (one-step: each
+// element's spatial block, then its temporal block JLT); constrained rows: identity.  An element
+// term whose column is outside the pattern is an exact zero in the reference (never written, or a
+// forward difference of an unchanged value): skipped.
 __global__ void __launch_bounds__(kB)
     k_seq_jacobian_gather(SeqMesh M, int nf, const double *__restrict__ JL,
-                          const int *__restrict__ rowptr, const int *__restrict__ col,
-                          const unsigned char *__restrict__ mask, double *__restrict__ val) {
+                          const double *__restrict__ JLT, const int *__restrict__ rowptr,
+                          const int *__restrict__ col, const unsigned char *__restrict__ mask,
+                          double *__restrict__ val) {
   const int R = blockIdx.x * kB + threadIdx.x;
   if (R >= nf * M.nv) return;
   const int f = R / M.nv, v = R % M.nv, nl = 3 * nf;
@@ -486,21 +532,24 @@ __global__ void __launch_bounds__(kB)
   for (int q = M.vptr[v]; q < M.vptr[v + 1]; q++) {
     const int e = M.vinc[q] >> 2, a = M.vinc[q] & 3;
     const int t[3] = {M.tri[3 * e], M.tri[3 * e + 1], M.tri[3 * e + 2]};
-    for (int j = 0; j < nl; j++) {
-      const int C = (j / 3) * M.nv + t[j % 3];
-      int lo = k0, hi = k1 - 1, at = -1;
-      while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        if (col[mid] == C) {
-          at = mid;
-          break;
+    for (int pass = 0; pass < (JLT ? 2 : 1); pass++) {
+      const double *B = pass ? JLT : JL;
+      for (int j = 0; j < nl; j++) {
+        const int C = (j / 3) * M.nv + t[j % 3];
+        int lo = k0, hi = k1 - 1, at = -1;
+        while (lo <= hi) {
+          const int mid = (lo + hi) >> 1;
+          if (col[mid] == C) {
+            at = mid;
+            break;
+          }
+          if (col[mid] < C)
+            lo = mid + 1;
+          else
+            hi = mid - 1;
         }
-        if (col[mid] < C)
-          lo = mid + 1;
-        else
-          hi = mid - 1;
+        if (at >= 0) val[at] += B[size_t(e) * nl * nl + size_t(3 * f + a) * nl + j];
       }
-      if (at >= 0) val[at] += JL[size_t(e) * nl * nl + size_t(3 * f + a) * nl + j];
     }
   }
   if (mask[R])
@@ -588,23 +637,25 @@ inline dim3 grid(long long n) { return dim3(unsigned((n + kB - 1) / kB)); }
 }  // namespace
 
 hipError_t launch_seq_element(const SeqMesh &M, const SeqOp &P, const double *x, int mode,
-                              double *RL, double *RLO, double *JL, hipStream_t s) {
+                              double *RL, double *RLT, double *RLO, double *JL, double *JLT,
+                              const int *bptr, const double *bval, hipStream_t s) {
   if (M.nt <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_seq_element, grid(M.nt), dim3(kB), 0, s, M, P, x, mode, RL, RLO, JL);
+  hipLaunchKernelGGL(k_seq_element, grid(M.nt), dim3(kB), 0, s, M, P, x, mode, RL, RLT, RLO, JL,
+                     JLT, bptr, bval);
   return hipGetLastError();
 }
 hipError_t launch_seq_residual_gather(const SeqMesh &M, int nf, int has_old, const double *RL,
-                                      const double *RLO, const int *bptr, const double *bval,
+                                      const double *RLT, const double *RLO,
                                       const unsigned char *mask, double *r, hipStream_t s) {
   hipLaunchKernelGGL(k_seq_residual_gather, grid((long long)nf * M.nv), dim3(kB), 0, s, M, nf,
-                     has_old, RL, RLO, bptr, bval, mask, r);
+                     has_old, RL, RLT, RLO, mask, r);
   return hipGetLastError();
 }
 hipError_t launch_seq_jacobian_gather(const SeqMesh &M, int nf, const double *JL,
-                                      const int *rowptr, const int *col,
+                                      const double *JLT, const int *rowptr, const int *col,
                                       const unsigned char *mask, double *val, hipStream_t s) {
   hipLaunchKernelGGL(k_seq_jacobian_gather, grid((long long)nf * M.nv), dim3(kB), 0, s, M, nf, JL,
-                     rowptr, col, mask, val);
+                     JLT, rowptr, col, mask, val);
   return hipGetLastError();
 }
 hipError_t launch_seq_spmv(int n, const int *rowptr, const int *col, const double *val,

@@ -396,15 +396,17 @@ enum {
    * variable PNP_GRAPH=0/1 sets the default).  Not used with AMG, timers or more than one rank. */
   PNP_OPT_GRAPH = 6,
   /* 1: reference-order mode.  pnp_residual / pnp_jacobian / pnp_jacobian_apply / pnp_linear_solve /
-   * pnp_prec_apply / pnp_newton then perform the CPU oracle's single-rank arithmetic in its order
-   * (oracle/pnp_oracle.c: element-order assembly into the CSR view -- every element's volume
-   * terms, then the boundary terms --, ISTL's sequential mv / dot / vector updates, PDELab Newton's
-   * defect as a sequential sum), so iterates and iteration counts are the oracle's even where
-   * BiCGSTAB is chaotic in the last bits.  PDELab itself adds alpha_boundary into each element's
-   * local vector before the scatter and weights one-step terms per accumulation, so the rounding
-   * of the DUNE program may differ: parity against the reference program is unpinned (the
-   * reference ships no vectors and DUNE cannot be built here).  A parity mode, far slower than
-   * the default.  Preconditioners NONE, JACOBI, SSOR_NATURAL; P1 contexts of one rank;
+   * pnp_prec_apply / pnp_newton then perform the CPU oracle's single-rank arithmetic in its order,
+   * which restates PDELab's GridOperator (oracle/pnp_oracle.c): per element in element order one
+   * local vector -- alpha_volume, then alpha_boundary of the element's boundary faces in DUNE's
+   * face order -- added into the CSR view / residual once; implicit Euler as OneStepGridOperator:
+   * the const residual -M(x_old) first, then per element the spatial and the temporal local
+   * vectors; ISTL's sequential mv / dot / vector updates; PDELab Newton's defect as a sequential
+   * sum.  So iterates and iteration counts are the oracle's even where BiCGSTAB is chaotic in the
+   * last bits.  What the restatement cannot see -- the DUNE grid's own vertex order and
+   * dune-geometry's tabulated quadrature points -- leaves parity with the DUNE program's rounding
+   * unpinned (the reference ships no vectors and DUNE cannot be built here).  A parity mode, far
+   * slower than the default.  Preconditioners NONE, JACOBI, SSOR_NATURAL; P1 contexts of one rank;
    * pnp_op_args.c_extra unsupported.  0 (default): the GPU's own summation orders. */
   PNP_OPT_SEQ_ORDER = 7,
   /* 1: each ILU(0) application (PNP_PREC_ILU0) is ONE dataflow launch instead of one launch per

@@ -328,6 +328,59 @@ static void eh_put(ehash *h, long long k, int v) {
   h->val[s] = v;
 }
 
+/* PDELab's boundary intersections of each element (a8): the faces of the reference triangle in
+ * DUNE's numbering, face 0 = local vertices (0,1), face 1 = (0,2), face 2 = (1,2), each a boundary
+ * intersection when its edge is a boundary segment.  ebf[3e + k] = that segment, or -1. */
+static const int kFaceV[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+static int *elem_boundary_faces(const orc_mesh *m) {
+  ehash h;
+  eh_init(&h, m->nb);
+  for (int b = 0; b < m->nb; b++) {
+    long long k = ekey(m->bseg[2 * b], m->bseg[2 * b + 1]);
+    if (eh_get(&h, k) < 0) eh_put(&h, k, b); /* a segment listed twice: its first record */
+  }
+  int *ebf = (int *)malloc(sizeof(int) * 3 * (size_t)(m->nt > 0 ? m->nt : 1));
+  for (int e = 0; e < m->nt; e++) {
+    const int *t = m->tri + 3 * e;
+    for (int k = 0; k < 3; k++)
+      ebf[3 * e + k] = m->nb ? eh_get(&h, ekey(t[kFaceV[k][0]], t[kFaceV[k][1]])) : -1;
+  }
+  eh_free(&h);
+  return ebf;
+}
+
+/* PnpOperator / PBOperator / PoissonOperator::alpha_boundary on face k of element e (segment b)
+ * into the element's local residual rl (src/pnp_operator.hh:198-315, src/pb_operator.hh:126-194):
+ * the face's geometry runs from its lower to its higher local vertex (ig.geometry(), the
+ * reference element's sub-entity order), 2-point Gauss on it, factor = w |face| (* y 2 PI), and
+ * for every non-Dirichlet field the loop over ALL of the element's basis functions (lfsv.size())
+ * evaluated at the face point in element coordinates (geometryInInside(): P1LocalBasis
+ * 1 - x - y, x, y), accumulated with the operator's weight (scale). */
+static void boundary_face(const orc_mesh *m, const orc_params *p, const double *flux, int e, int k,
+                          int b, int nfields, double scale, double *rl) {
+  static const double corner[3][2] = {{0.0, 0.0}, {1.0, 0.0}, {0.0, 1.0}};
+  const double PI = p->pi;
+  const double gt[2] = {0.5 - 0.5 / sqrt(3.0), 0.5 + 0.5 / sqrt(3.0)};
+  const int ia = kFaceV[k][0], ib = kFaceV[k][1];
+  const int va = m->tri[3 * e + ia], vb = m->tri[3 * e + ib];
+  const int g = m->bgroup[b];
+  double dx = m->xy[2 * vb] - m->xy[2 * va], dy = m->xy[2 * vb + 1] - m->xy[2 * va + 1];
+  double len = sqrt(dx * dx + dy * dy);
+  for (int q = 0; q < 2; q++) {
+    double factor = 0.5 * len;
+    double y = m->xy[2 * va + 1] + gt[q] * dy;
+    if (p->cylindrical) factor *= y * 2 * PI;
+    double lx = corner[ia][0] + (corner[ib][0] - corner[ia][0]) * gt[q];
+    double ly = corner[ia][1] + (corner[ib][1] - corner[ia][1]) * gt[q];
+    double phi[3] = {1.0 - lx - ly, lx, ly};
+    for (int f = 0; f < nfields; f++) {
+      if (surface_btype(p, g, f) == 0) continue; /* isDirichlet */
+      double j = flux[3 * b + f];
+      for (int i = 0; i < 3; i++) rl[3 * f + i] += scale * (j * phi[i] * factor);
+    }
+  }
+}
+
 /* Q6: distance of a point to the INFINITE line through a segment, src/dirichlet_bc.hh:21-39 */
 static int on_line(const orc_mesh *m, int b, double px, double py) {
   const double *c0 = m->xy + 2 * m->bseg[2 * b], *c1 = m->xy + 2 * m->bseg[2 * b + 1];
@@ -479,21 +532,26 @@ static void op_volume(const orc_mesh *m, const orc_params *p, const orc_operator
   }
 }
 
+/* PDELab GridOperator::residual (a8; DefaultLocalAssembler, instantiated at
+ * src/stationary_pnp_from_pb.hh:165,315-321), restated: per element in element order, the local
+ * residual is alpha_volume, then alpha_boundary of each of the element's boundary intersections in
+ * face order (boundary_face), and the local vector is added into r once.  One-step operators
+ * (OneStepGridOperator, src/instationary_pnp_from_pb.hh:324; implicit Euler): r starts as the
+ * const residual of the old time level, -M(x_old), assembled by its own element pass (preStage);
+ * then per element the spatial operator's local vector (volume + boundary, weight dt) is added,
+ * then the temporal operator's.  This library writes the implicit-Euler residual as
+ * M(u) - M(u_old) + dt R(u); PDELab's implicit scaling R(u) + (M(u) - M(u_old)) / dt is the same
+ * equation divided by dt, and every weight is 1 at the reference's tau = dt = 1 (pore.cfg).
+ * Constrained rows are zero. */
 void orc_op_residual(const orc_mesh *m, const orc_params *p, const orc_operator *op,
                      const double *x, double *r) {
   int nf = orc_operator_nfields(op);
   int n = nf * m->nv;
   memset(r, 0, sizeof(double) * n);
   double xl[9], rl[9];
-  for (int e = 0; e < m->nt; e++) {
-    elgeo G;
-    element_geometry(m, e, &G);
-    gather(m, e, nf, x, xl);
-    op_volume(m, p, op, e, &G, xl, rl);
-    scatter_add(m, e, nf, rl, r);
-  }
-  /* old-time mass for implicit Euler: r -= M(x_old) */
-  if (op->kind == ORC_OP_PNP_IMPLICIT_EULER || op->kind == ORC_OP_DIFF_IMPLICIT_EULER) {
+  const int onestep = op->kind == ORC_OP_PNP_IMPLICIT_EULER || op->kind == ORC_OP_DIFF_IMPLICIT_EULER;
+  /* const residual (old time level): -M(x_old), element by element */
+  if (onestep) {
     for (int e = 0; e < m->nt; e++) {
       elgeo G;
       element_geometry(m, e, &G);
@@ -507,11 +565,43 @@ void orc_op_residual(const orc_mesh *m, const orc_params *p, const orc_operator 
       scatter_add(m, e, nf, rl, r);
     }
   }
-  /* boundary terms */
-  if (op->kind == ORC_OP_PNP) boundary_flux(m, p, op->flux, 3, 0, 1.0, r);
-  if (op->kind == ORC_OP_PNP_IMPLICIT_EULER) boundary_flux(m, p, op->flux, 3, 0, op->dt, r);
-  if (op->kind == ORC_OP_PB || op->kind == ORC_OP_POISSON)
-    boundary_flux(m, p, op->flux, 1, 0, 1.0, r);
+  const int bnd = op->kind == ORC_OP_PNP || op->kind == ORC_OP_PNP_IMPLICIT_EULER ||
+                  op->kind == ORC_OP_PB || op->kind == ORC_OP_POISSON;
+  int *ebf = bnd ? elem_boundary_faces(m) : NULL;
+  const double bscale = op->kind == ORC_OP_PNP_IMPLICIT_EULER ? op->dt : 1.0;
+  for (int e = 0; e < m->nt; e++) {
+    elgeo G;
+    element_geometry(m, e, &G);
+    gather(m, e, nf, x, xl);
+    if (onestep) {
+      /* the spatial operator's local vector, weight dt */
+      double rs[9] = {0};
+      memset(rl, 0, sizeof rl);
+      if (nf == 3) {
+        lop_pnp_volume(&G, p, xl, rs);
+      } else {
+        const int *t = m->tri + 3 * e;
+        double phil[3] = {op->phi[t[0]], op->phi[t[1]], op->phi[t[2]]};
+        lop_diff_volume(&G, op->z, phil, xl, rs);
+      }
+      for (int i = 0; i < 3 * nf; i++) rl[i] = op->dt * rs[i];
+    } else {
+      op_volume(m, p, op, e, &G, xl, rl);
+    }
+    if (ebf)
+      for (int k = 0; k < 3; k++)
+        if (ebf[3 * e + k] >= 0) boundary_face(m, p, op->flux, e, k, ebf[3 * e + k], nf, bscale, rl);
+    scatter_add(m, e, nf, rl, r);
+    if (onestep) { /* the temporal operator's local vector, weight 1 */
+      memset(rl, 0, sizeof rl);
+      if (nf == 3)
+        lop_pnpt_volume(&G, p, p->tau, xl, rl);
+      else
+        lop_difft_volume(&G, xl, rl);
+      scatter_add(m, e, nf, rl, r);
+    }
+  }
+  free(ebf);
   /* constraints: constrained residual rows are zero */
   if (op->mask)
     for (int i = 0; i < n; i++)
@@ -760,38 +850,110 @@ static void jac_difft_volume(const elgeo *G, double *J) {
   }
 }
 
+/* the spatial / temporal element residuals of a one-step operator (the FD Jacobian's evaluations) */
+static void onestep_spatial(const orc_mesh *m, const orc_params *p, const orc_operator *op, int e,
+                            const elgeo *G, const double *xl, double *rl) {
+  int nf = orc_operator_nfields(op);
+  memset(rl, 0, sizeof(double) * 3 * nf);
+  if (nf == 3) {
+    lop_pnp_volume(G, p, xl, rl);
+  } else {
+    const int *t = m->tri + 3 * e;
+    double phil[3] = {op->phi[t[0]], op->phi[t[1]], op->phi[t[2]]};
+    lop_diff_volume(G, op->z, phil, xl, rl);
+  }
+}
+static void onestep_temporal(const orc_params *p, int nf, const elgeo *G, const double *xl,
+                             double *rl) {
+  memset(rl, 0, sizeof(double) * 3 * nf);
+  if (nf == 3)
+    lop_pnpt_volume(G, p, p->tau, xl, rl);
+  else
+    lop_difft_volume(G, xl, rl);
+}
+
+/* PDELab NumericalJacobianVolume::jacobian_volume, epsilon = 1e-7: J[i nl + j] = w (r_i(u + delta
+ * e_j) - r_i(u)) / delta of the element residual `ev`, accumulated with weight w */
+typedef void (*elres_fn)(const orc_mesh *, const orc_params *, const orc_operator *, int,
+                         const elgeo *, const double *, double *);
+static void fd_element(const orc_mesh *m, const orc_params *p, const orc_operator *op, int e,
+                       const elgeo *G, const double *xl, int nl, elres_fn ev, double w, double *Jl) {
+  double u[9], down[9], up[9];
+  memcpy(u, xl, sizeof(double) * nl);
+  ev(m, p, op, e, G, u, down);
+  for (int j = 0; j < nl; j++) {
+    double delta = 1e-7 * (1.0 + fabs(u[j]));
+    u[j] += delta;
+    ev(m, p, op, e, G, u, up);
+    for (int i = 0; i < nl; i++) Jl[i * nl + j] += w * ((up[i] - down[i]) / delta);
+    u[j] = xl[j];
+  }
+}
+static void onestep_temporal_ev(const orc_mesh *m, const orc_params *p, const orc_operator *op,
+                                int e, const elgeo *G, const double *xl, double *rl) {
+  (void)m;
+  (void)e;
+  onestep_temporal(p, orc_operator_nfields(op), G, xl, rl);
+}
+
+/* BCRSMatrix accumulate of an element matrix: row search per entry */
+static void scatter_jac(const orc_mesh *m, int e, int nl, const double *Jl, orc_csr *A) {
+  const int *t = m->tri + 3 * e;
+  const int nv = m->nv;
+  for (int i = 0; i < nl; i++) {
+    int I = (i / 3) * nv + t[i % 3];
+    for (int j = 0; j < nl; j++) {
+      int Jc = (j / 3) * nv + t[j % 3];
+      *csr_find(A, I, Jc) += Jl[i * nl + j];
+    }
+  }
+}
+
+/* PDELab GridOperator::jacobian (a3, a8), restated like orc_op_residual: per element in element
+ * order the local matrix (analytic, or fd = 1: NumericalJacobianVolume's forward differences of
+ * the element residual -- the reference's own Jacobian, src/pnp_operator.hh:22-27) is added into
+ * A once.  alpha_boundary's terms do not depend on x: NumericalJacobianBoundary adds exact zeros.
+ * One-step operators: per element the spatial operator's matrix (weight dt), then the temporal
+ * operator's.  Constrained rows -> identity (columns kept, non-symmetric). */
 void orc_op_jacobian(const orc_mesh *m, const orc_params *p, const orc_operator *op,
                      const double *x, int fd, orc_csr *A) {
   int nf = orc_operator_nfields(op);
   int nl = 3 * nf;
-  int nv = m->nv;
   memset(A->val, 0, sizeof(double) * A->nnz);
-  double xl[9], u[9], down[9], up[9], Jl[81];
+  double xl[9], Jl[81];
+  const int onestep = op->kind == ORC_OP_PNP_IMPLICIT_EULER || op->kind == ORC_OP_DIFF_IMPLICIT_EULER;
   for (int e = 0; e < m->nt; e++) {
     elgeo G;
     element_geometry(m, e, &G);
     gather(m, e, nf, x, xl);
+    const int *t = m->tri + 3 * e;
     memset(Jl, 0, sizeof Jl);
-    if (fd) {
-      /* PDELab NumericalJacobianVolume::jacobian_volume, epsilon = 1e-7 */
-      memcpy(u, xl, sizeof(double) * nl);
-      op_volume(m, p, op, e, &G, u, down);
-      for (int j = 0; j < nl; j++) {
-        double delta = 1e-7 * (1.0 + fabs(u[j]));
-        u[j] += delta;
-        op_volume(m, p, op, e, &G, u, up);
-        for (int i = 0; i < nl; i++) Jl[i * nl + j] += (up[i] - down[i]) / delta;
-        u[j] = xl[j];
+    if (onestep) {
+      if (fd) {
+        fd_element(m, p, op, e, &G, xl, nl, onestep_spatial, op->dt, Jl);
+      } else if (nf == 3) {
+        jac_pnp_volume(&G, p, xl, Jl, op->dt);
+      } else {
+        double phil[3] = {op->phi[t[0]], op->phi[t[1]], op->phi[t[2]]};
+        jac_scalar_volume(p, op, &G, xl, phil, Jl, op->dt);
       }
+      scatter_jac(m, e, nl, Jl, A);
+      memset(Jl, 0, sizeof Jl);
+      if (fd)
+        fd_element(m, p, op, e, &G, xl, nl, onestep_temporal_ev, 1.0, Jl);
+      else if (nf == 3)
+        jac_pnpt_volume(&G, p, p->tau, Jl);
+      else
+        jac_difft_volume(&G, Jl);
+      scatter_jac(m, e, nl, Jl, A);
+      continue;
+    }
+    if (fd) {
+      fd_element(m, p, op, e, &G, xl, nl, op_volume, 1.0, Jl);
     } else {
-      const int *t = m->tri + 3 * e;
       switch (op->kind) {
       case ORC_OP_PNP:
         jac_pnp_volume(&G, p, xl, Jl, 1.0);
-        break;
-      case ORC_OP_PNP_IMPLICIT_EULER:
-        jac_pnp_volume(&G, p, xl, Jl, op->dt);
-        jac_pnpt_volume(&G, p, p->tau, Jl);
         break;
       case ORC_OP_PB:
       case ORC_OP_POISSON:
@@ -801,22 +963,9 @@ void orc_op_jacobian(const orc_mesh *m, const orc_params *p, const orc_operator 
         double phil[3] = {op->phi[t[0]], op->phi[t[1]], op->phi[t[2]]};
         jac_scalar_volume(p, op, &G, xl, phil, Jl, 1.0);
       } break;
-      case ORC_OP_DIFF_IMPLICIT_EULER: {
-        double phil[3] = {op->phi[t[0]], op->phi[t[1]], op->phi[t[2]]};
-        jac_scalar_volume(p, op, &G, xl, phil, Jl, op->dt);
-        jac_difft_volume(&G, Jl);
-      } break;
       }
     }
-    const int *t = m->tri + 3 * e;
-    for (int i = 0; i < nl; i++) {
-      int I = (i / 3) * nv + t[i % 3];
-      for (int j = 0; j < nl; j++) {
-        int Jc = (j / 3) * nv + t[j % 3];
-        double *a = csr_find(A, I, Jc);
-        *a += Jl[i * nl + j]; /* BCRSMatrix accumulate: row search per entry */
-      }
-    }
+    scatter_jac(m, e, nl, Jl, A);
   }
   /* constrained rows -> identity (columns kept, non-symmetric) */
   if (op->mask)

@@ -155,9 +155,26 @@ def poisson_vol(G, par, cpl, cml, xl):
     return out
 
 
+FACE_V = ((0, 1), (0, 2), (1, 2))  # DUNE reference-triangle faces (local vertex pairs)
+CORNER = np.array([[0.0, 0.0], [1.0, 0.0], [0.0, 1.0]])
+
+
 def boundary(m, par, surfs, nf, scale=1.0):
+    """alpha_boundary (src/pnp_operator.hh:198-315) as PDELab assembles it: each boundary segment is
+    the face of its element, run from the lower to the higher local vertex; every one of the
+    element's three P1 basis functions is evaluated at the face's Gauss points in element
+    coordinates (the off-face one is 0 up to rounding) and accumulated with weight `scale`."""
     r = np.zeros(nf * m.nv)
-    a, b = m.bseg[:, 0], m.bseg[:, 1]
+    face_of = {}
+    for e, t in enumerate(m.tri):
+        for k, (i, j) in enumerate(FACE_V):
+            face_of.setdefault((min(t[i], t[j]), max(t[i], t[j])), (e, k))
+    ek = np.array([face_of[(min(a, b), max(a, b))] for a, b in m.bseg]).reshape(-1, 2)
+    e, k = ek[:, 0], ek[:, 1]
+    fv = np.array(FACE_V)[k]
+    tv = m.tri[e]
+    a = tv[np.arange(len(e)), fv[:, 0]]
+    b = tv[np.arange(len(e)), fv[:, 1]]
     d = m.xy[b] - m.xy[a]
     ln = np.hypot(d[:, 0], d[:, 1])
     for q in range(2):
@@ -165,12 +182,14 @@ def boundary(m, par, surfs, nf, scale=1.0):
         f = GL2[1][q] * ln
         if par["cyl"]:
             f = f * (m.xy[a, 1] + t * d[:, 1]) * 2 * PI
+        loc = CORNER[fv[:, 0]] + (CORNER[fv[:, 1]] - CORNER[fv[:, 0]]) * t
+        phi = np.stack([1.0 - loc[:, 0] - loc[:, 1], loc[:, 0], loc[:, 1]], axis=1)
         for fld in range(nf):
             bt = np.array([[s.cb, s.pb, s.mb][fld] for s in surfs])[m.bgroup]
             jf = np.array([[s.cflux, s.pflux, s.mflux][fld] for s in surfs])[m.bgroup]
             on = bt != 0
-            np.add.at(r, fld * m.nv + a[on], scale * jf[on] * (1 - t) * f[on])
-            np.add.at(r, fld * m.nv + b[on], scale * jf[on] * t * f[on])
+            for i in range(3):
+                np.add.at(r, fld * m.nv + tv[on, i], scale * (jf[on] * phi[on, i] * f[on]))
     return r
 
 
