@@ -46,13 +46,13 @@ import pnp_amd as P  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured stream ceilings
 #                       are in the line (`measured_stream_gbs`, tools/micro/stream.hip)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06", "pmc_summary.json")
 SCRUB_BYTES = 1 << 30  # > 4x the 256 MiB Infinity Cache
 
 
 def pmc_summary():
     """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py), or None."""
-    for path in (PMC_SUMMARY, PMC_SUMMARY.replace("r05", "r04"), PMC_SUMMARY.replace("r05", "r03")):
+    for path in (PMC_SUMMARY, PMC_SUMMARY.replace("r06", "r05")):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -74,8 +74,8 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-ASM_REGIMES = os.path.join(ROOT, "profiles", "r05", "final", "asm_regimes_config3.json")
-BICG_SPLIT = os.path.join(ROOT, "profiles", "r05", "bicg_split_final.json")
+ASM_REGIMES = os.path.join(ROOT, "profiles", "r06", "asm_regimes_config3.json")
+BICG_SPLIT = os.path.join(ROOT, "profiles", "r06", "bicg_split.json")
 
 
 def profile_bicg(config):
@@ -83,7 +83,7 @@ def profile_bicg(config):
     --kernel-trace, split by tools/bicg_split.py): per kernel class the trace's device time per unit,
     the event timers' time of the same pass and the fraction of 8 TB/s on the stored-format bytes;
     None when absent."""
-    for path in (BICG_SPLIT, BICG_SPLIT.replace("_final", "_r5a")):
+    for path in (BICG_SPLIT,):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -95,7 +95,7 @@ def profile_bicg(config):
     return None
 
 
-ILU_MODEL = os.path.join(ROOT, "profiles", "r05", "ilu", "launch_model.json")
+ILU_MODEL = os.path.join(ROOT, "profiles", "r06", "ilu_launch_model.json")
 
 
 def ilu_launch_model():

@@ -3040,10 +3040,6 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     std::vector<uint16_t> li, ui;
     const bool ok = lists(lcl, lco, lcol, 0, rowL, lp, ll, li) &&
                     lists(ucl, uco, ucol, 1, rowU, up2, ul, ui);
-    // padding past the last chunk: the sweeps' branch-free prefetch (linalg.hip ILU_PF) reads slot
-    // 0 of a chunk whose rows have no slots at all
-    li.resize(li.size() + 64 * 16, 0xFFFF);
-    ui.resize(ui.size() + 64 * 16, 0xFFFF);
     int mx = 0;
     for (size_t k = 0; ok && k + 1 < lp.size(); k++) mx = std::max(mx, lp[k + 1] - lp[k]);
     for (size_t k = 0; ok && k + 1 < up2.size(); k++) mx = std::max(mx, up2[k + 1] - up2[k]);

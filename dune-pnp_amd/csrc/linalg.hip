@@ -1791,17 +1791,21 @@ __global__ __launch_bounds__(kRedMwBlock) void k_reduce_mw(const double *__restr
   unsigned *ticket = reinterpret_cast<unsigned *>(mw);
   double *slices = mw + 1;
   __shared__ int last;
+  // publish as the dataflow kernels do (cdna_hip_programming.md Guideline 16): agent-scope
+  // (write-through) stores drained by s_waitcnt before a relaxed ticket, agent-scope loads by the
+  // last workgroup -- no release / acquire fence (the same time, 6.8 / 7.1 us at config 5,
+  // gpurun_out r6c / r6d, and no L2 write-back / invalidate for the kernels around it)
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < K; j++)
       __hip_atomic_store(slices + size_t(blockIdx.x) * K + j, out[j], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double v[K];
 #pragma unroll
   for (int j = 0; j < K; j++)
