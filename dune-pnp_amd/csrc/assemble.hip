@@ -17,6 +17,8 @@
 // order-2 rule, src/pnp_toperator.hh:26) use the reference's quadrature points explicitly.
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 
 namespace pnp {
@@ -713,7 +715,12 @@ hipError_t launch_ion_flux(int ns, const int4 *seg, const double *xy, const doub
   return hipGetLastError();
 }
 
-hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) {
+// t0 / t1 (may be null): events the launch itself records at the kernel's start and end
+// (hipExtLaunchKernelGGL), so the library's timers see the kernel's own duration -- an event pair
+// recorded around the launch adds the dispatch of two markers (~5 us at config 3 in situ, against
+// the kernel trace: 75.7 vs 69.6 us, gpurun_out r6final1 / profiles/r06/asm_regimes_config3.json)
+hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s, hipEvent_t t0,
+                           hipEvent_t t1) {
   if (L.n_owned == 0) return hipSuccess;
   dim3 grid((L.n_owned + 255) / 256), block(256);
   // occupancy variant (A/B knob, PNP_ASM_WAVES=3|4): 4 waves/SIMD caps the fused PNP kernel at
@@ -769,39 +776,39 @@ hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s) 
 #define PNP_ASM_CASE(OPK)                                                          \
   case OPK:                                                                        \
     if (!fanr && a.jac)                                                            \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, L, a);     \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 1, 3, 0>), grid, block, 0, s, t0, t1, 0, L, a);     \
     else if (!fanr)                                                                \
-      hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, L, a);     \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 0, 4, 0>), grid, block, 0, s, t0, t1, 0, L, a);     \
     else if (!a.jac && fanr == 9 && ga && lds_env == 1 && L.uown &&                 \
              size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9, 9, 0, 1>), grid, block,         \
-                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9, 9, 0, 1>), grid, block,         \
+                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, t0, t1, 0, L, a);             \
     else if (!a.jac && fanr == 9 && ga)                                            \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9>), grid, block, 0, s, L, a);  \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 0, 3, 9>), grid, block, 0, s, t0, t1, 0, L, a);  \
     else if (!a.jac)                                                               \
-      hipLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, L, a);    \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 0, 4, 12>), grid, block, 0, s, t0, t1, 0, L, a);    \
     else if (ga == 1 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9>), grid, block, 0, s, L, a);  \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9>), grid, block, 0, s, t0, t1, 0, L, a);  \
     else if (ga == 2 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, L, a);  \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 2, 9>), grid, block, 0, s, t0, t1, 0, L, a);  \
     else if (ga == 3 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, L, a); \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 5>), grid, block, 0, s, t0, t1, 0, L, a); \
     else if (ga == 4 && fanr == 9 && lds_walk(OpTraits<OPK>::NK) && L.uown &&       \
              size_t(L.unmax) * asm_lds_rec<OPK>() * 8 <= 53 * 1024)                    \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \
-                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, L, a);             \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 0, 1>), grid, block,         \
+                         size_t(L.unmax) * asm_lds_rec<OPK>() * 8, s, t0, t1, 0, L, a);             \
     else if (ga == 4 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, L, a); \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6>), grid, block, 0, s, t0, t1, 0, L, a); \
     else if (ga == 5 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 3>), grid, block, 0, s, L, a); \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 3>), grid, block, 0, s, t0, t1, 0, L, a); \
     else if (ga == 6 && fanr == 9)                                                 \
-      hipLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 1>), grid, block, 0, s, L, a); \
+      hipExtLaunchKernelGGL((k_assemble_ga<OPK, 1, 3, 9, 6, 1>), grid, block, 0, s, t0, t1, 0, L, a); \
     else if (fanr == 12)                                                           \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, L, a);    \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 1, 3, 12>), grid, block, 0, s, t0, t1, 0, L, a);    \
     else if (waves == 3)                                                           \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 3, 9>), grid, block, 0, s, L, a);     \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 1, 3, 9>), grid, block, 0, s, t0, t1, 0, L, a);     \
     else                                                                           \
-      hipLaunchKernelGGL((k_assemble<OPK, 1, 4, 9>), grid, block, 0, s, L, a);     \
+      hipExtLaunchKernelGGL((k_assemble<OPK, 1, 4, 9>), grid, block, 0, s, t0, t1, 0, L, a);     \
     break;
   switch (a.kind) {
     PNP_ASM_CASE(OP_PNP)

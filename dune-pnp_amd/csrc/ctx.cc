@@ -559,10 +559,19 @@ struct pnp_ctx {
     if (!split_spmv) {
       int rc = halo(vin, nf);
       if (rc) return rc;
-      hipEvent_t t0 = tb(T_SPMV);
-      e = pnp::launch_spmv(dl, nf, pat, vals.p, vin, yout, mode, w, partials.p, nsp, stream, w2);
+      // the launch records the timer events itself (the kernel's own duration)
+      hipEvent_t t0 = nullptr, t1 = nullptr;
+      if (timing && L.n_owned > 0) {
+        t0 = ev_get();
+        t1 = ev_get();
+      }
+      e = pnp::launch_spmv(dl, nf, pat, vals.p, vin, yout, mode, w, partials.p, nsp, stream, w2,
+                           t0, t1);
       if (e != hipSuccess) return hipfail(e, "spmv");
-      te(T_SPMV, t0);
+      if (t1) {
+        ev_pending[T_SPMV].push_back({t0, t1});
+        t_n[T_SPMV]++;
+      }
       return PNP_OK;
     }
     const int kd = mode == 4 ? 3 : (mode == 2 ? 2 : 1);
@@ -805,17 +814,31 @@ struct pnp_ctx {
     aa.jac = fd_mode ? 0 : jac;
     aa.r = r.p;
     aa.cold = after_solve ? 1 : 0;
-    hipEvent_t t0 = tb(T_ASM);
+    // the P1 analytic assembly is one launch: it records its own start / end events (the
+    // kernel's duration, as the kernel trace reports it); the other forms take an event pair
+    const bool one = degree == 1 && !(jac && fd_mode);
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    if (timing && one) {
+      t0 = ev_get();
+      t1 = ev_get();
+    } else {
+      t0 = tb(T_ASM);
+    }
     hipError_t e;
     if (degree > 1)
       e = pnp::launch_pk_assemble(dl, aa, pkd, jac ? (fd_mode ? 2 : 1) : 0, stream);
     else
-      e = pnp::launch_assemble(dl, aa, stream);
+      e = pnp::launch_assemble(dl, aa, stream, t1 ? t0 : nullptr, t1);
     if (e == hipSuccess && jac && fd_mode && degree == 1)
       e = pnp::launch_fd_jacobian(dl, aa, nf, pat, fd_ne, fd_etri.p, fd_rptr.p, fd_cdata.p,
                                   fd_jel.p, stream);
     if (e != hipSuccess) return hipfail(e, "assemble");
-    te(T_ASM, t0);
+    if (t1) {
+      ev_pending[T_ASM].push_back({t0, t1});
+      t_n[T_ASM]++;
+    } else {
+      te(T_ASM, t0);
+    }
     if (jac) {
       assembled = true;
       lu_valid = false;
@@ -1185,6 +1208,12 @@ struct pnp_ctx {
   DBuf<unsigned> nat_probe;
   int nat_probe_run() {
     if (nat_resident >= 0 || !use_nat_flow()) return PNP_OK;
+    // test hook: PNP_NAT_PROBE_FAIL=1 takes the probe's "not resident" answer without running it
+    // (tests/test_gpu_ssor_natural.py: the level launches are then used, bitwise the same)
+    if (const char *ev = std::getenv("PNP_NAT_PROBE_FAIL"); ev && std::atoi(ev) == 1) {
+      nat_resident = 0;
+      return PNP_OK;
+    }
     hipError_t e = nat_probe.p ? hipSuccess : nat_probe.alloc(2);
     if (e != hipSuccess) return hipfail(e, "natural SSOR probe");
     const int r = pnp::ssor_natural_flow_resident(nat_flow_view(), nat_probe.p, stream);
@@ -1366,7 +1395,8 @@ struct pnp_ctx {
   }
   // v = ILU(0)^-1 d over the owned rows, colours from c_first (launch_ilu0_apply's contract): one
   // dataflow launch when PNP_OPT_ILU_FLOW is on and d and v are distinct, else the colour launches
-  int ilu_apply(const double *d, double *vout, int c_first, const char *what) {
+  int ilu_apply(const double *d, double *vout, int c_first, const char *what,
+                hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
     // the resident-grid form needs the device to itself: not with in-process ranks sharing it
     // (and one context per GPU at N > 1); PNP_ILU_FLOW_TICKET=1: the ticketed form (any residency)
     // PNP_ILU_FLOW_MODE: IluFlow::persistent (0 ticket, 1 static resident grid, the default).
@@ -1385,8 +1415,10 @@ struct pnp_ctx {
       if (!D.built && (rc = ilu_flow_build(c_first, D))) return rc;
       D.F.persistent = fmode;
       if (D.ok) {
+        if (t0) hipEventRecord(t0, stream);
         hipError_t e = pnp::launch_ilu0_flow(dl, D.F, nf, pat, lvals.p, uvals.p, d, vout, stream,
                                              f32_now());
+        if (t1) hipEventRecord(t1, stream);
         if (e != hipSuccess) return hipfail(e, what);
         ilu_flow_used = true;
         ilu_flow_n++;
@@ -1395,7 +1427,7 @@ struct pnp_ctx {
     }
     hipError_t e = pnp::launch_ilu0_apply(dl, L.color_ptr.data(), nf, pat, lvals.p, uvals.p, d,
                                           vout, stream, c_first, nullptr, nullptr, f32_now(),
-                                          ilu_y32());
+                                          ilu_y32(), t0, t1);
     return e == hipSuccess ? PNP_OK : hipfail(e, what);
   }
   // a dataflow application that timed out (never expected) leaves void results and a sticky word
@@ -2035,11 +2067,20 @@ struct pnp_ctx {
     }();
     const bool fuse = fuse_env && prec == PNP_PREC_ILU0 && L.color_ptr.size() > 2;
     const int c0_end = L.color_ptr.size() > 1 ? L.color_ptr[1] : 0;
+    // the colour launches record the timer events themselves: the first launch's start and the
+    // last launch's end (no marker dispatch in the measured span)
     auto ilu_from1 = [&](const double *d, double *out) -> int {
-      hipEvent_t tp = tb(T_PREC);
-      const int rc1 = ilu_apply(d, out, 1, "preconditioner");
+      hipEvent_t t0 = nullptr, t1 = nullptr;
+      if (timing && L.n_owned > 0) {
+        t0 = ev_get();
+        t1 = ev_get();
+      }
+      const int rc1 = ilu_apply(d, out, 1, "preconditioner", t0, t1);
       if (rc1) return rc1;
-      te(T_PREC, tp);
+      if (t1) {
+        ev_pending[T_PREC].push_back({t0, t1});
+        t_n[T_PREC]++;
+      }
       return PNP_OK;
     };
     // two-reduction iteration (two allreduces per iteration instead of three: rho_new from the

@@ -310,7 +310,8 @@ struct Scalars {
 };
 
 // ---- launchers (return hipError_t of the launch) ----------------------------------------------
-hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s);
+hipError_t launch_assemble(const DevLayout &L, const AsmArgs &a, hipStream_t s,
+                           hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // old-time mass M(x_old) (PnpTOperator / DiffusionTOperator) subtracted into cvec
 hipError_t launch_ion_flux(int ns, const int4 *seg, const double *xy, const double *x, int cyl,
                            double pi, double *out, hipStream_t s);
@@ -320,9 +321,12 @@ hipError_t launch_mass_apply(const DevLayout &L, int kind, double tau, double pi
 // y = A x over owned rows; optional fused dots: out partials[block*k + j]
 //   mode 0: none; 1: <w, y> (k=1); 2: <y, w>, <y, y> (k=2); 3: y = w - A x (no dots);
 //   4: <y, w>, <y, y>, <y, w2> (k=3)
+// t0 / t1 (may be null; the LDS-staged form only): events the launch records at the kernel's
+// start and end (hipExtLaunchKernelGGL), so the library's timers see the kernel's own duration
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
-                       hipStream_t s, const double *w2 = nullptr);
+                       hipStream_t s, const double *w2 = nullptr, hipEvent_t t0 = nullptr,
+                       hipEvent_t t1 = nullptr);
 
 // preconditioners: v = M^{-1} d (v over owned rows)
 hipError_t launch_jacobi(const DevLayout &L, int nf, int pat, const double *vals, const double *d,
@@ -359,10 +363,13 @@ hipError_t launch_ilu0_factor_fused(const DevLayout &L, const int *color_ptr_hos
 // factors only, f32 = 2): the forward sweep's intermediate y = L^-1 d is stored in single precision
 // there (colour 0's by launch_update_fwd0 when c_first = 1) instead of in v, and the forward
 // gathers and the backward sweep's own rows read it from there
+// t0 / t1 (may be null; the LDS-staged colour launches only): recorded by the first launch's
+// start and the last launch's end, so a timer spans the colour launches without marker dispatch
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *color_ptr_host, int nf, int pat,
                              const void *lv, const void *uv, const double *d, double *v,
                              hipStream_t s, int c_first = 0, const double *add = nullptr,
-                             double *out = nullptr, int f32 = 0, float *yf = nullptr);
+                             double *out = nullptr, int f32 = 0, float *yf = nullptr,
+                             hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // The same application as ONE dataflow launch (k_ilu0_flow, PNP_ILU_FLOW): the colour launches'
 // 256-row blocks become units in the launches' order (forward colours c_first .. nc-2, the last
 // colour, backward colours nc-2 .. 0); a workgroup takes the next unit by an atomic ticket, waits

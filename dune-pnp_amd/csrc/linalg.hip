@@ -17,6 +17,8 @@
 
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 
 // split sweeps: issue a batch's L/U value loads with its column-index loads (1) or after them (0)
@@ -2063,7 +2065,7 @@ static bool spmv_nt() {
 template <int NF, int PAT, int MODE>
 static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double *vals,
                         const double *x, double *y, const double *w, double *partials,
-                        const double *w2) {
+                        const double *w2, hipEvent_t t0, hipEvent_t t1) {
 #define PNP_SPMV_GO(SBc, LPRc)                                                                 \
   hipLaunchKernelGGL((k_spmv<NF, PAT, MODE, SBc, LPRc>), dim3(g.x * LPRc), dim3(kBlock), 0, s, \
                      L, vals, x, y, w, partials, w2)
@@ -2073,10 +2075,19 @@ static void spmv_launch(dim3 g, hipStream_t s, const DevLayout &L, const double 
   const int b = spmv_batch(), l = spmv_lpr();
   if (spmv_uses_lds(L)) {
     const size_t lds = size_t(SPMV_OWN_DIRECT && L.uown ? L.unmax : L.umax) * NF * sizeof(double);
-    hipLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, L, vals, x, y,
-                       w, partials, w2);
+    hipExtLaunchKernelGGL((k_spmv_lds<NF, PAT, MODE, 2, 1>), g, dim3(kBlock), lds, s, t0, t1, 0, L,
+                          vals, x, y, w, partials, w2);
     return;
   }
+  // the other forms: the timer events as plain markers around the launch
+  if (t0) hipEventRecord(t0, s);
+  struct Stop {
+    hipEvent_t e;
+    hipStream_t s;
+    ~Stop() {
+      if (e) hipEventRecord(e, s);
+    }
+  } stop{t1, s};
   if (spmv_nt() && l == 2 && b == 2) {
     PNP_SPMV_GO2(2, 2, 1);
     return;
@@ -2101,7 +2112,7 @@ int spmv_parts(int nrows) { return int(rows_grid(nrows).x) * 2; }
 
 hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, const double *x,
                        double *y, int mode, const double *w, double *partials, int *nparts,
-                       hipStream_t s, const double *w2) {
+                       hipStream_t s, const double *w2, hipEvent_t t0, hipEvent_t t1) {
   if (L.blkcount < 0) {  // an empty block subset (e.g. a rank without interior blocks)
     if (nparts) *nparts = 0;
     return hipSuccess;
@@ -2111,15 +2122,15 @@ hipError_t launch_spmv(const DevLayout &L, int nf, int pat, const double *vals, 
   if (L.n_owned == 0) return hipSuccess;
   PNP_PAT_DISPATCH(nf, pat, {
     if (mode == 0)
-      (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials, w2);
+      (spmv_launch<NFc, PATc, 0>)(g, s, L, vals, x, y, w, partials, w2, t0, t1);
     else if (mode == 1)
-      (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials, w2);
+      (spmv_launch<NFc, PATc, 1>)(g, s, L, vals, x, y, w, partials, w2, t0, t1);
     else if (mode == 2)
-      (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials, w2);
+      (spmv_launch<NFc, PATc, 2>)(g, s, L, vals, x, y, w, partials, w2, t0, t1);
     else if (mode == 4)
-      (spmv_launch<NFc, PATc, 4>)(g, s, L, vals, x, y, w, partials, w2);
+      (spmv_launch<NFc, PATc, 4>)(g, s, L, vals, x, y, w, partials, w2, t0, t1);
     else
-      (spmv_launch<NFc, PATc, 3>)(g, s, L, vals, x, y, w, partials, w2);
+      (spmv_launch<NFc, PATc, 3>)(g, s, L, vals, x, y, w, partials, w2, t0, t1);
   });
   return hipGetLastError();
 }
@@ -2278,7 +2289,8 @@ static int ilu_lds_bsel() {
 
 hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat, const void *lvp,
                              const void *uvp, const double *d, double *v, hipStream_t s,
-                             int c_first, const double *add, double *out, int f32, float *yf) {
+                             int c_first, const double *add, double *out, int f32, float *yf,
+                             hipEvent_t t0, hipEvent_t t1) {
   if (L.n_owned == 0) return hipSuccess;
   if (yf && f32 != 2) return hipErrorInvalidValue;  // the bf16-factor mode only
   const int nc = L.ncolors;
@@ -2289,6 +2301,20 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     blk0[0] = 0;
     for (int c = 0; c < nc; c++) blk0[c + 1] = blk0[c] + (cp[c + 1] - cp[c] + kBlock - 1) / kBlock;
     const size_t lds = size_t(L.sx_max) * nf * sizeof(double);
+    // the timer events: t0 at the first launch's start, t1 at the last launch's end (launch
+    // order: forward colours c_first .. nc-2, the last colour, backward colours nc-2 .. 0)
+    int first_c = -1;
+    int last_c = -1;
+    for (int c = c_first; c < nc; c++)
+      if (cp[c + 1] > cp[c]) {
+        if (first_c < 0) first_c = c;
+        last_c = c;
+      }
+    for (int c = 0; c < nc - 1; c++)  // the backward launches end with the lowest colour
+      if (cp[c + 1] > cp[c]) {
+        last_c = -(c + 1);  // encoded: backward launch of colour c
+        break;
+      }
     auto run = [&](auto vt, auto *yv) -> hipError_t {
       using VT = decltype(vt);
       using YT = std::remove_pointer_t<decltype(yv)>;
@@ -2303,17 +2329,19 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
           const int n = cp[c + 1] - cp[c];
           if (n <= 0) return;
           constexpr int K = decltype(kind)::value;
+          const hipEvent_t e0 = (K == kIluBwd || c != first_c) ? nullptr : t0;
+          const hipEvent_t e1 = (K == kIluBwd ? last_c == -(c + 1) : last_c == c) ? t1 : nullptr;
           auto launch = [&](auto ntc, auto bc) {
             constexpr int NT = decltype(ntc)::value;
             constexpr int BB = decltype(bc)::value;
             if (add && K != kIluFwd)
-              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 1, VT, YT>), rows_grid(n),
-                                 dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
-                                 add, out, yv);
+              hipExtLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 1, VT, YT>),
+                                    rows_grid(n), dim3(kBlock), lds, s, e0, e1, 0, L, cp[c],
+                                    cp[c + 1], blk0[c], lv, uv, d, v, add, out, yv);
             else
-              hipLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 0, VT, YT>), rows_grid(n),
-                                 dim3(kBlock), lds, s, L, cp[c], cp[c + 1], blk0[c], lv, uv, d, v,
-                                 nullptr, nullptr, yv);
+              hipExtLaunchKernelGGL((k_ilu0_solve_lds<NFc, PATc, K, BB, NT, 0, VT, YT>),
+                                    rows_grid(n), dim3(kBlock), lds, s, e0, e1, 0, L, cp[c],
+                                    cp[c + 1], blk0[c], lv, uv, d, v, nullptr, nullptr, yv);
           };
           auto batch = [&](auto ntc) {
             if (kBsel == 8)
@@ -2339,6 +2367,15 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
     if (yf) return run(bf16s(), yf);
     return f32 == 2 ? run(bf16s(), v) : f32 ? run(float(), v) : run(double(), v);
   }
+  // the direct-gather form: the timer events as plain markers around its launches
+  if (t0) hipEventRecord(t0, s);
+  struct Stop {
+    hipEvent_t e;
+    hipStream_t s;
+    ~Stop() {
+      if (e) hipEventRecord(e, s);
+    }
+  } stop{t1, s};
   auto run = [&](auto vt, auto *yv) -> hipError_t {
     using VT = decltype(vt);
     using YT = std::remove_pointer_t<decltype(yv)>;

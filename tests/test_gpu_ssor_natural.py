@@ -267,3 +267,30 @@ def test_graph_cache_survives_csr_pattern_switch():
         np.testing.assert_array_equal(got[k][0], want[0])
         assert got[k][1]["it_half"] == want[1]["it_half"]
         ref.close()
+
+
+def test_failed_coresidency_probe_keeps_the_level_launches(monkeypatch):
+    """Round 6: the one-launch dataflow sweep runs only after its head and chain grids were seen
+    resident at once on the device (ssor_natural_flow_resident, checked once per schedule).  When
+    the probe says no (PNP_NAT_PROBE_FAIL=1 forces that answer), the context keeps the level
+    launches -- no dataflow application at all -- and BiCGSTAB's iterates are bitwise those of the
+    dataflow schedule."""
+    z, mesh, par, orc = golden("pore_small_k0")
+    out = {}
+    for fail in (0, 1):
+        monkeypatch.setenv("PNP_NAT_PROBE_FAIL", str(fail))
+        ctx = P.Context(mesh, par)
+        ctx.set_operator(P.OP_PNP)
+        x = z["newton_pnp_x0"]
+        ctx.jacobian(x)
+        b = ctx.residual(x)
+        i0 = ctx.info()
+        zsol, res = ctx.linear_solve(b, prec=P.PREC_SSOR_NATURAL, reduction=1e-8, maxit=2000)
+        i1 = ctx.info()
+        ctx.close()
+        out[fail] = (zsol, res["it_half"], i1["nat_flow_applies"] - i0["nat_flow_applies"],
+                     i1["nat_level_applies"] - i0["nat_level_applies"])
+    assert out[0][2] > 0 and out[0][3] == 0  # the probe passed on this GPU: dataflow
+    assert out[1][2] == 0 and out[1][3] > 0  # forced "not resident": level launches only
+    assert out[0][1] == out[1][1]
+    np.testing.assert_array_equal(out[0][0], out[1][0])
