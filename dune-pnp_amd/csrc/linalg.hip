@@ -12,6 +12,7 @@
 //   coupling among themselves, so each colour is one fully parallel launch (forward: colours
 //   ascending, backward: descending); couplings to ghost rows are dropped (block-Jacobi across
 //   GPUs, like the reference's non-overlapping SSOR on the local matrix).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -2537,9 +2538,18 @@ hipError_t launch_dot(long long n, const double *a, const double *b, int two, do
   return hipGetLastError();
 }
 
-// the multi-workgroup grid for np partials, or 0 for the one-workgroup k_reduce
+// the multi-workgroup grid for np partials, or 0 for the one-workgroup k_reduce.
+// PNP_RED_MW_MIN (test hook, read once) lowers the threshold, so that small systems exercise the
+// multi-workgroup path (tests/test_gpu_reduce_mw.py)
+static int reduce_mw_min() {
+  static const int v = [] {
+    const char *e = std::getenv("PNP_RED_MW_MIN");
+    return e ? std::max(1, std::atoi(e)) : kRedMwMin;
+  }();
+  return v;
+}
 static int reduce_mw_grid(int np, const double *mw) {
-  if (!mw || np < kRedMwMin) return 0;
+  if (!mw || np < reduce_mw_min()) return 0;
   const int g = (np + kRedMwPer * kRedMwBlock - 1) / (kRedMwPer * kRedMwBlock);
   return g < 2 ? 0 : (g > kRedMwMax ? kRedMwMax : g);
 }
