@@ -2321,10 +2321,11 @@ hipError_t launch_ilu0_apply(const DevLayout &L, const int *cp, int nf, int pat,
       using YT = std::remove_pointer_t<decltype(yv)>;
       const VT *lv = static_cast<const VT *>(lvp), *uv = static_cast<const VT *>(uvp);
       // slot batch (the sums run over the slots in order whatever the batch, so bitwise alike):
-      // 2 below 1.5 M rows, 3 above -- config 3 apply 69.5 -> 66.8 us with 2, config 5 215 ->
-      // 207 us with 3 (profiles/r03/ab_ilu_lds_batch_r5n.log); 4 before; 8 lost (config 3 77 ->
-      // 89 us, ab_ilu_lds_b.log).  PNP_ILU_LDS_B = 2 / 3 / 4 / 8 forces one
-      const int kBsel = ilu_lds_bsel() ? ilu_lds_bsel() : (L.n_owned > 1500000 ? 3 : 2);
+      // 2 -- round 3 chose 3 above 1.5 M rows (config 5 215 -> 207 us, profiles/r03/
+      // ab_ilu_lds_batch_r5n.log), but with the bfloat16 factors 2 is faster there too (config 5
+      // 181.7 -> 177.6 us per apply, interleaved twice, gpurun_out/r6c5/ab_cfg5.log); 4 and 8
+      // lose at both sizes.  PNP_ILU_LDS_B = 2 / 3 / 4 / 8 forces one
+      const int kBsel = ilu_lds_bsel() ? ilu_lds_bsel() : 2;
       PNP_PAT_DISPATCH(nf, pat, {
         auto go = [&](auto kind, int c) {
           const int n = cp[c + 1] - cp[c];
