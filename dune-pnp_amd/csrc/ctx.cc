@@ -2879,6 +2879,17 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
   }
   std::vector<int> part;
   pnp::rcb_partition(c->mesh, c->nranks, part);
+  {  // every rank computes the same partition: all of them fail here, before any collective or
+     // group barrier, when one part is empty (more ranks than vertices)
+    std::vector<int> cnt(c->nranks, 0);
+    for (int p : part) cnt[p]++;
+    for (int r = 0; r < c->nranks; r++)
+      if (cnt[r] == 0) {
+        g_err = "partition: rank " + std::to_string(r) + " of " + std::to_string(c->nranks) +
+                " owns no vertices (the mesh has " + std::to_string(c->mesh.nv) + ")";
+        return PNP_E_MESH;
+      }
+  }
   if (!pnp::build_local_layout(c->mesh, c->fans, part, c->rank, c->nranks, c->L, err)) {
     g_err = err;
     return PNP_E_MESH;

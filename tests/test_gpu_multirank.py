@@ -345,3 +345,60 @@ def test_parallel_dot_and_norm_equal_single_rank(nranks):
     for d, n, s in run_ranks(nranks, mesh, par, fn):
         assert abs(d - d1) <= 1e-14 * abs(d1) * 10 and abs(n - n1) <= 1e-14 * n1
         assert abs(s - s1) <= 1e-14 * s1
+
+
+def _square():
+    """4 vertices, 2 triangles: the smallest mesh a partition can split to one vertex per rank"""
+    xy = np.array([[0.0, 1.0], [1.0, 1.0], [1.0, 2.0], [0.0, 2.0]])
+    tri = np.array([[0, 1, 2], [0, 2, 3]], dtype=np.int32)
+    bseg = np.array([[0, 1], [1, 2], [2, 3], [3, 0]], dtype=np.int32)
+    bgroup = np.array([0, 1, 0, 1], dtype=np.int32)
+    surf = [P.Surface(cb=1, cflux=0.3, cpot=0.0, pb=1, pflux=-0.2, pconc=0.0, mb=1, mflux=0.1,
+                      mconc=0.0),
+            P.Surface(cb=0, cflux=0.0, cpot=1.0, pb=0, pflux=0.0, pconc=0.05, mb=0, mflux=0.0,
+                      mconc=0.07)]
+    return P.Mesh(xy, tri, bseg, bgroup), P.Params(surf, l_b=0.7, c0=0.06, tau=1.0)
+
+
+def test_one_vertex_per_rank_matches_single_rank():
+    """the ragged extreme: as many ranks as vertices, every rank one owned row and the rest ghosts"""
+    mesh, par = _square()
+    rng = np.random.default_rng(4)
+    x = np.concatenate([rng.uniform(-1, 1, 4), 0.06 * rng.uniform(0.5, 1.5, 8)])
+
+    x0 = np.concatenate([np.zeros(4), np.full(8, 0.06)])
+
+    def fn(ctx, r):
+        ctx.set_operator(P.OP_PNP)
+        out = ctx.residual(x), ctx.jacobian(x), ctx.info()["nv_owned"]
+        u, res = ctx.newton(x0, prec=P.PREC_ILU0)
+        return out + (ctx.sync_vector(u), res)
+    outs = run_ranks(4, mesh, par, fn)
+    assert [o[2] for o in outs] == [1, 1, 1, 1]
+    ctx1 = P.Context(mesh, par)
+    ctx1.set_operator(P.OP_PNP)
+    r1, J1 = ctx1.residual(x), ctx1.jacobian(x)
+    u1, res1 = ctx1.newton(x0, prec=P.PREC_ILU0)
+    ctx1.close()
+    assert np.max(np.abs(sum(o[0] for o in outs) - r1)) <= 1e-13 * np.max(np.abs(r1))
+    assert abs(sum(o[1] for o in outs) - J1).max() <= 1e-13 * abs(J1).max()
+    assert res1["converged"] == 1, res1
+    for o in outs:  # block-Jacobi ILU(0) of one row per rank: the same Newton solution
+        assert o[4]["converged"] == 1 and o[4]["status"] == 0, o[4]
+        assert np.max(np.abs(o[3] - u1)) <= 1e-6 * np.max(np.abs(u1))
+
+
+def test_more_ranks_than_vertices_fails_on_every_rank():
+    """an empty part is refused by every rank before the group joins (no rank left waiting)"""
+    mesh, par = _square()
+    name = f"t{next(_grp)}"
+
+    def work(r):
+        try:
+            P.Context(mesh, par, device=0, rank=r, size=6, local_group=name).close()
+        except P.PnpError as e:
+            return str(e)
+        return None
+    with ThreadPoolExecutor(6) as ex:
+        errs = list(ex.map(work, range(6)))
+    assert all(e and "owns no vertices" in e for e in errs), errs
