@@ -268,6 +268,7 @@ struct pnp_ctx {
     return (e && std::atoi(e) != 0) ? 1 : 0;
   }();
   std::vector<int> h_posrowL, h_posrowU, h_lsx_ptr, h_lsx_list, h_usx_ptr, h_usx_list;
+  int64_t lslots_live = 0, uslots_live = 0;  // pnp_info
   struct IluFlowDev {
     bool built = false, ok = false;
     pnp::IluFlow F;
@@ -2978,10 +2979,13 @@ extern "C" int pnp_create_pk(const pnp_mesh *mesh, const pnp_params *params, int
     lpinv[rowL(pos)] = uint8_t(pos % 64);
     upinv[rowU(pos)] = uint8_t(pos % 64);
   }
+  c->lslots_live = c->uslots_live = 0;
   for (int pos = 0; pos < npos; pos++) {
     llen8[pos] = uint8_t(nlr[rowL(pos)]);
     ulen8[pos] = uint8_t(nur[rowU(pos)]);
     ldl[pos] = upinv[rowL(pos)];
+    if (rowL(pos) < no) c->lslots_live += nlr[rowL(pos)];
+    if (rowU(pos) < no) c->uslots_live += nur[rowU(pos)];
   }
   std::vector<int> lcl(L.nchunks), lco(L.nchunks + 1, 0), ucl(L.nchunks), uco(L.nchunks + 1, 0);
   for (int ch = 0; ch < L.nchunks; ch++) {
@@ -3457,6 +3461,10 @@ extern "C" int pnp_get_info(pnp_ctx *c, pnp_info *info) {
   info->nat_flow_applies = c->nat_flow_n;
   info->nat_level_applies = c->nat_level_n;
   info->ilu_flow_applies = c->ilu_flow_n;
+  info->lslots_live = c->lslots_live;
+  info->uslots_live = c->uslots_live;
+  info->lsx_entries = (int64_t)c->h_lsx_list.size();
+  info->usx_entries = (int64_t)c->h_usx_list.size();
   size_t b = 0;
   b += c->vals.n * 8 + (c->x.n + c->r.n + c->rs.n + c->z.n + c->rt.n + c->p.n + c->v.n + c->t.n + c->y.n +
                         c->y2.n + c->b.n + c->prevu.n + c->ext.n) * 8 + c->ilu_y32buf.n * 4;

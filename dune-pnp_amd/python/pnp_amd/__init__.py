@@ -171,7 +171,9 @@ class _Info(C.Structure):
                 ("uslots", C.c_int64), ("ilu_f32", C.c_int32), ("degree", C.c_int32),
                 ("color_conflicts", C.c_int64), ("transport", C.c_int32),
                 ("nat_flow_applies", C.c_int64), ("nat_level_applies", C.c_int64),
-                ("ilu_flow_applies", C.c_int64)]
+                ("ilu_flow_applies", C.c_int64), ("lslots_live", C.c_int64),
+                ("uslots_live", C.c_int64), ("lsx_entries", C.c_int64),
+                ("usx_entries", C.c_int64)]
 
 
 class _SpaceInfo(C.Structure):

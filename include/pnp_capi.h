@@ -195,6 +195,10 @@ typedef struct {
                                 ranks share one device; or PNP_NAT_FLOW=0) */
   int64_t ilu_flow_applies;  /* PNP_PREC_ILU0 applications launched as one dataflow launch
                                 (PNP_OPT_ILU_FLOW; a graph capture counts once) */
+  int64_t lslots_live, uslots_live; /* split slots that hold a coupling (lslots / uslots without
+                                       the lane padding; U with the diagonal slot) */
+  int64_t lsx_entries, usx_entries; /* the LDS sweeps' staged neighbour rows, summed over the
+                                       256-row blocks: the gathers of one ILU(0) application */
 } pnp_info;
 int pnp_get_info(pnp_ctx *ctx, pnp_info *info);
 
