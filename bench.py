@@ -215,6 +215,17 @@ def progress(rank, msg):
         print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
+def guarded(rank, name, fn):
+    """A secondary leg (time to solution, SSORk, per-config, config 5): an error it raises on
+    every rank costs the line that leg only, recorded as {"error": ...}; the primary metric has
+    been measured before any of them runs."""
+    try:
+        return fn()
+    except (P.PnpError, RuntimeError, ValueError, KeyError, OSError) as exc:
+        progress(rank, f"{name} failed: {type(exc).__name__}: {exc}")
+        return {"error": f"{type(exc).__name__}: {exc}"}
+
+
 def barrier_sync(dist, world):
     import torch
     if torch.cuda.is_available():
@@ -888,7 +899,8 @@ def main():
     progress(rank, "time to solution: PNP Newton (ILU(0) f32 / f64, AMG)")
     nt_red = args.newton_reduction or cfg.system["newtonReduction"]
     nt_linred = args.min_linear_reduction or cfg.system["newtonMinLinearReduction"]
-    if not args.no_solve:
+
+    def tts_leg():
         barrier_sync(dist, world)
         t0 = time.perf_counter()
         # bounded (10 Newton steps) so a block-Jacobi preconditioner that converges slowly at N>1
@@ -896,37 +908,46 @@ def main():
         _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=prec,
                              linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
         barrier_sync(dist, world)
-        newton = {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
-                  "status": nres["status"], "iterations": nres["iterations"],
-                  "linear_iterations": nres["linear_iterations"],
-                  "first_defect": nres["first_defect"], "defect": nres["defect"],
-                  "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
-                  "reduction": nt_red, "min_linear_reduction": nt_linred,
-                  "preconditioner": args.prec + (
-                      ", " + {1: "f32 factors", 2: "bf16 factors",
-                              3: "bf16 factors, f32 intermediate"}.get(
-                          ctx.get_option(P.OPT_ILU_F32), "f64 factors")
-                      if prec == P.PREC_ILU0 else "")}
+        return {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
+                "status": nres["status"], "iterations": nres["iterations"],
+                "linear_iterations": nres["linear_iterations"],
+                "first_defect": nres["first_defect"], "defect": nres["defect"],
+                "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
+                "precision_retries": nres.get("precision_retries"),
+                "reduction": nt_red, "min_linear_reduction": nt_linred,
+                "preconditioner": args.prec + (
+                    ", " + {1: "f32 factors", 2: "bf16 factors",
+                            3: "bf16 factors, f32 intermediate"}.get(
+                        ctx.get_option(P.OPT_ILU_F32), "f64 factors")
+                    if prec == P.PREC_ILU0 else "")}
+    if not args.no_solve:
+        newton = guarded(rank, "time to solution", tts_leg)
     # the same with fp64 ILU(0) factors (the default stores them in single precision): the f32
     # choice's effect on time to solution, linear iterations and seconds side by side
     newton_f64 = None
-    if not args.no_solve and prec == P.PREC_ILU0:
+
+    def tts_f64_leg():
         f_default = ctx.get_option(P.OPT_ILU_F32)
         ctx.set_option(P.OPT_ILU_F32, 0)
-        barrier_sync(dist, world)
-        t0 = time.perf_counter()
-        _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=prec,
-                             linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
-        barrier_sync(dist, world)
-        newton_f64 = {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
-                      "iterations": nres["iterations"],
-                      "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
-                      "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
-                      "preconditioner": "ilu0, fp64 factors"}
-        ctx.set_option(P.OPT_ILU_F32, f_default)
+        try:
+            barrier_sync(dist, world)
+            t0 = time.perf_counter()
+            _, nres = ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=prec,
+                                 linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
+            barrier_sync(dist, world)
+        finally:
+            ctx.set_option(P.OPT_ILU_F32, f_default)
+        return {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
+                "iterations": nres["iterations"],
+                "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
+                "assemble_s": nres["assemble_seconds"], "solve_s": nres["solve_seconds"],
+                "preconditioner": "ilu0, fp64 factors"}
+    if not args.no_solve and prec == P.PREC_ILU0:
+        newton_f64 = guarded(rank, "time to solution (fp64 factors)", tts_f64_leg)
     # the same with the aggregation AMG (PNP_PREC_AMG, ILU(0) smoother) preconditioning BiCGSTAB
     newton_amg = None
-    if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
+
+    def tts_amg_leg():
         ctx.amg_configure(smoother=P.PREC_ILU0)  # defaults: omega 0.8, 2 coarse sweeps
         # warm-up (untimed): first AMG setup loads rocSOLVER's getrf/getri kernels
         ctx.newton(x0, reduction=nt_red, min_linear_reduction=nt_linred, prec=P.PREC_AMG,
@@ -937,51 +958,63 @@ def main():
                              prec=P.PREC_AMG,
                              linear_maxit=int(cfg.system["linearSolverIterations"]), maxit=10)
         barrier_sync(dist, world)
-        newton_amg = {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
-                      "status": nres["status"], "iterations": nres["iterations"],
-                      "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
-                      "linear_fallbacks": nres["linear_fallbacks"],
-                      "preconditioner": "amg (ILU0 smoother, 2 block-Jacobi sweeps omega=0.8 "
-                                        "on the coarse levels)",
-                      "amg_rows": ctx.amg_info()["rows"]}
+        return {"seconds": time.perf_counter() - t0, "converged": nres["converged"],
+                "status": nres["status"], "iterations": nres["iterations"],
+                "linear_iterations": nres["linear_iterations"], "defect": nres["defect"],
+                "linear_fallbacks": nres["linear_fallbacks"],
+                "preconditioner": "amg (ILU0 smoother, 2 block-Jacobi sweeps omega=0.8 "
+                                  "on the coarse levels)",
+                "amg_rows": ctx.amg_info()["rows"]}
+    if not args.no_solve and not args.no_amg and (world == 1 or args.amg_multi):
+        newton_amg = guarded(rank, "time to solution (AMG)", tts_amg_leg)
     ssork = None
     if not args.no_ssork:
         progress(rank, "BCGS_SSORk (natural-order SSOR)")
-        ssork = ssork_natural_leg(ctx, mesh, x0, args.bicg_iters, dist, world)
+        ssork = guarded(rank, "BCGS_SSORk",
+                        lambda: ssork_natural_leg(ctx, mesh, x0, args.bicg_iters, dist, world))
     ctx.close()
     per_config = None
     if world == 1 and not args.no_per_config:
         progress(rank, "per-config legs (configs 1, 2, 4)")
-        per_config = per_config_legs(prec)
+        per_config = guarded(rank, "per-config legs", lambda: per_config_legs(prec))
 
     # ---- config 5, one mesh split over the ranks (strong scaling of the north-star system) -----
     strong = parity = None
-    if args.scaling == "weak" and not args.no_strong:
+
+    def strong_leg():
         progress(rank, "config 5 (strong scaling)")
         scfg, smesh = strong_mesh(args.strong_refine)
         sctx, sx0, spb, s_setup = make_context(smesh, scfg, rank, world, local, dist)
-        S = measure(sctx, smesh, args, prec, dist, world)
-        if not args.no_parity:
-            progress(rank, "rccl_parity (partitioned vs one-rank Newton on config 5)")
-            parity = rccl_parity(sctx, smesh, scfg, sx0, rank, world, local, dist)
-        sctx.close()
-        strong = {"workload": f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
-                              f"natively (scale 0.85), refined k={args.strong_refine}, one mesh "
-                              f"RCB-split over {world} GPU(s)",
-                  "scaling": "strong", "dofs": S["N_global"], "dofs_per_gpu": S["N_local"],
-                  "assembled_dofs_per_s": S["dofs_per_s"],
-                  "ms_per_step": 1e3 * S["t_asm"] / args.steps,
-                  "bicgstab_iters_per_s": S["iters_per_s"],
-                  "bicgstab_ms_per_iter": 1e3 * S["t_bicg"] / (args.steps * args.bicg_iters),
-                  "roofline_assembly_warm": S["asm_warm"], "roofline_assembly_cold": S["asm_cold"],
-                  "roofline_bicgstab_stored": S["it_stored"], "spmv_stored": S["spmv_stored"],
-                  "roofline_assembly_in_situ": S["asm_situ"],
-                  "ilu0_apply_stored": S["ilu_stored"], "blas_per_iter": S["blas"],
-                  "kernels_profile": profile_bicg(5) if world == 1 else None,
-                  "colors": S["info"]["ncolors"],
-                  "ghost_vertices": S["info"]["nv_ghost"], "setup_s": s_setup,
-                  "halo_ms_per_iter": S["timers"]["halo_ms"] / args.bicg_iters,
-                  "allreduce_ms_per_iter": S["timers"]["allreduce_ms"] / args.bicg_iters}
+        try:
+            S = measure(sctx, smesh, args, prec, dist, world)
+            par = None
+            if not args.no_parity:
+                progress(rank, "rccl_parity (partitioned vs one-rank Newton on config 5)")
+                par = guarded(rank, "rccl_parity",
+                              lambda: rccl_parity(sctx, smesh, scfg, sx0, rank, world, local, dist))
+        finally:
+            sctx.close()
+        st = {"workload": f"config 5: stationary 3-ion PNP, test/pore_without_dna .geo meshed "
+                          f"natively (scale 0.85), refined k={args.strong_refine}, one mesh "
+                          f"RCB-split over {world} GPU(s)",
+              "scaling": "strong", "dofs": S["N_global"], "dofs_per_gpu": S["N_local"],
+              "assembled_dofs_per_s": S["dofs_per_s"],
+              "ms_per_step": 1e3 * S["t_asm"] / args.steps,
+              "bicgstab_iters_per_s": S["iters_per_s"],
+              "bicgstab_ms_per_iter": 1e3 * S["t_bicg"] / (args.steps * args.bicg_iters),
+              "roofline_assembly_warm": S["asm_warm"], "roofline_assembly_cold": S["asm_cold"],
+              "roofline_bicgstab_stored": S["it_stored"], "spmv_stored": S["spmv_stored"],
+              "roofline_assembly_in_situ": S["asm_situ"],
+              "ilu0_apply_stored": S["ilu_stored"], "blas_per_iter": S["blas"],
+              "kernels_profile": profile_bicg(5) if world == 1 else None,
+              "colors": S["info"]["ncolors"],
+              "ghost_vertices": S["info"]["nv_ghost"], "setup_s": s_setup,
+              "halo_ms_per_iter": S["timers"]["halo_ms"] / args.bicg_iters,
+              "allreduce_ms_per_iter": S["timers"]["allreduce_ms"] / args.bicg_iters}
+        return st, par
+    if args.scaling == "weak" and not args.no_strong:
+        res = guarded(rank, "config 5 (strong scaling)", strong_leg)
+        strong, parity = (res, None) if isinstance(res, dict) else res
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the contract: rank 0 at N=1 only

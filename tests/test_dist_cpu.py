@@ -73,3 +73,15 @@ def test_two_process_gloo_partition_and_halo():
         for p, ghosts in recv.items():
             assert everyone[p][2][r] == ghosts  # p sends r exactly r's ghosts, in order
             assert len(ghosts) > 0
+
+
+def test_guarded_leg_records_an_error_and_passes_results_through():
+    """a secondary bench leg that raises on every rank costs the line that leg only"""
+    import pnp_amd as P
+    B = _bench()
+    assert B.guarded(0, "ok", lambda: {"seconds": 1.0}) == {"seconds": 1.0}
+
+    def boom():
+        raise P.PnpError(P.E_STATE, "leg failed")
+    out = B.guarded(0, "boom", boom)
+    assert set(out) == {"error"} and "leg failed" in out["error"]
