@@ -406,12 +406,12 @@ def byte_models(info, nf, N_local, T_local, prec):
     spmv = info["nslots"] * (8 * info["nks"] + 4) + 8 * n_loc + 16 * N_local
     # ILU(0) apply: split factors (NV expanded values + index per slot), d read, forward result
     # written, re-read by the backward sweep (gathers counted once), v written
-    # bytes per block of the stored factors: float (quads + the remainder), bfloat16 (NV rounded
-    # up to 8 shorts: one 16-B record), or double; mode 3: bfloat16 factors and a 4-B forward
-    # intermediate (scalar systems run 2 and 3 as 1)
+    # bytes per block of the stored factors: float (quads + the remainder), bfloat16 (the 7-value
+    # PNP block in 14 B, linalg.hip ILU_BF16_B7; other NV rounded up to 8 shorts), or double;
+    # mode 3: bfloat16 factors and a 4-B forward intermediate (scalar systems run 2 and 3 as 1)
     nvb = info["nvb"]
     mode = info["ilu_f32"] if nvb > 1 or info["ilu_f32"] < 2 else 1
-    vb = {1: 4 * nvb, 2: 2 * (nvb if nvb == 1 else (nvb + 7) // 8 * 8)}.get(min(mode, 2), 8 * nvb)
+    vb = {1: 4 * nvb, 2: 2 * (nvb if nvb in (1, 7) else (nvb + 7) // 8 * 8)}.get(min(mode, 2), 8 * nvb)
     yb = 4 if mode == 3 else 8
     ilu = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * N_local + (2 * yb + 8) * n_loc
     if mode == 1 and nvb == 7:

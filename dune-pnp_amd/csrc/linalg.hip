@@ -444,12 +444,27 @@ __device__ __forceinline__ void load_f32_slot(const float *__restrict__ sb, int 
 // (nearest even), fp64 arithmetic as before.  Slots of NV > 1 values hold NV rounded up to 8
 // shorts per lane, so one dwordx4 per lane moves a PNP block (16 B instead of 28): value q of
 // lane l at (q >> 3) * 8 * kRows + 8 l + (q & 7); NV == 1 is row-contiguous (2 B per row).
+// ILU_BF16_B7 (default): the 7-value stationary PNP block in 14 B instead of 16 -- six shorts per
+// lane (one dwordx3) then one short per lane (a 128-B plane) -- with the two strictly lower
+// values of the pattern, (1,0) and (2,0), in the dwordx3's last dword: a forward step reads only
+// that dword of a diagonal block (4 B instead of 16).  Same values, same arithmetic: bitwise the
+// 16-B layout's results.
 // Measured first with f32 storage rounded to 8 / 11 bits (ILU_ROUND_BITS): the config-3 PNP
 // Newton's BiCGSTAB count stays inside its last-bit spread.
+#ifndef ILU_BF16_B7
+#define ILU_BF16_B7 1
+#endif
 typedef unsigned short bf16s;
-__host__ __device__ constexpr int nvp_b(int nv) { return nv == 1 ? 1 : ((nv + 7) & ~7); }
+__host__ __device__ constexpr bool b7(int nv) { return ILU_BF16_B7 && nv == 7; }
+__host__ __device__ constexpr int nvp_b(int nv) { return nv == 1 ? 1 : b7(nv) ? 7 : ((nv + 7) & ~7); }
+// b7 position of value q: (0,0) (0,1) (0,2) (1,1) | (1,0) (2,0) in the third dword | (2,2) apart
+__host__ __device__ constexpr int bperm7(int q) {
+  return q == 3 ? 4 : q == 4 ? 3 : q;  // q 5 -> 5, q 6 -> 6
+}
 __host__ __device__ constexpr int vinb(int nv, int q, int lane) {
-  return nv == 1 ? lane : (q >> 3) * 8 * kRows + 8 * lane + (q & 7);
+  return nv == 1 ? lane
+         : b7(nv) ? (bperm7(q) < 6 ? 6 * lane + bperm7(q) : 6 * kRows + lane)
+                  : (q >> 3) * 8 * kRows + 8 * lane + (q & 7);
 }
 __device__ __forceinline__ bf16s to_bf16(float x) {
   unsigned u = __float_as_uint(x);
@@ -457,10 +472,35 @@ __device__ __forceinline__ bf16s to_bf16(float x) {
   return bf16s(u >> 16);
 }
 __device__ __forceinline__ float from_bf16(unsigned h) { return __uint_as_float(h << 16); }
-template <int NV, int NT, typename T = double>
+// LOWER (b7 only): just the dword of the two strictly lower values, the others zero
+template <int NV, int NT, typename T = double, int LOWER = 0>
 __device__ __forceinline__ void load_bf16_slot(const bf16s *__restrict__ sb, int lane, T *B) {
   if constexpr (NV == 1) {
     B[0] = T(from_bf16(NT ? __builtin_nontemporal_load(sb + lane) : sb[lane]));
+  } else if constexpr (b7(NV)) {
+    const unsigned *pw = reinterpret_cast<const unsigned *>(sb) + 3 * lane;
+    auto lo = [](unsigned w) { return from_bf16(w & 0xFFFFu); };
+    auto hi = [](unsigned w) { return from_bf16(w >> 16); };
+    if constexpr (LOWER) {
+      const unsigned w2 = NT ? __builtin_nontemporal_load(pw + 2) : pw[2];
+#pragma unroll
+      for (int q = 0; q < 7; q++) B[q] = T(0);
+      B[3] = T(lo(w2));
+      B[5] = T(hi(w2));
+    } else {
+      typedef unsigned u3v __attribute__((ext_vector_type(3)));
+      const u3v t = NT ? __builtin_nontemporal_load(reinterpret_cast<const u3v *>(pw))
+                       : *reinterpret_cast<const u3v *>(pw);
+      const unsigned short t6 = NT ? __builtin_nontemporal_load(sb + 6 * kRows + lane)
+                                   : sb[6 * kRows + lane];
+      B[0] = T(lo(t[0]));
+      B[1] = T(hi(t[0]));
+      B[2] = T(lo(t[1]));
+      B[4] = T(hi(t[1]));  // position 3
+      B[3] = T(lo(t[2]));  // position 4
+      B[5] = T(hi(t[2]));
+      B[6] = T(from_bf16(t6));
+    }
   } else {
     typedef unsigned u4v __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -491,7 +531,7 @@ __device__ __forceinline__ void load_split_vals(const VT *__restrict__ sb, int l
     else
       load_vals<NV>(sb, lane, B);
   } else if constexpr (std::is_same<VT, bf16s>::value) {
-    load_bf16_slot<NV, NT, double>(sb, lane, B);
+    load_bf16_slot<NV, NT, double, LOWER>(sb, lane, B);
   } else if constexpr (NV == 1) {
     B[0] = NT ? __builtin_nontemporal_load(sb + lane) : sb[lane];
   } else {

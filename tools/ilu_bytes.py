@@ -3,8 +3,9 @@ reads and writes, from the layout's own counts (pnp_info: live split slots, stag
 against bench.py's stored-format model -- to say what the counted traffic
 (profiles/r06/pmc_summary.json) is made of.  Per application (colour 0's forward step runs in the
 BiCGSTAB update, outside these launches):
-  factors      every live L / U slot's 16-B bf16 record (U: the diagonal block too), plus the
-               diagonal block read again by each forward launch (16 B per row outside colour 0)
+  factors      every live L / U slot's bf16 record (U: the diagonal block too), 14 B for the
+               7-value PNP block (16 B before ILU_BF16_B7), plus the diagonal block's lower pair
+               read again by each forward launch (4 B per row; 16 B before)
   positions    the 2-B list position of every live off-diagonal slot
   staging      every staged list entry: its 4-B row index and the 24-B record it gathers
   rows         d read (24 B) and y written (24 B) per forward row outside colour 0; y re-read
@@ -42,12 +43,13 @@ def main():
         # colour sizes are not in pnp_info; colour 0 and the last colour are bounded by the
         # row count, so the row terms are given for "all rows" and noted as an upper bound
         Ls, Us = info["lslots_live"], info["uslots_live"]
-        factors = 16 * (Ls + Us) + 16 * rows
+        nvb = info["nvb"]
+        rec_b = 14 if nvb == 7 else 2 * ((nvb + 7) // 8 * 8)  # bf16 bytes per block
+        factors = rec_b * (Ls + Us) + (4 if nvb == 7 else rec_b) * rows
         positions = 2 * (Ls + Us - rows)
         staging = (4 + rec) * (info["lsx_entries"] + info["usx_entries"])
         row_terms = 4 * rec * rows
-        nvb = info["nvb"]
-        vb = 2 * ((nvb + 7) // 8 * 8)
+        vb = 2 * (nvb if nvb == 7 else (nvb + 7) // 8 * 8)
         model = (info["lslots"] + info["uslots"]) * (vb + 4) + 8 * nf * rows + 24 * nf * rows
         out = {"config": c, "rows": rows, "lslots_live": Ls, "uslots_live": Us,
                "lslots_stored": info["lslots"], "uslots_stored": info["uslots"],
