@@ -151,8 +151,8 @@ struct pnp_ctx {
   // sweeps compute in fp64, the matrix, SpMV, SSOR and every vector stay fp64).  Measured at
   // config 3: ILU(0) apply 119 -> 95 us, BiCGSTAB 428 -> 389 us/it, Newton 9,295 -> 9,177
   // iterations (profiles/r02/ab_ilu_f32.log)
-  // 2 (the default since round 5): bfloat16 factors for block systems (linalg.hip bf16s: 16 B per
-  // PNP block instead of 28; ILU(0) apply 66.3 -> 58.6 us, BiCGSTAB 0.285 -> 0.270 ms per
+  // 2 (the default since round 5): bfloat16 factors for block systems (linalg.hip bf16s: 14 B per
+  // PNP block instead of 28 -- 16 B until ILU_BF16_B7; ILU(0) apply 66.3 -> 58.6 us, BiCGSTAB 0.285 -> 0.270 ms per
   // iteration at config 3, Newton counts inside their last-bit spread); scalar
   // systems (PB, Poisson, diffusion: one value per block, 2 B saved per slot) keep f32, where the
   // PB Newton at config 1 took 13 % more iterations with bf16

@@ -362,7 +362,7 @@ enum {
    * sweeps compute in fp64 whatever it is.  The matrix, the SpMV, SSOR/Jacobi and every vector stay
    * fp64, so the operator and the converged solutions are those of the fp64 path; only the
    * preconditioner is a rounded ILU(0).  2 (default): bfloat16 factors for block systems (8
-   * significant bits, 16 B per PNP block instead of 28; config 3: apply 66 -> 59 us, Newton counts
+   * significant bits, 14 B per PNP block instead of 28; config 3: apply 66 -> 57 us, Newton counts
    * within their last-bit spread).  3 (opt-in): the factors of 2, and the forward sweep's
    * intermediate L^-1 d kept in single precision between the colour launches (12 B per PNP row
    * instead of 24; apply -1.8 us at config 3); the rounding makes the preconditioner nonlinear,
