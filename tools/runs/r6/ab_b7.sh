@@ -2,6 +2,7 @@
 # round 6: the 14-B bfloat16 PNP block record (ILU_BF16_B7, in-tree default) against the 16-B one
 # (dune-pnp_amd/ab/lib_b16.so): the full GPU suite, bit-for-bit hashes of both, then
 # tools/time_bicg.py at configs 3 and 5, interleaved three times
+# the A/B lib first: tools/build_ab.sh b16 "-DILU_BF16_B7=0" (the 14-B layout is the default)
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_b7.log"
 fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }

@@ -2,6 +2,7 @@
 # round 6: colour 1 of the second half step's forward sweep inside the BiCGSTAB update (PNP_FUSE1,
 # default on) against its own colour launch: bit-for-bit hashes, the ILU variant tests, then
 # tools/time_bicg.py at configs 3 and 5 interleaved three times, then the full GPU suite
+# record: the colour-1 fusion (PNP_FUSE1) was reverted after this A/B
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_fuse1.log"
 fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }

@@ -2,6 +2,8 @@
 # round 6: non-temporal vector stores in the BiCGSTAB kernels (VEC_NT, in-tree)
 # against plain stores (dune-pnp_amd/ab/lib_plain.so): bit-for-bit hashes, tools/time_bicg.py at
 # configs 3 and 5 interleaved three times, the in-situ assembly probe, then the full GPU suite
+# record: the non-temporal stores (VEC_NT; A/B lib: tools/build_ab.sh plain -DVEC_NT=0) were
+# reverted after this A/B
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_nt.log"
 fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }

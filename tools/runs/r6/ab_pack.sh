@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 6: packed ILU(0) row metadata (PNP_ILU_PACK, default on) against the byte arrays, the
 # ILU LDS variant tests first, then tools/time_bicg.py at configs 3 and 5, interleaved three times
+# record: the packed-metadata variant (PNP_ILU_PACK) was reverted after this A/B
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_pack.log"
 fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }

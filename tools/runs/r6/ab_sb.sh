@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 6: the partition edge-case tests, then the LDS SpMV's four-slot step (PNP_SPMV_LDS_SB=4)
 # against the pairs: bitwise test, then tools/time_bicg.py at configs 3 and 5, interleaved 3 times
+# record: the four-slot SpMV step (PNP_SPMV_LDS_SB) was reverted after this A/B
 set -u
 OUT=gpurun_out/$1; mkdir -p "$OUT"; : > "$OUT/ab_sb.log"
 fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
