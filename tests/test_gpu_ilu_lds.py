@@ -82,3 +82,24 @@ def test_sweep_variants_are_bitwise_equal():
         assert run(PNP_ILU_LDS_B=b) == ref, b
     assert run(PNP_SPLIT_SORT=0) == ref
     assert run(PNP_SPLIT_SORT=0, PNP_ILU_LDS=0) == ref
+
+
+def test_layout_counts_in_pnp_info():
+    """pnp_info's split-storage counts (tools/ilu_bytes.py reads them): every owned coupling of two
+    colours is one live L or U slot, the diagonal one U slot per row, same-colour pairs none; each
+    staged list entry serves at least one live off-diagonal slot"""
+    import conftest  # noqa: F401
+    import pnp_amd as P
+    from test_gpu import golden
+    for name in ("pore_small_k0", "cylinder_k0"):
+        z, mesh, par, orc = golden(name)
+        ctx = P.Context(mesh, par)
+        ctx.set_operator(P.OP_PNP)
+        info = ctx.info()
+        ctx.close()
+        rows = info["nv_owned"]
+        assert info["lslots_live"] + info["uslots_live"] + 2 * info["color_conflicts"] == \
+            info["nblocks"], info
+        assert info["lslots_live"] <= info["lslots"] and info["uslots_live"] <= info["uslots"]
+        assert 0 < info["lsx_entries"] <= info["lslots_live"]
+        assert 0 < info["usx_entries"] <= info["uslots_live"] - rows
